@@ -1,0 +1,159 @@
+/*
+ * kanode.h — C-ABI of the MI355X-native KAN-ODE right-hand side and its VJP.
+ *
+ * This is the drop-in boundary for the reference's hot path.  A
+ * host (the Julia `ccall` shim in INTEGRATION.md, or the Python harness in
+ * kan-odes_amd/kanode) binds exactly these entry points.  Plain C: integer status
+ * codes, plain pointers and sizes, no exceptions across the ABI.
+ *
+ * Reference interfaces replaced (file:line relative to /root/reference):
+ *   kanode_create / kanode_param_length / kanode_knots
+ *       KDense ctor + LuxCore.initialparameters/initialstates/parameterlength/statelength
+ *       Lotka-Volterra/src/kdense.jl:20-107 (PDE copy: PDE examples/src/kdense.jl:20-107)
+ *   kanode_layer_forward
+ *       (l::KDense)(x, p, st) -> (y, st)                     Lotka-Volterra/src/kdense.jl:109-130
+ *   kanode_layer_vjp
+ *       Zygote pullback of the above incl. rrule(_rbf)        Lotka-Volterra/src/utils.jl:15-21
+ *   kanode_rhs  (rhs_kind = CHAIN)
+ *       NeuralODE dudt(u,p,t) = first(Chain(u, p, st))      Lotka-Volterra/LV_driver_KANODE.jl:139-143,180
+ *                                                           PDE examples/Burgers_Surrogate.jl:85-97,
+ *                                                           PDE examples/Schrodinger_Surrogate.jl:93-104
+ *   kanode_rhs  (rhs_kind = POINTWISE_PERIODIC_LAPLACIAN)
+ *       rc_kanode(u,p,t) = D*lap*u + kan1_.(u)              PDE examples/Fisher-KPP_Source.jl:55-59,95-98
+ *   kanode_vjp
+ *       the RHS pullback SciMLSensitivity requests per adjoint stage (λᵀ∂f/∂u, λᵀ∂f/∂p)
+ *   kanode_edge_activations
+ *       per-edge activations                                 Lotka-Volterra/Activation_getter.jl:3-63
+ *
+ * Layout: the reference's Julia column-major arrays.  A state / layer input is
+ * [N, B] with element (n, b) at n + N*b (one trajectory contiguous).  The flat
+ * parameter vector p is the ComponentArray order of the Lux chain:
+ * layer_1.C [O,G*I] col-major, layer_1.W [O,I], layer_2.C, ... (kdense.jl:70-86,
+ * LV_driver_KANODE.jl:173-175) — the same vector the reference stores in `.mat`
+ * p_list rows.
+ *
+ * Ownership / threading: the caller owns every buffer passed in.  Device
+ * variants take DEVICE pointers and are asynchronous on `stream` (a hipStream_t,
+ * NULL = default stream); they never allocate once kanode_reserve() covered the
+ * batch, so they can be captured into a hipGraph.  *_host variants take host
+ * pointers, stage through handle-owned device buffers and return after the
+ * stream synchronises.  A handle is bound to one device, is NOT thread-safe,
+ * and separate handles are independent.  `dp`/`pbar` ACCUMULATE (+=): the adjoint
+ * integrates μ across stages, so zeroing is the caller's job.
+ */
+#ifndef KANODE_H
+#define KANODE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KANODE_ABI_VERSION 1
+#define KANODE_MAX_LAYERS 8
+#define KANODE_MAX_GRID 32
+
+typedef enum {
+    KANODE_OK = 0,
+    KANODE_ERR_INVALID_ARG = 1,
+    KANODE_ERR_UNSUPPORTED = 2,
+    KANODE_ERR_HIP = 3,
+    KANODE_ERR_ALLOC = 4,
+    KANODE_ERR_CAPTURE = 5 /* would need to allocate during stream capture: call kanode_reserve first */
+} kanode_status;
+
+typedef enum { KANODE_F32 = 0, KANODE_F64 = 1 } kanode_dtype;
+
+/* normalizer (kdense.jl:25,57-61; NNlib.fast_act maps tanh -> tanh_fast when
+ * allow_fast_activation, the reference default) */
+typedef enum {
+    KANODE_NORM_TANH_FAST = 0,
+    KANODE_NORM_TANH = 1,
+    KANODE_NORM_SOFTSIGN = 2,
+    KANODE_NORM_SIGMOID = 3,
+    KANODE_NORM_SIGMOID_FAST = 4,
+    KANODE_NORM_IDENTITY = 5
+} kanode_normalizer;
+
+/* basis_func (utils.jl:8-62) */
+typedef enum { KANODE_BASIS_RBF = 0, KANODE_BASIS_RSWAF = 1, KANODE_BASIS_IQF = 2 } kanode_basis;
+
+typedef enum {
+    KANODE_RHS_CHAIN = 0,                        /* du = Chain(u)                           */
+    KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN = 1  /* du = D*lap*u + KDense(1,1,G).(u)        */
+} kanode_rhs_kind;
+
+/* One KDense layer (kdense.jl:20-37). */
+typedef struct {
+    int32_t in_dims;
+    int32_t out_dims;
+    int32_t grid_len;               /* G, 2 <= G <= KANODE_MAX_GRID */
+    int32_t normalizer;             /* kanode_normalizer */
+    int32_t basis;                  /* kanode_basis */
+    int32_t use_base_act;           /* 1: y += W * swish.(x) */
+    float grid_lo, grid_hi;         /* grid_lims, Float32 (default -1f0, 1f0) */
+    float denominator;              /* <= 0: Float32(2/(G-1)) (kdense.jl:27) */
+    int32_t iqf_reference_quirk;    /* 1: IQF pullback exactly as utils.jl:59 */
+} kanode_layer_spec;
+
+typedef struct {
+    int32_t n_layers;
+    kanode_layer_spec layers[KANODE_MAX_LAYERS];
+    int32_t dtype;                  /* kanode_dtype of u, p and every output */
+    int32_t rhs_kind;               /* kanode_rhs_kind */
+    /* POINTWISE_PERIODIC_LAPLACIAN only: state [nx, B], one [1,1] layer */
+    int64_t nx;
+    double diffusion;               /* D (Fisher-KPP_Source.jl:34) */
+    double dx;                      /* grid spacing (lap = tridiag(1,-2,1)/dx^2 + periodic corners) */
+    int32_t device;                 /* HIP device ordinal */
+} kanode_spec;
+
+typedef struct kanode_handle kanode_handle;
+
+/* --- lifecycle ------------------------------------------------------------- */
+kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out);
+void kanode_destroy(kanode_handle* h);
+const char* kanode_last_error(const kanode_handle* h);   /* message of the last failure on h */
+const char* kanode_status_string(kanode_status s);
+int32_t kanode_abi_version(void);
+
+/* --- introspection (LuxCore.parameterlength / statelength / initialstates) -- */
+int64_t kanode_param_length(const kanode_handle* h);     /* whole chain */
+int64_t kanode_layer_param_length(const kanode_handle* h, int32_t layer);
+int64_t kanode_state_length(const kanode_handle* h);     /* N of the [N, B] state */
+kanode_status kanode_knots(const kanode_handle* h, int32_t layer, float* grid_out /* [G] host */);
+
+/* Pre-size handle workspaces for batches up to max_batch (no allocation in later
+ * device calls with batch <= max_batch; required before hipGraph capture). */
+kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
+
+/* --- the RHS and its VJP (device pointers, async on stream) ----------------- */
+/* du[N,B] = f(u[N,B]; p) */
+kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch, void* stream);
+/* lam_J[N,B] = (∂f/∂u)ᵀ lam   (nullable: skip)
+ * dp[P]     += Σ_b (∂f/∂p)ᵀ lam  (nullable: skip) */
+kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,
+                         int64_t batch, void* stream);
+
+/* host-pointer variants (synchronous) */
+kanode_status kanode_rhs_host(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch);
+kanode_status kanode_vjp_host(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J,
+                              void* dp, int64_t batch);
+
+/* --- single-layer entry points (one Lux KDense call) ------------------------ */
+/* y[O,K] = KDense_layer(x[I,K]; p_layer)  (p_layer = that layer's (C, W) slice) */
+kanode_status kanode_layer_forward(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, void* y,
+                                   int64_t K, void* stream);
+/* xbar[I,K] = pullback(ybar)  (nullable); pbar_layer[P_l] += ... (nullable) */
+kanode_status kanode_layer_vjp(kanode_handle* h, int32_t layer, const void* p_layer, const void* x,
+                               const void* ybar, void* xbar, void* pbar_layer, int64_t K, void* stream);
+/* act[O, I, K] with act(o,i,k) = Σ_g C[o,g+G i] φ_g(x[i,k]) + W[o,i] swish(x[i,k])
+ * (Σ_i act(o,i,k) == y(o,k): the Activation_getter.jl:33-36,55-61 identity) */
+kanode_status kanode_edge_activations(kanode_handle* h, int32_t layer, const void* p_layer, const void* x,
+                                      void* act, int64_t K, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KANODE_H */

@@ -1,0 +1,29 @@
+// kan_kernels.hpp — internal launcher declarations (C++ linkage, not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kan_device.hpp"
+
+namespace kan {
+
+// `hlc` is the host copy of the layer constants (selects the kernel variant),
+// `lc` the device copy the kernels read.  All pointers are device pointers.
+template <typename T>
+hipError_t launch_fk_rhs(const LayerConst& hlc, const LayerConst* lc, const T* p, T cd, T co, int Nx,
+                         const T* u, T* du, int64_t B, hipStream_t st);
+template <typename T>
+hipError_t launch_fk_vjp(const LayerConst& hlc, const LayerConst* lc, const T* p, T cd, T co, int Nx,
+                         const T* u, const T* lam, T* lamJ, T* dp, T* slab, int slab_blocks, int64_t B,
+                         hipStream_t st);
+template <typename T>
+hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
+                             hipStream_t st);
+template <typename T>
+hipError_t launch_kd_vjp_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb,
+                             T* xb, T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st);
+template <typename T>
+hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* act, int64_t K,
+                              hipStream_t st);
+
+}  // namespace kan

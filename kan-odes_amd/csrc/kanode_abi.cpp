@@ -1,0 +1,534 @@
+// kanode_abi.cpp — the C-ABI (include/kanode.h) over the HIP kernels.
+//
+// Host-side responsibilities: validate the spec exactly as the reference ctor
+// would accept it (kdense.jl:20-68), precompute the per-layer constants the
+// kernels read (knots with Julia LinRange semantics, Float32 1/h, recurrence
+// constants), own the device workspaces, and dispatch each layer to its kernel.
+// No C++ exception crosses the ABI: every entry point returns a kanode_status.
+#include "kanode.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "kan_device.hpp"
+#include "kan_kernels.hpp"
+
+using kan::LayerConst;
+
+namespace {
+
+constexpr int kSlabBlocks = 2048;   // grid cap of the VJP kernels = slab rows
+
+enum LayerKind { KIND_COL = 0 };
+
+}  // namespace
+
+struct kanode_handle {
+    kanode_spec spec{};
+    int n_layers = 0;
+    LayerConst hlc[KANODE_MAX_LAYERS];
+    LayerKind kind[KANODE_MAX_LAYERS];
+    LayerConst* dlc = nullptr;        // device copy
+    int64_t P = 0;
+    int64_t n_in = 0, n_out = 0;      // state length (input / output of the RHS)
+    size_t esize = 8;
+    int max_layer_P = 0;
+    int max_dim = 0;
+    // workspaces (device)
+    void* slab = nullptr;
+    size_t slab_bytes = 0;
+    void* ws = nullptr;               // chain activations / gradients
+    size_t ws_bytes = 0;
+    int64_t reserved_batch = 0;
+    // host staging (device buffers) for *_host calls
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    std::string err;
+};
+
+namespace {
+
+kanode_status fail(kanode_handle* h, kanode_status s, const std::string& msg) {
+    if (h) h->err = msg;
+    return s;
+}
+
+#define HIP_TRY(h, expr)                                                                         \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail((h), KANODE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// Julia LinRange{Float32}(a, b, G)[j] = Float32((1-t)*a + t*b), t = j/(G-1) in Float64.
+void knots_linrange(float lo, float hi, int G, float* out) {
+    const double a = (double)lo, b = (double)hi;
+    for (int j = 0; j < G; ++j) {
+        const double t = (double)j / (double)(G - 1);
+        out[j] = (float)((1.0 - t) * a + t * b);
+    }
+}
+
+bool norm_range(int norm, double& lo, double& hi) {
+    switch (norm) {
+    case KANODE_NORM_TANH_FAST:
+    case KANODE_NORM_TANH:
+    case KANODE_NORM_SOFTSIGN: lo = -1.0; hi = 1.0; return true;
+    case KANODE_NORM_SIGMOID:
+    case KANODE_NORM_SIGMOID_FAST: lo = 0.0; hi = 1.0; return true;
+    default: return false;   // identity: unbounded
+    }
+}
+
+// Host-side layer constants (see kan_device.hpp for the recurrence).
+kanode_status make_layer_const(kanode_handle* h, const kanode_layer_spec& s, int dtype, int64_t p_off,
+                               LayerConst& lc) {
+    std::memset(&lc, 0, sizeof(lc));
+    if (s.in_dims < 1 || s.out_dims < 1)
+        return fail(h, KANODE_ERR_INVALID_ARG, "in_dims and out_dims must be >= 1");
+    if (s.grid_len < 2 || s.grid_len > KANODE_MAX_GRID)
+        return fail(h, KANODE_ERR_UNSUPPORTED, "grid_len must be in [2, " + std::to_string(KANODE_MAX_GRID) + "]");
+    if (s.normalizer < 0 || s.normalizer > KANODE_NORM_IDENTITY)
+        return fail(h, KANODE_ERR_INVALID_ARG, "unknown normalizer");
+    if (s.basis < 0 || s.basis > KANODE_BASIS_IQF) return fail(h, KANODE_ERR_INVALID_ARG, "unknown basis");
+    if (!(s.grid_hi > s.grid_lo)) return fail(h, KANODE_ERR_INVALID_ARG, "grid_lims must satisfy lo < hi");
+    lc.I = s.in_dims;
+    lc.O = s.out_dims;
+    lc.G = s.grid_len;
+    lc.norm = s.normalizer;
+    lc.basis = s.basis;
+    lc.use_base = s.use_base_act ? 1 : 0;
+    lc.iqf_quirk = s.iqf_reference_quirk ? 1 : 0;
+    lc.p_off = p_off;
+    lc.w_off = p_off + (int64_t)lc.O * lc.G * lc.I;
+    knots_linrange(s.grid_lo, s.grid_hi, lc.G, lc.grid);
+    volatile float den = s.denominator > 0.f ? s.denominator : (float)(2.0 / (double)(lc.G - 1));
+    volatile float one = 1.0f;
+    lc.invh = one / den;   // Float32 1/h (utils.jl:9)
+    const double sd = (double)lc.invh;
+    lc.g0 = (double)lc.grid[0];
+    lc.s = sd;
+    lc.delta = ((double)s.grid_hi - (double)s.grid_lo) * sd / (double)(lc.G - 1);
+    double emax = 0.0;
+    bool exact = true;
+    for (int j = 0; j < lc.G; ++j) {
+        const double D = ((double)lc.grid[j] - (double)lc.grid[0]) * sd;
+        lc.Dl[j] = D;
+        lc.e[j] = D - (double)j * lc.delta;
+        lc.K[j] = (double)std::exp(-(long double)D * (long double)D);
+        emax = std::max(emax, std::fabs(lc.e[j]));
+        if (lc.e[j] != 0.0) exact = false;
+    }
+    // recurrence admissibility: bounded normalizer, no overflow of exp(-z0²) or
+    // R^(G-1), and a 2nd-order Taylor correction that is exact to < 1 ulp.
+    lc.path = kan::PATH_DIRECT;
+    double nlo, nhi;
+    if (lc.basis == KANODE_BASIS_RBF && norm_range(lc.norm, nlo, nhi)) {
+        const double zmax = std::max(std::fabs((nlo - lc.g0) * sd), std::fabs((nhi - lc.g0) * sd));
+        const double lim = (dtype == KANODE_F64) ? 600.0 : 80.0;
+        const double tmax = 2.0 * zmax * emax;
+        const bool ok = zmax * zmax <= lim && 2.0 * zmax * std::fabs(lc.delta) * (lc.G - 1) <= lim &&
+                        lc.delta > 0.0 && (dtype == KANODE_F64 ? tmax <= 1e-5 : tmax <= 1e-3);
+        if (ok) lc.path = exact ? kan::PATH_REC : kan::PATH_REC_CORR;
+    }
+    return KANODE_OK;
+}
+
+int64_t layer_P(const LayerConst& lc) {
+    return (int64_t)lc.O * lc.G * lc.I + (lc.use_base ? (int64_t)lc.O * lc.I : 0);
+}
+
+bool is_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return false;
+    return cs != hipStreamCaptureStatusNone;
+}
+
+// Chain workspace: every hidden layer's activations (kept for the VJP) + two
+// gradient ping-pong buffers of the widest layer.
+size_t chain_ws_bytes(const kanode_handle* h, int64_t B) {
+    int64_t elems = 0;
+    for (int l = 1; l < h->n_layers; ++l) elems += (int64_t)h->hlc[l].I * B;
+    elems += 2 * (int64_t)h->max_dim * B;
+    return (size_t)elems * h->esize;
+}
+
+kanode_status ensure_ws(kanode_handle* h, int64_t B, hipStream_t st) {
+    const size_t need = h->spec.rhs_kind == KANODE_RHS_CHAIN ? chain_ws_bytes(h, B) : 0;
+    if (need <= h->ws_bytes) return KANODE_OK;
+    if (is_capturing(st))
+        return fail(h, KANODE_ERR_CAPTURE, "batch exceeds reserved workspace during stream capture; call kanode_reserve");
+    HIP_TRY(h, hipStreamSynchronize(st));
+    if (h->ws) HIP_TRY(h, hipFree(h->ws));
+    h->ws = nullptr;
+    h->ws_bytes = 0;
+    HIP_TRY(h, hipMalloc(&h->ws, need));
+    h->ws_bytes = need;
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status layer_fwd_t(kanode_handle* h, int l, const T* p_full, const T* x, T* y, int64_t K, hipStream_t st) {
+    const LayerConst& hl = h->hlc[l];
+    switch (h->kind[l]) {
+    case KIND_COL:
+        HIP_TRY(h, kan::launch_kd_fwd_col<T>(hl, h->dlc + l, p_full, x, y, K, st));
+        return KANODE_OK;
+    }
+    return fail(h, KANODE_ERR_UNSUPPORTED, "layer kind");
+}
+
+template <typename T>
+kanode_status layer_vjp_t(kanode_handle* h, int l, const T* p_full, const T* x, const T* yb, T* xb, T* pbar_full,
+                          int64_t K, hipStream_t st) {
+    const LayerConst& hl = h->hlc[l];
+    switch (h->kind[l]) {
+    case KIND_COL:
+        HIP_TRY(h, kan::launch_kd_vjp_col<T>(hl, h->dlc + l, p_full, x, yb, xb, pbar_full, (T*)h->slab, kSlabBlocks,
+                                             K, st));
+        return KANODE_OK;
+    }
+    return fail(h, KANODE_ERR_UNSUPPORTED, "layer kind");
+}
+
+template <typename T>
+kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, hipStream_t st) {
+    if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
+        const double dx2 = h->spec.dx * h->spec.dx;
+        const T cd = (T)(h->spec.diffusion * (-2.0 / dx2)), co = (T)(h->spec.diffusion * (1.0 / dx2));
+        HIP_TRY(h, kan::launch_fk_rhs<T>(h->hlc[0], h->dlc, p, cd, co, (int)h->spec.nx, u, du, B, st));
+        return KANODE_OK;
+    }
+    kanode_status s = ensure_ws(h, B, st);
+    if (s != KANODE_OK) return s;
+    T* ws = (T*)h->ws;
+    const T* cur = u;
+    T* ping = ws + (h->ws_bytes / h->esize) - 2 * (int64_t)h->max_dim * B;
+    for (int l = 0; l < h->n_layers; ++l) {
+        T* out = (l == h->n_layers - 1) ? du : ping + (l % 2) * (int64_t)h->max_dim * B;
+        s = layer_fwd_t<T>(h, l, p, cur, out, B, st);
+        if (s != KANODE_OK) return s;
+        cur = out;
+    }
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* lamJ, T* dp, int64_t B,
+                    hipStream_t st) {
+    if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
+        const double dx2 = h->spec.dx * h->spec.dx;
+        const T cd = (T)(h->spec.diffusion * (-2.0 / dx2)), co = (T)(h->spec.diffusion * (1.0 / dx2));
+        // lam_J is needed for the kernel's store; use workspace when the caller passes NULL
+        T* out = lamJ;
+        if (!out) {
+            kanode_status s = ensure_ws(h, B, st);
+            if (s != KANODE_OK) return s;
+            if (h->ws_bytes < (size_t)(h->spec.nx * B) * h->esize) {
+                if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "workspace too small during capture");
+                HIP_TRY(h, hipStreamSynchronize(st));
+                if (h->ws) HIP_TRY(h, hipFree(h->ws));
+                HIP_TRY(h, hipMalloc(&h->ws, (size_t)(h->spec.nx * B) * h->esize));
+                h->ws_bytes = (size_t)(h->spec.nx * B) * h->esize;
+            }
+            out = (T*)h->ws;
+        }
+        HIP_TRY(h, kan::launch_fk_vjp<T>(h->hlc[0], h->dlc, p, cd, co, (int)h->spec.nx, u, lam, out, dp, (T*)h->slab,
+                                         kSlabBlocks, B, st));
+        return KANODE_OK;
+    }
+    kanode_status s = ensure_ws(h, B, st);
+    if (s != KANODE_OK) return s;
+    T* ws = (T*)h->ws;
+    // forward recompute, keeping every hidden layer's input
+    const T* acts[KANODE_MAX_LAYERS];
+    acts[0] = u;
+    T* wp = ws;
+    for (int l = 1; l < h->n_layers; ++l) {
+        T* out = wp;
+        wp += (int64_t)h->hlc[l].I * B;
+        s = layer_fwd_t<T>(h, l - 1, p, acts[l - 1], out, B, st);
+        if (s != KANODE_OK) return s;
+        acts[l] = out;
+    }
+    T* g0 = wp;
+    T* g1 = wp + (int64_t)h->max_dim * B;
+    const T* g = lam;
+    for (int l = h->n_layers - 1; l >= 0; --l) {
+        T* out = (l == 0) ? lamJ : ((l % 2) ? g0 : g1);
+        if (l == 0 && !out) out = (g == g0) ? g1 : g0;   // caller skipped lam_J
+        s = layer_vjp_t<T>(h, l, p, acts[l], g, out, dp, B, st);
+        if (s != KANODE_OK) return s;
+        g = out;
+    }
+    return KANODE_OK;
+}
+
+kanode_status check_handle(kanode_handle* h) {
+    if (!h) return KANODE_ERR_INVALID_ARG;
+    hipError_t e = hipSetDevice(h->spec.device);
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    return KANODE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t kanode_abi_version(void) { return KANODE_ABI_VERSION; }
+
+const char* kanode_status_string(kanode_status s) {
+    switch (s) {
+    case KANODE_OK: return "ok";
+    case KANODE_ERR_INVALID_ARG: return "invalid argument";
+    case KANODE_ERR_UNSUPPORTED: return "unsupported configuration";
+    case KANODE_ERR_HIP: return "HIP runtime error";
+    case KANODE_ERR_ALLOC: return "allocation failure";
+    case KANODE_ERR_CAPTURE: return "allocation needed during stream capture";
+    }
+    return "unknown status";
+}
+
+const char* kanode_last_error(const kanode_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
+    if (!spec || !out) return KANODE_ERR_INVALID_ARG;
+    *out = nullptr;
+    kanode_handle* h = new (std::nothrow) kanode_handle();
+    if (!h) return KANODE_ERR_ALLOC;
+    h->spec = *spec;
+    auto bail = [&](kanode_status s) {
+        // keep the handle so the caller can read kanode_last_error, then destroy
+        *out = h;
+        return s;
+    };
+    if (spec->dtype != KANODE_F32 && spec->dtype != KANODE_F64)
+        return bail(fail(h, KANODE_ERR_INVALID_ARG, "dtype must be KANODE_F32 or KANODE_F64"));
+    h->esize = spec->dtype == KANODE_F64 ? 8 : 4;
+    if (spec->n_layers < 1 || spec->n_layers > KANODE_MAX_LAYERS)
+        return bail(fail(h, KANODE_ERR_INVALID_ARG, "n_layers must be in [1, 8]"));
+    h->n_layers = spec->n_layers;
+    int64_t off = 0;
+    for (int l = 0; l < h->n_layers; ++l) {
+        kanode_status s = make_layer_const(h, spec->layers[l], spec->dtype, off, h->hlc[l]);
+        if (s != KANODE_OK) return bail(s);
+        if (l > 0 && spec->layers[l].in_dims != spec->layers[l - 1].out_dims)
+            return bail(fail(h, KANODE_ERR_INVALID_ARG,
+                             "layer " + std::to_string(l) + " in_dims != previous out_dims (Lux.Chain)"));
+        off += layer_P(h->hlc[l]);
+        h->max_layer_P = std::max<int>(h->max_layer_P, (int)layer_P(h->hlc[l]));
+        h->max_dim = std::max({h->max_dim, h->hlc[l].I, h->hlc[l].O});
+        // kernel class for this layer
+        const LayerConst& lc = h->hlc[l];
+        if (lc.O <= 16 && (size_t)(lc.G * lc.I + lc.O + lc.I) * 65 * h->esize <= 150 * 1024 &&
+            layer_P(lc) <= 64 * 32) {
+            h->kind[l] = KIND_COL;
+        } else {
+            return bail(fail(h, KANODE_ERR_UNSUPPORTED,
+                             "layer " + std::to_string(l) + " shape (I=" + std::to_string(lc.I) + ", O=" +
+                                 std::to_string(lc.O) + ") is not supported by this build"));
+        }
+    }
+    h->P = off;
+    if (spec->rhs_kind == KANODE_RHS_CHAIN) {
+        h->n_in = spec->layers[0].in_dims;
+        h->n_out = spec->layers[h->n_layers - 1].out_dims;
+    } else if (spec->rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
+        if (h->n_layers != 1 || spec->layers[0].in_dims != 1 || spec->layers[0].out_dims != 1)
+            return bail(fail(h, KANODE_ERR_INVALID_ARG, "pointwise RHS needs exactly one KDense(1, 1, G)"));
+        if (spec->nx < 1 || spec->nx > (1 << 30)) return bail(fail(h, KANODE_ERR_INVALID_ARG, "nx must be >= 1"));
+        if (!(spec->dx > 0.0)) return bail(fail(h, KANODE_ERR_INVALID_ARG, "dx must be > 0"));
+        h->n_in = h->n_out = spec->nx;
+    } else {
+        return bail(fail(h, KANODE_ERR_INVALID_ARG, "unknown rhs_kind"));
+    }
+    hipError_t e = hipSetDevice(spec->device);
+    if (e != hipSuccess) return bail(fail(h, KANODE_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)));
+    if ((e = hipMalloc(&h->dlc, sizeof(LayerConst) * h->n_layers)) != hipSuccess)
+        return bail(fail(h, KANODE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)));
+    if ((e = hipMemcpy(h->dlc, h->hlc, sizeof(LayerConst) * h->n_layers, hipMemcpyHostToDevice)) != hipSuccess)
+        return bail(fail(h, KANODE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)));
+    h->slab_bytes = (size_t)kSlabBlocks * (size_t)std::max(h->max_layer_P, 1) * h->esize;
+    if ((e = hipMalloc(&h->slab, h->slab_bytes)) != hipSuccess)
+        return bail(fail(h, KANODE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)));
+    *out = h;
+    return KANODE_OK;
+}
+
+void kanode_destroy(kanode_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->spec.device);
+    if (h->dlc) (void)hipFree(h->dlc);
+    if (h->slab) (void)hipFree(h->slab);
+    if (h->ws) (void)hipFree(h->ws);
+    if (h->stage) (void)hipFree(h->stage);
+    delete h;
+}
+
+int64_t kanode_param_length(const kanode_handle* h) { return h ? h->P : -1; }
+int64_t kanode_layer_param_length(const kanode_handle* h, int32_t layer) {
+    if (!h || layer < 0 || layer >= h->n_layers) return -1;
+    return layer_P(h->hlc[layer]);
+}
+int64_t kanode_state_length(const kanode_handle* h) { return h ? h->n_in : -1; }
+
+kanode_status kanode_knots(const kanode_handle* h, int32_t layer, float* grid_out) {
+    if (!h || !grid_out || layer < 0 || layer >= h->n_layers) return KANODE_ERR_INVALID_ARG;
+    std::memcpy(grid_out, h->hlc[layer].grid, sizeof(float) * h->hlc[layer].G);
+    return KANODE_OK;
+}
+
+kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (max_batch < 0) return fail(h, KANODE_ERR_INVALID_ARG, "max_batch < 0");
+    s = ensure_ws(h, max_batch, nullptr);
+    if (s != KANODE_OK) return s;
+    if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
+        const size_t need = (size_t)(h->spec.nx * max_batch) * h->esize;
+        if (need > h->ws_bytes) {
+            HIP_TRY(h, hipDeviceSynchronize());
+            if (h->ws) HIP_TRY(h, hipFree(h->ws));
+            HIP_TRY(h, hipMalloc(&h->ws, need));
+            h->ws_bytes = need;
+        }
+    }
+    h->reserved_batch = std::max(h->reserved_batch, max_batch);
+    return KANODE_OK;
+}
+
+kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (batch < 0) return fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    if (batch == 0) return KANODE_OK;
+    if (!p || !u || !du) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64) return rhs_t<double>(h, (const double*)p, (const double*)u, (double*)du, batch, st);
+    return rhs_t<float>(h, (const float*)p, (const float*)u, (float*)du, batch, st);
+}
+
+kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,
+                         int64_t batch, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (batch < 0) return fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    if (batch == 0) return KANODE_OK;
+    if (!p || !u || !lam) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return vjp_t<double>(h, (const double*)p, (const double*)u, (const double*)lam, (double*)lam_J, (double*)dp,
+                             batch, st);
+    return vjp_t<float>(h, (const float*)p, (const float*)u, (const float*)lam, (float*)lam_J, (float*)dp, batch, st);
+}
+
+static kanode_status stage_alloc(kanode_handle* h, size_t bytes) {
+    if (bytes <= h->stage_bytes) return KANODE_OK;
+    if (h->stage) HIP_TRY(h, hipFree(h->stage));
+    h->stage = nullptr;
+    h->stage_bytes = 0;
+    HIP_TRY(h, hipMalloc(&h->stage, bytes));
+    h->stage_bytes = bytes;
+    return KANODE_OK;
+}
+
+kanode_status kanode_rhs_host(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (batch <= 0) return batch == 0 ? KANODE_OK : fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    const size_t bp = (size_t)h->P * h->esize, bu = (size_t)(h->n_in * batch) * h->esize,
+                 bo = (size_t)(h->n_out * batch) * h->esize;
+    if ((s = stage_alloc(h, bp + bu + bo)) != KANODE_OK) return s;
+    char* d = (char*)h->stage;
+    HIP_TRY(h, hipMemcpy(d, p, bp, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMemcpy(d + bp, u, bu, hipMemcpyHostToDevice));
+    if ((s = kanode_rhs(h, d, d + bp, d + bp + bu, batch, nullptr)) != KANODE_OK) return s;
+    HIP_TRY(h, hipMemcpy(du, d + bp + bu, bo, hipMemcpyDeviceToHost));
+    return KANODE_OK;
+}
+
+kanode_status kanode_vjp_host(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,
+                              int64_t batch) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (batch <= 0) return batch == 0 ? KANODE_OK : fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    const size_t bp = (size_t)h->P * h->esize, bu = (size_t)(h->n_in * batch) * h->esize,
+                 bo = (size_t)(h->n_out * batch) * h->esize;
+    if ((s = stage_alloc(h, 2 * bp + 2 * bu + bo)) != KANODE_OK) return s;
+    char* d = (char*)h->stage;
+    char* dp_d = d + bp;
+    char* u_d = dp_d + bp;
+    char* lam_d = u_d + bu;
+    char* lj_d = lam_d + bo;
+    HIP_TRY(h, hipMemcpy(d, p, bp, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMemcpy(u_d, u, bu, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMemcpy(lam_d, lam, bo, hipMemcpyHostToDevice));
+    if (dp) HIP_TRY(h, hipMemcpy(dp_d, dp, bp, hipMemcpyHostToDevice));
+    if ((s = kanode_vjp(h, d, u_d, lam_d, lam_J ? lj_d : nullptr, dp ? dp_d : nullptr, batch, nullptr)) != KANODE_OK)
+        return s;
+    if (lam_J) HIP_TRY(h, hipMemcpy(lam_J, lj_d, bu, hipMemcpyDeviceToHost));
+    if (dp) HIP_TRY(h, hipMemcpy(dp, dp_d, bp, hipMemcpyDeviceToHost));
+    return KANODE_OK;
+}
+
+kanode_status kanode_layer_forward(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, void* y,
+                                   int64_t K, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (layer < 0 || layer >= h->n_layers) return fail(h, KANODE_ERR_INVALID_ARG, "layer out of range");
+    if (K < 0) return fail(h, KANODE_ERR_INVALID_ARG, "K < 0");
+    if (K == 0) return KANODE_OK;
+    if (!p_layer || !x || !y) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer");
+    // kernels index p_full + p_off: shift the caller's layer slice back
+    const int64_t off = h->hlc[layer].p_off;
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return layer_fwd_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, (double*)y, K, st);
+    return layer_fwd_t<float>(h, layer, (const float*)p_layer - off, (const float*)x, (float*)y, K, st);
+}
+
+kanode_status kanode_layer_vjp(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, const void* ybar,
+                               void* xbar, void* pbar_layer, int64_t K, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (layer < 0 || layer >= h->n_layers) return fail(h, KANODE_ERR_INVALID_ARG, "layer out of range");
+    if (K < 0) return fail(h, KANODE_ERR_INVALID_ARG, "K < 0");
+    if (K == 0) return KANODE_OK;
+    if (!p_layer || !x || !ybar || !xbar) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer (xbar is required)");
+    const int64_t off = h->hlc[layer].p_off;
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return layer_vjp_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, (const double*)ybar,
+                                   (double*)xbar, pbar_layer ? (double*)pbar_layer - off : nullptr, K, st);
+    return layer_vjp_t<float>(h, layer, (const float*)p_layer - off, (const float*)x, (const float*)ybar, (float*)xbar,
+                              pbar_layer ? (float*)pbar_layer - off : nullptr, K, st);
+}
+
+kanode_status kanode_edge_activations(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, void* act,
+                                      int64_t K, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (layer < 0 || layer >= h->n_layers) return fail(h, KANODE_ERR_INVALID_ARG, "layer out of range");
+    if (K < 0) return fail(h, KANODE_ERR_INVALID_ARG, "K < 0");
+    if (K == 0) return KANODE_OK;
+    if (!p_layer || !x || !act) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer");
+    const int64_t off = h->hlc[layer].p_off;
+    hipStream_t st = (hipStream_t)stream;
+    if (h->hlc[layer].O > 64) return fail(h, KANODE_ERR_UNSUPPORTED, "edge activations need out_dims <= 64");
+    if (h->spec.dtype == KANODE_F64) {
+        HIP_TRY(h, kan::launch_kd_edge_act<double>(h->hlc[layer], h->dlc + layer, (const double*)p_layer - off,
+                                                   (const double*)x, (double*)act, K, st));
+    } else {
+        HIP_TRY(h, kan::launch_kd_edge_act<float>(h->hlc[layer], h->dlc + layer, (const float*)p_layer - off,
+                                                  (const float*)x, (float*)act, K, st));
+    }
+    return KANODE_OK;
+}
+
+}  // extern "C"

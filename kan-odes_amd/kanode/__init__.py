@@ -1,0 +1,16 @@
+"""kanode — MI355X-native KAN-ODE right-hand side and adjoint (host-side mirror).
+
+The compute path is libkanode.so (hand-written HIP kernels for gfx950 behind
+the C-ABI in include/kanode.h).  This package mirrors the reference's
+KolmogorovArnold.jl / Lux interface (KDense, Chain, setup) and the ODE RHS
+forms its drivers solve (NeuralODE chain RHS, Fisher-KPP rc_kanode).
+"""
+from ._lib import KanodeError, LIB_PATH, lib
+from .handle import KanodeHandle, LayerCfg
+from .layers import Chain, KDense, glorot_uniform, linrange_f32
+from .rhs import ChainRHS, FisherKPPRHS, fisher_kpp_laplacian, layer_apply, rhs_apply
+
+__all__ = [
+    "KanodeError", "LIB_PATH", "lib", "KanodeHandle", "LayerCfg", "Chain", "KDense", "glorot_uniform",
+    "linrange_f32", "ChainRHS", "FisherKPPRHS", "fisher_kpp_laplacian", "layer_apply", "rhs_apply",
+]

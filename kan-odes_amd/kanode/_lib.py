@@ -1,0 +1,100 @@
+"""ctypes binding of libkanode.so (the C-ABI declared in include/kanode.h).
+
+This is the Python side of the drop-in boundary: it binds exactly the entry
+points a Julia `ccall` shim binds.  The library is built
+in-tree by `make -C kan-odes_amd` (or __graft_entry__.build()); if it is missing
+this module raises — there is no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkanode.so")
+
+MAX_LAYERS = 8
+MAX_GRID = 32
+
+OK, ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_ALLOC, ERR_CAPTURE = range(6)
+F32, F64 = 0, 1
+NORM = {"tanh_fast": 0, "tanh": 1, "softsign": 2, "sigmoid": 3, "sigmoid_fast": 4, "identity": 5}
+BASIS = {"rbf": 0, "rswaf": 1, "iqf": 2}
+RHS_CHAIN, RHS_POINTWISE_PERIODIC_LAPLACIAN = 0, 1
+
+
+class LayerSpecC(C.Structure):
+    _fields_ = [
+        ("in_dims", C.c_int32), ("out_dims", C.c_int32), ("grid_len", C.c_int32),
+        ("normalizer", C.c_int32), ("basis", C.c_int32), ("use_base_act", C.c_int32),
+        ("grid_lo", C.c_float), ("grid_hi", C.c_float), ("denominator", C.c_float),
+        ("iqf_reference_quirk", C.c_int32),
+    ]
+
+
+class SpecC(C.Structure):
+    _fields_ = [
+        ("n_layers", C.c_int32),
+        ("layers", LayerSpecC * MAX_LAYERS),
+        ("dtype", C.c_int32),
+        ("rhs_kind", C.c_int32),
+        ("nx", C.c_int64),
+        ("diffusion", C.c_double),
+        ("dx", C.c_double),
+        ("device", C.c_int32),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/kanode.h declares
+_P = C.c_void_p
+_H = C.c_void_p
+SIGNATURES = [
+    ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),
+    ("kanode_destroy", None, [_H]),
+    ("kanode_last_error", C.c_char_p, [_H]),
+    ("kanode_status_string", C.c_char_p, [C.c_int]),
+    ("kanode_abi_version", C.c_int32, []),
+    ("kanode_param_length", C.c_int64, [_H]),
+    ("kanode_layer_param_length", C.c_int64, [_H, C.c_int32]),
+    ("kanode_state_length", C.c_int64, [_H]),
+    ("kanode_knots", C.c_int, [_H, C.c_int32, _P]),
+    ("kanode_reserve", C.c_int, [_H, C.c_int64]),
+    ("kanode_rhs", C.c_int, [_H, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_vjp", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
+    ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),
+    ("kanode_layer_forward", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_layer_vjp", C.c_int, [_H, C.c_int32, _P, _P, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_edge_activations", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
+]
+
+_lib = None
+
+
+class KanodeError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libkanode.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KanodeError(
+                f"{LIB_PATH} not found: build it with `make -C kan-odes_amd` "
+                "(the HIP extension is required; there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, handle=None, what: str = "") -> None:
+    if status != OK:
+        L = lib()
+        msg = L.kanode_last_error(handle).decode() if handle else ""
+        base = L.kanode_status_string(status).decode()
+        raise KanodeError(f"{what}: {base}" + (f" ({msg})" if msg else ""))

@@ -1,0 +1,187 @@
+"""Owning wrapper of a `kanode_handle*` — device tensors in, device tensors out.
+
+Array convention: a Julia column-major [N, B] array (one trajectory contiguous)
+is a C-contiguous torch tensor of shape (B, N): identical memory, so no copies
+cross the boundary.  The flat parameter vector is the ComponentArray order
+(include/kanode.h).  Every call is asynchronous on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+@dataclass(frozen=True)
+class LayerCfg:
+    """One KDense layer's constructor arguments (kdense.jl:20-37)."""
+    in_dims: int
+    out_dims: int
+    grid_len: int
+    normalizer: str = "tanh_fast"
+    basis: str = "rbf"
+    use_base_act: bool = True
+    grid_lims: tuple = (-1.0, 1.0)
+    denominator: float | None = None
+    iqf_reference_quirk: bool = True
+
+    def to_c(self) -> L.LayerSpecC:
+        if self.normalizer not in L.NORM:
+            raise ValueError(f"normalizer {self.normalizer!r} not in {sorted(L.NORM)}")
+        if self.basis not in L.BASIS:
+            raise ValueError(f"basis_func {self.basis!r} not in {sorted(L.BASIS)}")
+        den = 0.0 if self.denominator is None else float(np.float32(self.denominator))
+        return L.LayerSpecC(self.in_dims, self.out_dims, self.grid_len, L.NORM[self.normalizer],
+                            L.BASIS[self.basis], int(bool(self.use_base_act)),
+                            float(np.float32(self.grid_lims[0])), float(np.float32(self.grid_lims[1])), den,
+                            int(bool(self.iqf_reference_quirk)))
+
+    @property
+    def param_length(self) -> int:
+        n = self.in_dims * self.grid_len * self.out_dims
+        return n + (self.in_dims * self.out_dims if self.use_base_act else 0)
+
+
+_DT = {torch.float32: L.F32, torch.float64: L.F64}
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class KanodeHandle:
+    """A configured RHS (chain or pointwise+periodic-Laplacian) bound to one device."""
+
+    def __init__(self, layers, dtype=torch.float64, rhs_kind: str = "chain", nx: int = 0,
+                 diffusion: float = 0.0, dx: float = 1.0, device=None):
+        if dtype not in _DT:
+            raise TypeError("dtype must be torch.float32 or torch.float64")
+        layers = list(layers)
+        if not 1 <= len(layers) <= L.MAX_LAYERS:
+            raise ValueError(f"need 1..{L.MAX_LAYERS} layers")
+        self.layers = layers
+        self.dtype = dtype
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        spec = L.SpecC()
+        spec.n_layers = len(layers)
+        for i, lay in enumerate(layers):
+            spec.layers[i] = lay.to_c()
+        spec.dtype = _DT[dtype]
+        spec.rhs_kind = {"chain": L.RHS_CHAIN, "pointwise_periodic_laplacian": L.RHS_POINTWISE_PERIODIC_LAPLACIAN}[rhs_kind]
+        spec.nx = int(nx)
+        spec.diffusion = float(diffusion)
+        spec.dx = float(dx)
+        spec.device = self.device.index or 0
+        h = C.c_void_p()
+        st = L.lib().kanode_create(C.byref(spec), C.byref(h))
+        self._h = h
+        if st != L.OK:
+            msg = L.lib().kanode_last_error(h).decode() if h.value else ""
+            L.lib().kanode_destroy(h)
+            self._h = None
+            raise L.KanodeError(f"kanode_create: {L.lib().kanode_status_string(st).decode()} ({msg})")
+        self.rhs_kind = rhs_kind
+        self.P = int(L.lib().kanode_param_length(h))
+        self.N = int(L.lib().kanode_state_length(h))          # input state length
+        self.N_out = self.N if rhs_kind != "chain" else layers[-1].out_dims
+        self.layer_P = [int(L.lib().kanode_layer_param_length(h, i)) for i in range(len(layers))]
+        self.layer_off = list(np.cumsum([0] + self.layer_P[:-1]))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.lib().kanode_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- helpers -----------------------------------------------------------
+    def _check_t(self, t: torch.Tensor, shape, name: str) -> None:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor")
+        if t.device != self.device or t.dtype != self.dtype:
+            raise TypeError(f"{name} must be {self.dtype} on {self.device}, got {t.dtype} on {t.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+
+    def knots(self, layer: int = 0) -> np.ndarray:
+        g = np.zeros(self.layers[layer].grid_len, np.float32)
+        L.check(L.lib().kanode_knots(self._h, layer, C.c_void_p(g.ctypes.data)), self._h, "kanode_knots")
+        return g
+
+    def reserve(self, max_batch: int) -> None:
+        L.check(L.lib().kanode_reserve(self._h, int(max_batch)), self._h, "kanode_reserve")
+
+    # -- RHS -----------------------------------------------------------------
+    def rhs(self, p: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """du (B, N_out) = f(u (B, N); p)."""
+        B = u.shape[0] if u.dim() == 2 else 1
+        self._check_t(p, (self.P,), "p")
+        self._check_t(u, None, "u")
+        if u.numel() != B * self.N:
+            raise ValueError(f"u must hold B x {self.N} values, got shape {tuple(u.shape)}")
+        shape = (B, self.N_out) if u.dim() == 2 else (self.N_out,)
+        du = torch.empty(shape, dtype=self.dtype, device=self.device) if out is None else out
+        self._check_t(du, shape, "du")
+        L.check(L.lib().kanode_rhs(self._h, _ptr(p), _ptr(u), _ptr(du), B, _stream(self.device)), self._h,
+                "kanode_rhs")
+        return du
+
+    def vjp(self, p: torch.Tensor, u: torch.Tensor, lam: torch.Tensor, want_lamJ: bool = True,
+            dp: torch.Tensor | None = None, accumulate_dp: bool = True):
+        """(λᵀ∂f/∂u, Σ_b λᵀ∂f/∂p).  dp (if given) is ACCUMULATED into."""
+        B = u.shape[0] if u.dim() == 2 else 1
+        self._check_t(p, (self.P,), "p")
+        self._check_t(u, None, "u")
+        self._check_t(lam, (B, self.N_out) if u.dim() == 2 else (self.N_out,), "lam")
+        lamJ = torch.empty_like(u) if want_lamJ else None
+        if dp is None and accumulate_dp:
+            dp = torch.zeros_like(p)
+        L.check(L.lib().kanode_vjp(self._h, _ptr(p), _ptr(u), _ptr(lam), _ptr(lamJ), _ptr(dp), B,
+                                   _stream(self.device)), self._h, "kanode_vjp")
+        return lamJ, dp
+
+    # -- single layer ----------------------------------------------------------
+    def layer_forward(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        cfg = self.layers[layer]
+        K = x.shape[0]
+        self._check_t(p_layer, (cfg.param_length,), "p_layer")
+        self._check_t(x, (K, cfg.in_dims), "x")
+        y = torch.empty((K, cfg.out_dims), dtype=self.dtype, device=self.device)
+        L.check(L.lib().kanode_layer_forward(self._h, layer, _ptr(p_layer), _ptr(x), _ptr(y), K,
+                                             _stream(self.device)), self._h, "kanode_layer_forward")
+        return y
+
+    def layer_vjp(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor, ybar: torch.Tensor):
+        cfg = self.layers[layer]
+        K = x.shape[0]
+        self._check_t(p_layer, (cfg.param_length,), "p_layer")
+        self._check_t(x, (K, cfg.in_dims), "x")
+        self._check_t(ybar, (K, cfg.out_dims), "ybar")
+        xbar = torch.empty_like(x)
+        pbar = torch.zeros_like(p_layer)
+        L.check(L.lib().kanode_layer_vjp(self._h, layer, _ptr(p_layer), _ptr(x), _ptr(ybar), _ptr(xbar), _ptr(pbar),
+                                         K, _stream(self.device)), self._h, "kanode_layer_vjp")
+        return xbar, pbar
+
+    def edge_activations(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """act (K, I, O) with act[k, i, o] = φ_{o,i}(x[k, i]) (Activation_getter.jl:28-31,48-53)."""
+        cfg = self.layers[layer]
+        K = x.shape[0]
+        self._check_t(p_layer, (cfg.param_length,), "p_layer")
+        self._check_t(x, (K, cfg.in_dims), "x")
+        act = torch.empty((K, cfg.in_dims, cfg.out_dims), dtype=self.dtype, device=self.device)
+        L.check(L.lib().kanode_edge_activations(self._h, layer, _ptr(p_layer), _ptr(x), _ptr(act), K,
+                                                _stream(self.device)), self._h, "kanode_edge_activations")
+        return act
