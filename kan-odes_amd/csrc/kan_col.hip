@@ -1,0 +1,344 @@
+// kan_col.hip — generic KDense layer kernels, "column" form (gfx950).
+//
+// One thread per column k of x [I, K] (a trajectory of a batched NeuralODE RHS,
+// e.g. Lotka-Volterra KAN [2,10,2]: LV_driver_KANODE.jl:139-142); O <= OMAX
+// output accumulators live in registers; C/W reads are wave-uniform (scalar
+// loads).  Reference: KDense forward kdense.jl:109-130, pullback = Zygote over it
+// with rrule(_rbf) (utils.jl:15-21), per-edge activations Activation_getter.jl.
+// Parameter gradients: per-block LDS-staged tile products into a slab, then the
+// ordered slab reduction (bitwise reproducible; no float atomics).
+#include "kan_common.hpp"
+#include "kan_kernels.hpp"
+
+namespace kan {
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) slab_reduce_kernel(const T* __restrict__ slab, int64_t nblk, int64_t P,
+                                                             T* __restrict__ dp) {
+    __shared__ T red[kBlock / kWave];
+    const int64_t q = blockIdx.x;
+    T s = T(0);
+    for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[b * P + q];
+    s = wave_sum(s);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        dp[q] += t;
+    }
+}
+
+template <typename T>
+hipError_t launch_slab_reduce(const T* slab, int64_t nblk, int64_t P, T* dp, hipStream_t st) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL((slab_reduce_kernel<T>), dim3((unsigned)P), dim3(kBlock), 0, st, slab, nblk, P, dp);
+    return hipGetLastError();
+}
+
+// Sequential basis generator for one normalised input: direct (per-knot formula)
+// or the Gaussian recurrence.
+template <typename T, int PATH>
+struct BasisStream {
+    T n, F, R, z0, tau, invh;
+    __device__ __forceinline__ void init(const Math<T>& M, const LayerConst& lc, T nn) {
+        n = nn;
+        invh = T(lc.invh);
+        if constexpr (PATH != PATH_DIRECT) rec_anchor<T>(M, lc, n, z0, F, R, tau);   // tau = τ - τ_c
+    }
+    // returns φ_g, z_g (the scaled argument), aux (tanh for rswaf)
+    __device__ __forceinline__ T next(const Math<T>& M, const LayerConst& lc, int g, T& z, T& aux) {
+        if constexpr (PATH == PATH_DIRECT) {
+            z = (n - T(lc.grid[g])) * invh;
+            aux = T(0);
+            return basis_direct<T>(M, lc.basis, z, aux);
+        } else {
+            T kc = T(lc.K[g]);
+            if constexpr (PATH == PATH_REC_CORR) {
+                const T e = T(lc.e[g]);
+                kc = kc * kfma<T>(tau, kfma<T>(tau, T(0.5) * e * e, e), T(1));
+            }
+            const T v = F * kc;
+            z = z0 - T(lc.Dl[g]);
+            aux = T(0);
+            F = F * R;
+            return v;
+        }
+    }
+};
+
+template <typename T, int NORM, int PATH, int OMAX>
+__global__ void __launch_bounds__(kBlock)
+kd_fwd_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                  T* __restrict__ y, int64_t K) {
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const LayerConst& lc = *lcp;
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const T* __restrict__ C = p + lc.p_off;
+    const T* __restrict__ W = p + lc.w_off;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+        T acc[OMAX], bas[OMAX];
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o) { acc[o] = T(0); bas[o] = T(0); }
+        for (int i = 0; i < I; ++i) {
+            const T xi = x[(int64_t)I * k + i];
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, normalize<NORM, T>(M, lc.norm, xi));
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                const T phi = bs.next(M, lc, g, z, aux);
+                const T* Cc = C + (int64_t)O * (g + (int64_t)G * i);
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o)
+                    if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
+            }
+            if (lc.use_base) {
+                const T sw = swish<T>(M, xi);
+                const T* Wi = W + (int64_t)O * i;
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o)
+                    if (o < O) bas[o] = kfma<T>(Wi[o], sw, bas[o]);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o)
+            if (o < O) y[(int64_t)O * k + o] = lc.use_base ? acc[o] + bas[o] : acc[o];
+    }
+}
+
+// Column VJP with LDS staging: per tile of TILE columns every thread stages its
+// basis values φ[c][t], ȳ[o][t], swish(x)[i][t] in LDS (rows padded to TILE+1),
+// then the block computes the tile's dC = ȳ·φᵀ, dW = ȳ·swish(x)ᵀ with each
+// thread owning <= NPT parameters (accumulated in registers across tiles).
+template <typename T, int NORM, int PATH, int OMAX, int TILE, int NPT>
+__global__ void __launch_bounds__(TILE)
+kd_vjp_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                  const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ slab, int64_t K) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    T* smem = reinterpret_cast<T*>(smem_raw);
+    const LayerConst& lc = *lcp;
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const int GI = G * I;
+    const int nC = O * GI;
+    const int P = nC + (lc.use_base ? O * I : 0);
+    constexpr int LD = TILE + 1;
+    T* phiL = smem;                        // [GI][LD]
+    T* ybL = phiL + (int64_t)GI * LD;      // [O][LD]
+    T* swL = ybL + (int64_t)O * LD;        // [I][LD]
+    const T* __restrict__ C = p + lc.p_off;
+    const T* __restrict__ W = p + lc.w_off;
+    const int t = threadIdx.x;
+    T dacc[NPT];
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) dacc[q] = T(0);
+    const T invh = T(lc.invh);
+    for (int64_t tile = blockIdx.x; tile * TILE < K; tile += gridDim.x) {
+        const int64_t k = tile * TILE + t;
+        const bool valid = k < K;
+        T yb[OMAX];
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o) yb[o] = (o < O && valid) ? ybar[(int64_t)O * k + o] : T(0);
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o)
+            if (o < O) ybL[o * LD + t] = yb[o];
+        for (int i = 0; i < I; ++i) {
+            const T xi = valid ? x[(int64_t)I * k + i] : T(0);
+            const T n = normalize<NORM, T>(M, lc.norm, xi);
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, n);
+            T nbar = T(0);
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                const T phi = bs.next(M, lc, g, z, aux);
+                const int c = g + G * i;
+                const T* Cc = C + (int64_t)O * c;
+                T bb = T(0);
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o)
+                    if (o < O) bb = kfma<T>(Cc[o], yb[o], bb);
+                const T zb = basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb);
+                nbar = nbar + zb * invh;
+                phiL[c * LD + t] = valid ? phi : T(0);
+            }
+            T xb = nbar * dnormalize<NORM, T>(lc.norm, n);
+            if (lc.use_base) {
+                T sw, dsw;
+                swish_and_grad<T>(M, xi, sw, dsw);
+                const T* Wi = W + (int64_t)O * i;
+                T sb = T(0);
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o)
+                    if (o < O) sb = kfma<T>(Wi[o], yb[o], sb);
+                xb = xb + sb * dsw;
+                swL[i * LD + t] = valid ? sw : T(0);
+            }
+            if (valid) xbar[(int64_t)I * k + i] = xb;
+        }
+        __syncthreads();
+        const int nt = (int)((K - tile * TILE) < TILE ? (K - tile * TILE) : TILE);
+#pragma unroll
+        for (int qq = 0; qq < NPT; ++qq) {
+            const int q = t + qq * TILE;
+            if (q < P) {
+                const T* a;
+                const T* b;
+                if (q < nC) { a = ybL + (q % O) * LD; b = phiL + (q / O) * LD; }
+                else { const int r = q - nC; a = ybL + (r % O) * LD; b = swL + (r / O) * LD; }
+                T s = T(0);
+                for (int tt = 0; tt < nt; ++tt) s = kfma<T>(a[tt], b[tt], s);
+                dacc[qq] += s;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int qq = 0; qq < NPT; ++qq) {
+        const int q = t + qq * TILE;
+        if (q < P) slab[(int64_t)blockIdx.x * P + q] = dacc[qq];
+    }
+}
+
+// Per-edge activations act[o + O*(i + I*k)] (Activation_getter.jl:28-31,48-53).
+template <typename T, int NORM, int PATH, int OMAX>
+__global__ void __launch_bounds__(kBlock)
+kd_edge_act_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                   T* __restrict__ act, int64_t K) {
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const LayerConst& lc = *lcp;
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const T* __restrict__ C = p + lc.p_off;
+    const T* __restrict__ W = p + lc.w_off;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+        for (int i = 0; i < I; ++i) {
+            const T xi = x[(int64_t)I * k + i];
+            T acc[OMAX];
+#pragma unroll
+            for (int o = 0; o < OMAX; ++o) acc[o] = T(0);
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, normalize<NORM, T>(M, lc.norm, xi));
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                const T phi = bs.next(M, lc, g, z, aux);
+                const T* Cc = C + (int64_t)O * (g + (int64_t)G * i);
+#pragma unroll
+                for (int o = 0; o < OMAX; ++o)
+                    if (o < O) acc[o] = kfma<T>(phi, Cc[o], acc[o]);
+            }
+            const T sw = lc.use_base ? swish<T>(M, xi) : T(0);
+#pragma unroll
+            for (int o = 0; o < OMAX; ++o)
+                if (o < O)
+                    act[(int64_t)O * ((int64_t)I * k + i) + o] =
+                        lc.use_base ? kfma<T>(sw, W[(int64_t)O * i + o], acc[o]) : acc[o];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers: the LV configuration (tanh_fast, exact G=5 grid) is specialised;
+// every other layer runs the runtime-normalizer kernels.
+template <typename T, int NORM, int PATH>
+static hipError_t col_fwd_go(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
+                             hipStream_t st) {
+    const int g = grid_for(K, kBlock, kGridCap);
+    if (hlc.O <= 16)
+        hipLaunchKernelGGL((kd_fwd_col_kernel<T, NORM, PATH, 16>), dim3(g), dim3(kBlock), 0, st, lc, p, x, y, K);
+    else
+        hipLaunchKernelGGL((kd_fwd_col_kernel<T, NORM, PATH, 64>), dim3(g), dim3(kBlock), 0, st, lc, p, x, y, K);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
+                             hipStream_t st) {
+    if (hlc.norm == NORM_TANH_FAST && hlc.path == PATH_REC) return col_fwd_go<T, NORM_TANH_FAST, PATH_REC>(hlc, lc, p, x, y, K, st);
+    switch (hlc.path) {
+    case PATH_REC_CORR: return col_fwd_go<T, NORM_RUNTIME, PATH_REC_CORR>(hlc, lc, p, x, y, K, st);
+    case PATH_REC: return col_fwd_go<T, NORM_RUNTIME, PATH_REC>(hlc, lc, p, x, y, K, st);
+    default: return col_fwd_go<T, NORM_RUNTIME, PATH_DIRECT>(hlc, lc, p, x, y, K, st);
+    }
+}
+
+template <typename T, int NORM, int PATH, int TILE, int NPT>
+static hipError_t col_vjp_go2(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb,
+                              T* xb, T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st) {
+    const int GI = hlc.G * hlc.I;
+    const size_t lds = sizeof(T) * (size_t)(GI + hlc.O + hlc.I) * (TILE + 1);
+    const int P = hlc.O * GI + (hlc.use_base ? hlc.O * hlc.I : 0);
+    const int nb = grid_for(K, TILE, slab_blocks);
+    hipLaunchKernelGGL((kd_vjp_col_kernel<T, NORM, PATH, 16, TILE, NPT>), dim3(nb), dim3(TILE), lds, st, lc, p, x,
+                       yb, xb, slab, K);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !pbar) return e;
+    return launch_slab_reduce<T>(slab, nb, P, pbar + hlc.p_off, st);
+}
+
+template <typename T, int NORM, int PATH>
+static hipError_t col_vjp_go(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
+                             T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st) {
+    const int GI = hlc.G * hlc.I;
+    const int P = hlc.O * GI + (hlc.use_base ? hlc.O * hlc.I : 0);
+    const size_t rows = (size_t)(GI + hlc.O + hlc.I);
+    if (rows * 257 * sizeof(T) <= 150 * 1024 && P <= 256 * 8)
+        return col_vjp_go2<T, NORM, PATH, 256, 8>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+    // narrow tile (64 columns, one wave) for wider layers
+    return col_vjp_go2<T, NORM, PATH, 64, 32>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+}
+
+template <typename T>
+hipError_t launch_kd_vjp_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb,
+                             T* xb, T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st) {
+    if (hlc.norm == NORM_TANH_FAST && hlc.path == PATH_REC)
+        return col_vjp_go<T, NORM_TANH_FAST, PATH_REC>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+    switch (hlc.path) {
+    case PATH_REC_CORR:
+        return col_vjp_go<T, NORM_RUNTIME, PATH_REC_CORR>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+    case PATH_REC:
+        return col_vjp_go<T, NORM_RUNTIME, PATH_REC>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+    default:
+        return col_vjp_go<T, NORM_RUNTIME, PATH_DIRECT>(hlc, lc, p, x, yb, xb, pbar, slab, slab_blocks, K, st);
+    }
+}
+
+template <typename T, int PATH>
+static hipError_t edge_go(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* act, int64_t K,
+                          hipStream_t st) {
+    const int g = grid_for(K, kBlock, kGridCap);
+    if (hlc.O <= 16)
+        hipLaunchKernelGGL((kd_edge_act_kernel<T, NORM_RUNTIME, PATH, 16>), dim3(g), dim3(kBlock), 0, st, lc, p, x,
+                           act, K);
+    else
+        hipLaunchKernelGGL((kd_edge_act_kernel<T, NORM_RUNTIME, PATH, 64>), dim3(g), dim3(kBlock), 0, st, lc, p, x,
+                           act, K);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* act, int64_t K,
+                              hipStream_t st) {
+    switch (hlc.path) {
+    case PATH_REC_CORR: return edge_go<T, PATH_REC_CORR>(hlc, lc, p, x, act, K, st);
+    case PATH_REC: return edge_go<T, PATH_REC>(hlc, lc, p, x, act, K, st);
+    default: return edge_go<T, PATH_DIRECT>(hlc, lc, p, x, act, K, st);
+    }
+}
+
+#define KAN_COL_INST(T)                                                                                          \
+    template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
+    template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
+                                             int64_t, hipStream_t);                                               \
+    template hipError_t launch_kd_vjp_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, const T*,  \
+                                             T*, T*, T*, int, int64_t, hipStream_t);                              \
+    template hipError_t launch_kd_edge_act<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,       \
+                                              int64_t, hipStream_t);
+KAN_COL_INST(double)
+KAN_COL_INST(float)
+#undef KAN_COL_INST
+
+}  // namespace kan

@@ -6,16 +6,29 @@
 //   NNlib 0.9.24 tanh_fast, sigmoid, sigmoid_fast, swish, softsign and their
 //   rrules (Lotka-Volterra/Manifest.toml:1776).
 //
+// fp64 is VALU-bound on MI355X (a wave64 fp64 op occupies a SIMD for 4 cycles;
+// measured ~1.87 GHz under this load), so the fp64 elementary functions are
+// written for VALU instruction count:
+//   exp  — x·256/ln2 rounded by the 1.5·2^52 magic add (no rndne/cvt), |r| <= ln2/512,
+//          2^(j/256) from a 256-entry LDS table, degree-4 Taylor (remainder 3.7e-17),
+//          one ldexp: 13 VALU, <= 2 ulp.
+//   rcp  — v_rcp_f64 + two Newton steps (0.5-1 ulp); a/b = a·rcp(b).
+// fp32 uses the hardware-accelerated library functions.
+//
 // The RBF basis on the reference's uniform Float32 knot grid is evaluated with a
 // left-anchored Gaussian recurrence:
 //     z_j = z_0 - Δ_j,  Δ_j = (g_j - g_0)·s = j·δ + e_j   (e_j: Float32 knot rounding)
 //     exp(-z_j²) = exp(-z_0²) · R^j · exp(-Δ_j²) · exp(2 z_0 e_j),  R = exp(2 z_0 δ)
-// i.e. 2 exp per input element instead of G, with exp(-z_0²) formed from the
-// exact square z_0² = p + perr (fma) and exp(2 z_0 e_j) by its 2nd-order Taylor
-// series (|2 z_0 e_j| < 3e-6).  Relative error vs per-knot exp: <= ~12 ulp.
+// i.e. 2 exp per input element instead of G.  exp(-z_0²) is formed from the exact
+// square z_0² = p + perr (fma); exp(2 z_0 e_j) = exp(τ_c e_j)·exp(τ' e_j) with
+// τ' = 2 z_0 - τ_c centred on the normalizer's range, the first factor folded into
+// the constants and the second taken to 2nd order (|τ' e_j| <= 1.1e-6 for G=10).
+// Relative error vs per-knot exp: <= ~3e-15 of Σ|C_j φ_j| (tools/ and tests).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "kan_exp_table.hpp"
 
 namespace kan {
 
@@ -23,13 +36,13 @@ constexpr int kMaxGrid = 32;    // knots per layer handled by the kernels
 constexpr int kMaxLayers = 8;
 
 enum Norm : int { NORM_TANH_FAST = 0, NORM_TANH = 1, NORM_SOFTSIGN = 2, NORM_SIGMOID = 3,
-                  NORM_SIGMOID_FAST = 4, NORM_IDENTITY = 5 };
+                  NORM_SIGMOID_FAST = 4, NORM_IDENTITY = 5, NORM_RUNTIME = -1 };
 enum Basis : int { BASIS_RBF = 0, BASIS_RSWAF = 1, BASIS_IQF = 2 };
 // basis evaluation path chosen on the host from the layer's constants
 enum Path : int { PATH_DIRECT = 0, PATH_REC = 1, PATH_REC_CORR = 2 };
 
-// Per-layer constants, computed once on the host at handle creation and passed
-// by value as a kernel argument (lives in the kernarg segment -> SGPR loads).
+// Per-layer constants, computed once on the host at handle creation and stored
+// in a device buffer (wave-uniform reads -> scalar loads).
 struct LayerConst {
     int32_t I, O, G;
     int32_t norm, basis, use_base, iqf_quirk, path;
@@ -37,41 +50,103 @@ struct LayerConst {
     int64_t w_off;            // offset of W (p_off + O*G*I)
     float grid[kMaxGrid];     // Float32 knots (LinRange semantics, kdense.jl:90)
     float invh;               // Float32 1/h (utils.jl:9)
+    int32_t unit_delta;       // δ == 1 exactly (default grids): R = exp(2 z0)
     double g0, s, delta;      // recurrence anchor constants (f64; cast per dtype)
-    double K[kMaxGrid];       // exp(-Δ_j²)
+    double gs;                // -g0·s  (z0 = fma(n, s, gs))
+    double tau_c;             // centre of 2·z0 over the normalizer's range
+    double K[kMaxGrid];       // exp(-Δ_j²) · exp(tau_c·e_j)
     double e[kMaxGrid];       // Δ_j - j·δ
     double Dl[kMaxGrid];      // Δ_j
 };
 
+// Every kernel that evaluates fp64 exponentials stages the table in LDS once.
+#define KAN_EXP_TABLE_LDS(name)                                                         \
+    __shared__ double name[256];                                                        \
+    for (int i_ = threadIdx.x; i_ < 256; i_ += blockDim.x) name[i_] = kExp2Tab256[i_]; \
+    __syncthreads();
+
 // ---------------------------------------------------------------------------
-// elementary functions
-template <typename T> __device__ __forceinline__ T kexp(T x);
-template <> __device__ __forceinline__ double kexp<double>(double x) { return exp(x); }
-template <> __device__ __forceinline__ float kexp<float>(float x) { return expf(x); }
-template <typename T> __device__ __forceinline__ T ktanh(T x);
-template <> __device__ __forceinline__ double ktanh<double>(double x) { return tanh(x); }
-template <> __device__ __forceinline__ float ktanh<float>(float x) { return tanhf(x); }
-template <typename T> __device__ __forceinline__ T kabs(T x) { return x < T(0) ? -x : x; }
+// elementary functions, per dtype
+template <typename T> struct Math;
+
+template <> struct Math<double> {
+    const double* __restrict__ tab;   // LDS copy of kExp2Tab256
+    // exp for -745 <= x <= 709 (no special-case handling; callers bound or clamp x)
+    __device__ __forceinline__ double exp(double x) const {
+        const double magic = 0x1.8p52;
+        const double t = ::fma(x, k256oLn2, magic);      // round(x·256/ln2) in the low mantissa bits
+        const int k = (int)__double2loint(t);
+        const double kd = t - magic;
+        double r = ::fma(-kd, kLn2o256Hi, x);
+        r = ::fma(-kd, kLn2o256Lo, r);
+        double p = ::fma(r, 0x1.5555555555555p-5, 0x1.5555555555555p-3);   // 1/24, 1/6
+        p = ::fma(r, p, 0.5);
+        p = ::fma(r, p, 1.0);
+        p = ::fma(r, p, 1.0);
+        return __builtin_amdgcn_ldexp(tab[k & 255] * p, k >> 8);
+    }
+    // exp of a non-positive argument, clamped below (underflow -> 0)
+    // exp of a non-positive argument (underflow -> 0).  Only |x| < 5.8e6 keeps the int32
+    // exponent exact; clamp there (ldexp flushes anything below -1075 to 0 anyway).
+    __device__ __forceinline__ double exp_neg(double x) const { return exp(x < -7.0e5 ? -7.0e5 : x); }
+    __device__ __forceinline__ double exp_clamped(double x) const { return exp(fmin(fmax(x, -745.0), 709.0)); }
+    __device__ __forceinline__ double rcp(double d) const {
+        double r = __builtin_amdgcn_rcp(d);
+        double e = ::fma(-d, r, 1.0);
+        r = ::fma(r, e, r);
+        e = ::fma(-d, r, 1.0);
+        return ::fma(r, e, r);
+    }
+    __device__ __forceinline__ double div(double a, double d) const { return a * rcp(d); }
+    __device__ __forceinline__ double fma(double a, double b, double c) const { return ::fma(a, b, c); }
+    __device__ __forceinline__ double tanh(double x) const { return ::tanh(x); }
+};
+
+template <> struct Math<float> {
+    const double* __restrict__ tab;   // unused
+    __device__ __forceinline__ float exp(float x) const { return ::expf(x); }
+    __device__ __forceinline__ float exp_neg(float x) const { return ::expf(x); }
+    __device__ __forceinline__ float exp_clamped(float x) const { return ::expf(x); }
+    __device__ __forceinline__ float rcp(float d) const { return 1.0f / d; }
+    __device__ __forceinline__ float div(float a, float d) const { return a / d; }
+    __device__ __forceinline__ float fma(float a, float b, float c) const { return ::fmaf(a, b, c); }
+    __device__ __forceinline__ float tanh(float x) const { return ::tanhf(x); }
+};
+
+// Move a wave-uniform value into SGPRs (v_readfirstlane): coefficients computed
+// once per thread with VALU ops then live in SGPRs and feed VALU ops as the one
+// scalar operand, instead of occupying VGPRs (occupancy).
+__device__ __forceinline__ double to_sgpr(double v) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float to_sgpr(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ double kabs(double x) { return __builtin_fabs(x); }   // |x| source modifier
+__device__ __forceinline__ float kabs(float x) { return __builtin_fabsf(x); }
 template <typename T> __device__ __forceinline__ T kfma(T a, T b, T c);
-template <> __device__ __forceinline__ double kfma<double>(double a, double b, double c) { return fma(a, b, c); }
-template <> __device__ __forceinline__ float kfma<float>(float a, float b, float c) { return fmaf(a, b, c); }
+template <> __device__ __forceinline__ double kfma<double>(double a, double b, double c) { return ::fma(a, b, c); }
+template <> __device__ __forceinline__ float kfma<float>(float a, float b, float c) { return ::fmaf(a, b, c); }
 
 // NNlib.tanh_fast (Float64: exp form + small-|x| polynomial; Float32: rational)
-__device__ __forceinline__ double tanh_fast(double x) {
+__device__ __forceinline__ double tanh_fast(const Math<double>& M, double x) {
     const double x2 = x * x;
     double p = -0.008697141630499953;
-    p = fma(x2, p, 0.02186660872609521);
-    p = fma(x2, p, -0.05396823125794372);
-    p = fma(x2, p, 0.13333333325511604);
-    p = fma(x2, p, -0.33333333333324583);
-    p = fma(x2, p, 1.0);
+    p = ::fma(x2, p, 0.02186660872609521);
+    p = ::fma(x2, p, -0.05396823125794372);
+    p = ::fma(x2, p, 0.13333333325511604);
+    p = ::fma(x2, p, -0.33333333333324583);
+    p = ::fma(x2, p, 1.0);
     const double ypoly = x * p;
-    const double e2x = exp(fmin(x + x, 700.0));
-    const double y = (e2x - 1.0) / (e2x + 1.0);
+    const double e2x = M.exp(fmin(fmax(x + x, -700.0), 700.0));
+    const double y = (e2x - 1.0) * M.rcp(e2x + 1.0);
     const double sg = x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : x);
     return x2 > 900.0 ? sg : (x2 < 0.017 ? ypoly : y);
 }
-__device__ __forceinline__ float tanh_fast(float x) {
+__device__ __forceinline__ float tanh_fast(const Math<float>&, float x) {
     const float x2 = x * x;
     float n = 1.587199e-8f;
     n = fmaf(x2, n, 2.2332108e-5f);
@@ -88,42 +163,39 @@ __device__ __forceinline__ float tanh_fast(float x) {
 }
 
 // NNlib.sigmoid: t = exp(-|x|); x >= 0 ? 1/(1+t) : t/(1+t)
-template <typename T> __device__ __forceinline__ T sigmoid(T x) {
-    const T t = kexp<T>(-kabs(x));
-    return (x >= T(0) ? T(1) : t) / (T(1) + t);
+template <typename T> __device__ __forceinline__ T sigmoid(const Math<T>& M, T x) {
+    const T t = M.exp_neg(-kabs(x));
+    return (x >= T(0) ? T(1) : t) * M.rcp(T(1) + t);
 }
-template <typename T> __device__ __forceinline__ T sigmoid_fast(T x) {
-    const T y = sigmoid(x);
+template <typename T> __device__ __forceinline__ T sigmoid_fast(const Math<T>& M, T x) {
+    const T y = sigmoid(M, x);
     return x > T(40) ? T(1) : (x < T(-80) ? T(0) : y);
 }
-// swish(x) = x * sigmoid(x), one exp + one division
-template <typename T> __device__ __forceinline__ T swish(T x) {
-    const T t = kexp<T>(-kabs(x));
-    return x * ((x >= T(0) ? T(1) : t) / (T(1) + t));
-}
+// swish(x) = x * sigmoid(x): one exp + one reciprocal
+template <typename T> __device__ __forceinline__ T swish(const Math<T>& M, T x) { return x * sigmoid(M, x); }
 // swish and its rrule derivative  Ω + sigmoid_fast(x)(1 - Ω)  sharing one exp
-template <typename T> __device__ __forceinline__ void swish_and_grad(T x, T& om, T& d) {
-    const T t = kexp<T>(-kabs(x));
-    const T sg = (x >= T(0) ? T(1) : t) / (T(1) + t);
+template <typename T> __device__ __forceinline__ void swish_and_grad(const Math<T>& M, T x, T& om, T& d) {
+    const T sg = sigmoid(M, x);
     om = x * sg;
     const T sf = x > T(40) ? T(1) : (x < T(-80) ? T(0) : sg);
     d = om + sf * (T(1) - om);
 }
-template <typename T> __device__ __forceinline__ T softsign(T x) { return x / (T(1) + kabs(x)); }
+template <typename T> __device__ __forceinline__ T softsign(const Math<T>& M, T x) { return M.div(x, T(1) + kabs(x)); }
 
-template <typename T> __device__ __forceinline__ T normalize(int norm, T x) {
-    switch (norm) {
-    case NORM_TANH_FAST: return tanh_fast(x);
-    case NORM_TANH: return ktanh<T>(x);
-    case NORM_SOFTSIGN: return softsign(x);
-    case NORM_SIGMOID: return sigmoid(x);
-    case NORM_SIGMOID_FAST: return sigmoid_fast(x);
-    default: return x;
-    }
+// normalizer; NORM >= 0 selects at compile time, NORM_RUNTIME switches on `rt`
+template <int NORM, typename T> __device__ __forceinline__ T normalize(const Math<T>& M, int rt, T x) {
+    const int n = NORM < 0 ? rt : NORM;
+    if (n == NORM_SOFTSIGN) return softsign(M, x);
+    if (n == NORM_TANH_FAST) return tanh_fast(M, x);
+    if (n == NORM_TANH) return M.tanh(x);
+    if (n == NORM_SIGMOID) return sigmoid(M, x);
+    if (n == NORM_SIGMOID_FAST) return sigmoid_fast(M, x);
+    return x;
 }
 // rrule derivative in NNlib's Ω form
-template <typename T> __device__ __forceinline__ T dnormalize(int norm, T om) {
-    switch (norm) {
+template <int NORM, typename T> __device__ __forceinline__ T dnormalize(int rt, T om) {
+    const int n = NORM < 0 ? rt : NORM;
+    switch (n) {
     case NORM_TANH_FAST:
     case NORM_TANH: return T(1) - om * om;
     case NORM_SOFTSIGN: { const T a = T(1) - kabs(om); return a * a; }
@@ -134,10 +206,10 @@ template <typename T> __device__ __forceinline__ T dnormalize(int norm, T om) {
 }
 
 // direct basis value (utils.jl:13,32-34,54); aux = tanh(y) for rswaf
-template <typename T> __device__ __forceinline__ T basis_direct(int basis, T y, T& aux) {
-    if (basis == BASIS_RBF) return kexp<T>(-(y * y));
-    if (basis == BASIS_RSWAF) { aux = ktanh<T>(y); return T(1) - aux * aux; }
-    return T(1) / (T(1) + y * y);
+template <typename T> __device__ __forceinline__ T basis_direct(const Math<T>& M, int basis, T y, T& aux) {
+    if (basis == BASIS_RBF) return M.exp_neg(-(y * y));
+    if (basis == BASIS_RSWAF) { aux = M.tanh(y); return T(1) - aux * aux; }
+    return M.rcp(T(1) + y * y);
 }
 // pullback dy for a basis value (utils.jl:15-21, 36-42, 56-62)
 template <typename T> __device__ __forceinline__ T basis_pull(int basis, int iqf_quirk, T y, T phi, T aux, T bbar) {
@@ -146,45 +218,32 @@ template <typename T> __device__ __forceinline__ T basis_pull(int basis, int iqf
     return iqf_quirk ? T(-2) * y * phi * bbar : T(-2) * y * phi * phi * bbar;
 }
 
-// Recurrence anchor: E0 = exp(-z0²) with exact square, R = exp(2 z0 δ).
-template <typename T> __device__ __forceinline__ void rec_anchor(const LayerConst& lc, T n, T& z0, T& E0, T& R) {
-    z0 = (n - T(lc.g0)) * T(lc.s);
+// The recurrence's per-layer scalars, hoisted into registers once per thread
+// (reading them through the LayerConst pointer inside the loop re-issues scalar
+// loads whose lgkmcnt waits serialise with the LDS exp-table reads).
+template <typename T> struct RecScalars {
+    T s, gs, delta, tau_c;
+    int unit_delta;
+    __device__ __forceinline__ explicit RecScalars(const LayerConst& lc)
+        : s(T(lc.s)), gs(T(lc.gs)), delta(T(lc.delta)), tau_c(T(lc.tau_c)), unit_delta(lc.unit_delta) {}
+};
+
+// Recurrence anchor for a normalised input n:
+//   z0 = (n - g0)·s,  E0 = exp(-z0²) (exact square),  R = exp(2 z0 δ),  τ' = 2 z0 - τ_c
+template <typename T> __device__ __forceinline__ void rec_anchor(const Math<T>& M, const RecScalars<T>& rc, T n, T& z0,
+                                                                  T& E0, T& R, T& taup) {
+    z0 = kfma<T>(n, rc.s, rc.gs);
     const T p2 = z0 * z0;
     const T perr = kfma<T>(z0, z0, -p2);          // z0² = p2 + perr exactly
-    E0 = kexp<T>(-p2) * (T(1) - perr);            // exp(-p2 - perr), |perr| <= ulp(p2)/2
-    R = kexp<T>((z0 + z0) * T(lc.delta));
+    const T E = M.exp(-p2);
+    E0 = kfma<T>(-E, perr, E);                    // exp(-p2 - perr), |perr| <= ulp(p2)/2
+    const T tw = z0 + z0;                         // the correction exp(2 z0 e_j) is in 2·z0
+    R = M.exp(rc.unit_delta ? tw : tw * rc.delta);
+    taup = tw - rc.tau_c;
 }
-
-// All G basis values of one normalised input n (into phi[]), plus z_j for the
-// pullback (zv[]).  PATH_DIRECT matches the reference formula term by term.
-template <typename T, int PATH>
-__device__ __forceinline__ void basis_all(const LayerConst& lc, T n, T* phi, T* zv, T* aux) {
-    const int G = lc.G;
-    if constexpr (PATH == PATH_DIRECT) {
-        const T invh = T(lc.invh);
-#pragma unroll 4
-        for (int g = 0; g < G; ++g) {
-            const T y = (n - T(lc.grid[g])) * invh;
-            zv[g] = y;
-            phi[g] = basis_direct<T>(lc.basis, y, aux[g]);
-        }
-    } else {
-        T z0, F, R;
-        rec_anchor<T>(lc, n, z0, F, R);
-        const T tau = z0 + z0;
-#pragma unroll 4
-        for (int g = 0; g < G; ++g) {
-            T v = F * T(lc.K[g]);
-            if constexpr (PATH == PATH_REC_CORR) {
-                const T e = T(lc.e[g]);
-                v = v * kfma<T>(tau, kfma<T>(tau, T(0.5) * e * e, e), T(1));
-            }
-            phi[g] = v;
-            zv[g] = z0 - T(lc.Dl[g]);
-            aux[g] = T(0);
-            F = F * R;
-        }
-    }
+template <typename T> __device__ __forceinline__ void rec_anchor(const Math<T>& M, const LayerConst& lc, T n, T& z0,
+                                                                  T& E0, T& R, T& taup) {
+    rec_anchor<T>(M, RecScalars<T>(lc), n, z0, E0, R, taup);
 }
 
 }  // namespace kan

@@ -23,7 +23,7 @@ using kan::LayerConst;
 
 namespace {
 
-constexpr int kSlabBlocks = 2048;   // grid cap of the VJP kernels = slab rows
+constexpr int kSlabBlocks = 4096;   // grid cap of the VJP kernels = slab rows
 
 enum LayerKind { KIND_COL = 0 };
 
@@ -114,25 +114,33 @@ kanode_status make_layer_const(kanode_handle* h, const kanode_layer_spec& s, int
     const double sd = (double)lc.invh;
     lc.g0 = (double)lc.grid[0];
     lc.s = sd;
+    lc.gs = -lc.g0 * sd;
     lc.delta = ((double)s.grid_hi - (double)s.grid_lo) * sd / (double)(lc.G - 1);
+    lc.unit_delta = lc.delta == 1.0 ? 1 : 0;
+    // the knot-rounding correction exp(2·z0·e_j) is expanded around the centre of
+    // 2·z0 ∈ [2 z_lo, 2 z_hi] over the normalizer's range
+    double nlo = -1.0, nhi = 1.0;
+    const bool bounded = norm_range(lc.norm, nlo, nhi);
+    const double zlo = (nlo - lc.g0) * sd, zhi = (nhi - lc.g0) * sd;
+    lc.tau_c = bounded ? (zlo + zhi) : 0.0;
     double emax = 0.0;
     bool exact = true;
     for (int j = 0; j < lc.G; ++j) {
         const double D = ((double)lc.grid[j] - (double)lc.grid[0]) * sd;
         lc.Dl[j] = D;
         lc.e[j] = D - (double)j * lc.delta;
-        lc.K[j] = (double)std::exp(-(long double)D * (long double)D);
+        const long double DL = D;
+        lc.K[j] = (double)(std::exp(-DL * DL) * std::exp((long double)lc.tau_c * (long double)lc.e[j]));
         emax = std::max(emax, std::fabs(lc.e[j]));
         if (lc.e[j] != 0.0) exact = false;
     }
     // recurrence admissibility: bounded normalizer, no overflow of exp(-z0²) or
-    // R^(G-1), and a 2nd-order Taylor correction that is exact to < 1 ulp.
+    // R^(G-1), and a centred 2nd-order correction accurate to < 1 ulp.
     lc.path = kan::PATH_DIRECT;
-    double nlo, nhi;
-    if (lc.basis == KANODE_BASIS_RBF && norm_range(lc.norm, nlo, nhi)) {
-        const double zmax = std::max(std::fabs((nlo - lc.g0) * sd), std::fabs((nhi - lc.g0) * sd));
+    if (lc.basis == KANODE_BASIS_RBF && bounded) {
+        const double zmax = std::max(std::fabs(zlo), std::fabs(zhi));
         const double lim = (dtype == KANODE_F64) ? 600.0 : 80.0;
-        const double tmax = 2.0 * zmax * emax;
+        const double tmax = (zhi - zlo) * emax;   // max |τ' e_j|
         const bool ok = zmax * zmax <= lim && 2.0 * zmax * std::fabs(lc.delta) * (lc.G - 1) <= lim &&
                         lc.delta > 0.0 && (dtype == KANODE_F64 ? tmax <= 1e-5 : tmax <= 1e-3);
         if (ok) lc.path = exact ? kan::PATH_REC : kan::PATH_REC_CORR;
