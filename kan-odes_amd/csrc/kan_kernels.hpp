@@ -26,4 +26,20 @@ template <typename T>
 hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* act, int64_t K,
                               hipStream_t st);
 
+// surrogate shapes (kan_wide.hip)
+constexpr int kWideKT = 8;       // column tile of the wide-out kernels
+constexpr int kWideOMax = 16;    // max out_dims of a wide-in layer
+template <typename T>
+hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
+                                int64_t K, hipStream_t st);
+template <typename T>
+hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
+                                 hipStream_t st);
+template <typename T>
+hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
+                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st);
+template <typename T>
+hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
+                                T* pbar, int64_t K, hipStream_t st);
+
 }  // namespace kan

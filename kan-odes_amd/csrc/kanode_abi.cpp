@@ -25,7 +25,9 @@ namespace {
 
 constexpr int kSlabBlocks = 4096;   // grid cap of the VJP kernels = slab rows
 
-enum LayerKind { KIND_COL = 0 };
+// column: thread per batch column (small I·G, O <= 16; e.g. LV [2,10,2]);
+// wide-in / wide-out: the surrogate shapes (kan_wide.hip)
+enum LayerKind { KIND_COL = 0, KIND_WIDE_IN = 1, KIND_WIDE_OUT = 2 };
 
 }  // namespace
 
@@ -158,14 +160,39 @@ bool is_capturing(hipStream_t st) {
     return cs != hipStreamCaptureStatusNone;
 }
 
-// Chain workspace: every hidden layer's activations (kept for the VJP) + two
-// gradient ping-pong buffers of the widest layer.
-size_t chain_ws_bytes(const kanode_handle* h, int64_t B) {
-    int64_t elems = 0;
-    for (int l = 1; l < h->n_layers; ++l) elems += (int64_t)h->hlc[l].I * B;
-    elems += 2 * (int64_t)h->max_dim * B;
-    return (size_t)elems * h->esize;
+// Partial-sum slab of the surrogate-shape kernels for a batch of B columns.
+int64_t wide_slab_elems(const kanode_handle* h, int64_t B) {
+    int64_t m = 0;
+    for (int l = 0; l < h->n_layers; ++l) {
+        const LayerConst& c = h->hlc[l];
+        if (h->kind[l] == KIND_WIDE_IN) m = std::max<int64_t>(m, (int64_t)((c.I + 255) / 256) * B * c.O);
+        if (h->kind[l] == KIND_WIDE_OUT)
+            m = std::max<int64_t>(m, (int64_t)((c.O + 255) / 256) * B * (c.G * c.I + c.I));
+    }
+    return m;
 }
+
+// Chain workspace layout (elements of the dtype), for a batch of B columns:
+//   [hidden activations: Σ_{l>=1} I_l·B][grad ping: max_dim·B][grad pong: max_dim·B][wide slab]
+struct WsLayout {
+    int64_t acts, g0, g1, wslab, total;
+};
+WsLayout ws_layout(const kanode_handle* h, int64_t B) {
+    WsLayout w{};
+    int64_t e = 0;
+    w.acts = e;
+    for (int l = 1; l < h->n_layers; ++l) e += (int64_t)h->hlc[l].I * B;
+    w.g0 = e;
+    e += (int64_t)h->max_dim * B;
+    w.g1 = e;
+    e += (int64_t)h->max_dim * B;
+    w.wslab = e;
+    e += wide_slab_elems(h, B);
+    w.total = e;
+    return w;
+}
+
+size_t chain_ws_bytes(const kanode_handle* h, int64_t B) { return (size_t)ws_layout(h, B).total * h->esize; }
 
 kanode_status ensure_ws(kanode_handle* h, int64_t B, hipStream_t st) {
     const size_t need = h->spec.rhs_kind == KANODE_RHS_CHAIN ? chain_ws_bytes(h, B) : 0;
@@ -181,12 +208,24 @@ kanode_status ensure_ws(kanode_handle* h, int64_t B, hipStream_t st) {
     return KANODE_OK;
 }
 
+// The wide kernels need the chain workspace's slab (sized by ensure_ws(K)).
+template <typename T>
+T* wide_slab(kanode_handle* h, int64_t K) {
+    return (T*)h->ws + ws_layout(h, K).wslab;
+}
+
 template <typename T>
 kanode_status layer_fwd_t(kanode_handle* h, int l, const T* p_full, const T* x, T* y, int64_t K, hipStream_t st) {
     const LayerConst& hl = h->hlc[l];
     switch (h->kind[l]) {
     case KIND_COL:
         HIP_TRY(h, kan::launch_kd_fwd_col<T>(hl, h->dlc + l, p_full, x, y, K, st));
+        return KANODE_OK;
+    case KIND_WIDE_IN:
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(hl, h->dlc + l, p_full, x, y, wide_slab<T>(h, K), K, st));
+        return KANODE_OK;
+    case KIND_WIDE_OUT:
+        HIP_TRY(h, kan::launch_kd_fwd_wideout<T>(hl, h->dlc + l, p_full, x, y, K, st));
         return KANODE_OK;
     }
     return fail(h, KANODE_ERR_UNSUPPORTED, "layer kind");
@@ -200,6 +239,13 @@ kanode_status layer_vjp_t(kanode_handle* h, int l, const T* p_full, const T* x, 
     case KIND_COL:
         HIP_TRY(h, kan::launch_kd_vjp_col<T>(hl, h->dlc + l, p_full, x, yb, xb, pbar_full, (T*)h->slab, kSlabBlocks,
                                              K, st));
+        return KANODE_OK;
+    case KIND_WIDE_IN:
+        HIP_TRY(h, kan::launch_kd_vjp_widein<T>(hl, h->dlc + l, p_full, x, yb, xb, pbar_full, K, st));
+        return KANODE_OK;
+    case KIND_WIDE_OUT:
+        HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(hl, h->dlc + l, p_full, x, yb, xb, pbar_full, wide_slab<T>(h, K), K,
+                                                 st));
         return KANODE_OK;
     }
     return fail(h, KANODE_ERR_UNSUPPORTED, "layer kind");
@@ -216,10 +262,10 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
     kanode_status s = ensure_ws(h, B, st);
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;
+    const WsLayout wl = ws_layout(h, B);
     const T* cur = u;
-    T* ping = ws + (h->ws_bytes / h->esize) - 2 * (int64_t)h->max_dim * B;
     for (int l = 0; l < h->n_layers; ++l) {
-        T* out = (l == h->n_layers - 1) ? du : ping + (l % 2) * (int64_t)h->max_dim * B;
+        T* out = (l == h->n_layers - 1) ? du : ws + ((l % 2) ? wl.g1 : wl.g0);
         s = layer_fwd_t<T>(h, l, p, cur, out, B, st);
         if (s != KANODE_OK) return s;
         cur = out;
@@ -254,10 +300,11 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
     kanode_status s = ensure_ws(h, B, st);
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;
+    const WsLayout wl = ws_layout(h, B);
     // forward recompute, keeping every hidden layer's input
     const T* acts[KANODE_MAX_LAYERS];
     acts[0] = u;
-    T* wp = ws;
+    T* wp = ws + wl.acts;
     for (int l = 1; l < h->n_layers; ++l) {
         T* out = wp;
         wp += (int64_t)h->hlc[l].I * B;
@@ -265,8 +312,8 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
         if (s != KANODE_OK) return s;
         acts[l] = out;
     }
-    T* g0 = wp;
-    T* g1 = wp + (int64_t)h->max_dim * B;
+    T* g0 = ws + wl.g0;
+    T* g1 = ws + wl.g1;
     const T* g = lam;
     for (int l = h->n_layers - 1; l >= 0; --l) {
         T* out = (l == 0) ? lamJ : ((l % 2) ? g0 : g1);
@@ -334,9 +381,14 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
         h->max_dim = std::max({h->max_dim, h->hlc[l].I, h->hlc[l].O});
         // kernel class for this layer
         const LayerConst& lc = h->hlc[l];
+        const size_t rows = (size_t)(lc.G * lc.I + lc.I);
         if (lc.O <= 16 && (size_t)(lc.G * lc.I + lc.O + lc.I) * 65 * h->esize <= 150 * 1024 &&
             layer_P(lc) <= 64 * 32) {
             h->kind[l] = KIND_COL;
+        } else if (lc.O <= kan::kWideOMax) {
+            h->kind[l] = KIND_WIDE_IN;
+        } else if (rows * kan::kWideKT * h->esize * (1 + 4) <= 150 * 1024) {
+            h->kind[l] = KIND_WIDE_OUT;
         } else {
             return bail(fail(h, KANODE_ERR_UNSUPPORTED,
                              "layer " + std::to_string(l) + " shape (I=" + std::to_string(lc.I) + ", O=" +
@@ -496,6 +548,7 @@ kanode_status kanode_layer_forward(kanode_handle* h, int32_t layer, const void* 
     // kernels index p_full + p_off: shift the caller's layer slice back
     const int64_t off = h->hlc[layer].p_off;
     hipStream_t st = (hipStream_t)stream;
+    if ((s = ensure_ws(h, K, st)) != KANODE_OK) return s;
     if (h->spec.dtype == KANODE_F64)
         return layer_fwd_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, (double*)y, K, st);
     return layer_fwd_t<float>(h, layer, (const float*)p_layer - off, (const float*)x, (float*)y, K, st);
@@ -511,6 +564,7 @@ kanode_status kanode_layer_vjp(kanode_handle* h, int32_t layer, const void* p_la
     if (!p_layer || !x || !ybar || !xbar) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer (xbar is required)");
     const int64_t off = h->hlc[layer].p_off;
     hipStream_t st = (hipStream_t)stream;
+    if ((s = ensure_ws(h, K, st)) != KANODE_OK) return s;
     if (h->spec.dtype == KANODE_F64)
         return layer_vjp_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, (const double*)ybar,
                                    (double*)xbar, pbar_layer ? (double*)pbar_layer - off : nullptr, K, st);

@@ -1,0 +1,92 @@
+"""Full-field surrogate chains on the GPU vs the oracle
+(PDE examples/Burgers_Surrogate.jl:85-97, Schrodinger_Surrogate.jl:93-104; kdense.jl:109-130)."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import RTOL, assert_close, cfgs_from_specs, chain_scale, device, specs_from_meta, t
+from oracle import oracle as O
+
+import kanode
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_chain(specs, p, u, ybar, dt=torch.float64, y_ref=None, xbar_ref=None, pbar_ref=None):
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=dt, rhs_kind="chain", device=device())
+    y = hd.rhs(t(p, dt), t(u, dt))
+    y_ref = O.chain_fwd(specs, p, u) if y_ref is None else y_ref
+    assert_close(y, y_ref, chain_scale(specs, p, u), RTOL[dt], "y")
+    xb, pb = hd.vjp(t(p, dt), t(u, dt), t(ybar, dt))
+    if xbar_ref is None:
+        xbar_ref, pbar_ref = O.chain_vjp(specs, p, u, ybar)
+    xs, ps = O.chain_vjp(specs, np.abs(p), u, np.abs(ybar))
+    assert_close(xb, xbar_ref, np.abs(xs) * 1e2 + np.max(np.abs(xs)) * 1e-2, RTOL[dt], "xbar")
+    assert_close(pb, pbar_ref, np.abs(ps) * 1e2 + np.max(np.abs(ps)) * 1e-2, RTOL[dt], "pbar")
+    return hd
+
+
+@pytest.mark.parametrize("name", ["burgers41", "schrodinger402"])
+def test_surrogate_golden(golden, name):
+    d = golden(name)
+    specs = specs_from_meta(d["meta"])
+    _check_chain(specs, d["p"], d["u"], d["ybar"], y_ref=d["y"], xbar_ref=d["xbar"], pbar_ref=d["pbar"])
+
+
+def _glorot_params(rng, specs):
+    parts = []
+    for s in specs:
+        lim = np.sqrt(6.0 / (s.out_dims + s.grid_len * s.in_dims))
+        parts.append(rng.uniform(-lim, lim, s.out_dims * s.grid_len * s.in_dims))
+        lim = np.sqrt(6.0 / (s.out_dims + s.in_dims))
+        parts.append(rng.uniform(-lim, lim, s.out_dims * s.in_dims))
+    return np.concatenate(parts)
+
+
+@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (2048, 10, 8), (300, 7, 3), (2048, 10, 1), (64, 5, 11)])
+def test_surrogate_baseline_sizes(N, G, B):
+    """BU512: KAN [512,10,512] G=5; SC1024: KAN [2048,10,2048] G=10 (state [Re; Im]); odd sizes and
+    a column count that is not a multiple of the 8-column tile."""
+    rng = np.random.default_rng(N + G + B)
+    specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+    p = _glorot_params(rng, specs)
+    x = np.linspace(-1, 1, N)
+    u = np.stack([-np.sin(np.pi * x) + 0.3 * rng.normal() * np.sin(2 * np.pi * x) for _ in range(B)])
+    ybar = rng.normal(size=u.shape)
+    _check_chain(specs, p, u, ybar)
+
+
+def test_surrogate_single_layers_and_kinds():
+    """Each wide layer through the single-layer entry points (one Lux KDense call each)."""
+    rng = np.random.default_rng(3)
+    specs = [O.LayerSpec(512, 10, 5, "softsign"), O.LayerSpec(10, 512, 5, "softsign")]
+    p = _glorot_params(rng, specs)
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=torch.float64, rhs_kind="chain", device=device())
+    x = rng.uniform(-1, 1, (4, 512))
+    off = 0
+    for li, s in enumerate(specs):
+        n = s.param_length()
+        pl = p[off:off + n]
+        y = hd.layer_forward(li, t(pl), t(x))
+        ry = O.layer_fwd(s, pl, x)
+        sc = np.abs(O.layer_fwd(s, np.abs(pl), x))
+        assert_close(y, ry, sc + 1e-3 * np.max(sc), RTOL[torch.float64], f"layer {li}")
+        yb = rng.normal(size=ry.shape)
+        xb, pb = hd.layer_vjp(li, t(pl), t(x), t(yb))
+        rxb, rpb = O.layer_vjp(s, pl, x, yb)
+        xs, ps = O.layer_vjp(s, np.abs(pl), x, np.abs(yb))
+        assert_close(xb, rxb, np.abs(xs) * 1e2 + np.max(np.abs(xs)) * 1e-2, RTOL[torch.float64], f"layer {li} xbar")
+        assert_close(pb, rpb, np.abs(ps) * 1e2 + np.max(np.abs(ps)) * 1e-2, RTOL[torch.float64], f"layer {li} pbar")
+        x = ry
+        off += n
+
+
+def test_surrogate_f32():
+    rng = np.random.default_rng(5)
+    specs = [O.LayerSpec(512, 10, 5, "softsign"), O.LayerSpec(10, 512, 5, "softsign")]
+    p = _glorot_params(rng, specs).astype(np.float32)
+    u = rng.uniform(-1, 1, (4, 512)).astype(np.float32)
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=torch.float32, rhs_kind="chain", device=device())
+    y = hd.rhs(t(p, torch.float32), t(u, torch.float32))
+    sc = chain_scale(specs, p.astype(np.float64), u.astype(np.float64))
+    assert_close(y, O.chain_fwd(specs, p, u), sc, RTOL[torch.float32], "y f32")
