@@ -1,0 +1,177 @@
+"""Device-resident Tsit5 integrator around the HIP RHS.
+
+Restates OrdinaryDiffEqTsit5 1.1.0 / OrdinaryDiffEq 6.89 semantics (pinned at
+Lotka-Volterra/Manifest.toml:1984,2162; third-party, not under /root/reference;
+restated from the published package — verify where Julia exists):
+  * Tsitouras 5(4) tableau, FSAL, 4th-order free dense output (Tsit5Interp);
+  * error norm: RMS over ALL state entries of  utilde / (abstol + max(|u_prev|,|u|)·reltol)
+    — a batched [N, B] state is ONE ODE with one step size, as in the reference
+    (NeuralODE / ODEProblem on a matrix state);
+  * PI step-size controller: beta1 = 7/(10·5), beta2 = 2/(5·5), gamma = 9/10,
+    qmin = 1/5, qmax = 10, qoldinit = 1e-4, qsteady_min = qsteady_max = 1;
+  * Hairer-Wanner initial step (ode_determine_initdt);
+  * defaults abstol = 1e-6, reltol = 1e-3; saveat values from the dense interpolant.
+Call sites the reference uses: LV_driver_KANODE.jl:122,180-184, Fisher-KPP_Source.jl:102-103.
+
+Every RHS evaluation is one libkanode.so call (through the autograd Function),
+so `solve(...)` is differentiable: backward runs the HIP VJP kernel once per
+stage (discrete adjoint, ≡ reverse-mode AD through the solver steps).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+# Tsitouras 5(4) coefficients (OrdinaryDiffEq tsit_tableaus.jl)
+C = (0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0)
+A = (
+    (0.161,),
+    (-0.008480655492356989, 0.335480655492357),
+    (2.897153057105493, -6.359448489975075, 4.3622954328695815),
+    (5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525),
+    (5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383),
+    (0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774),
+)
+BTILDE = (-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995, -0.1447110071732629,
+          0.5823571654525552, -0.45808210592918697, 0.015151515151515152)
+# dense output b_i(θ) = Σ_m R[i][m] θ^(m+1)  (Tsit5Interp), i = 1..7
+RI = (
+    (1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216),
+    (0.0, 0.13169999999999998, -0.2234, 0.1017),
+    (0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253),
+    (0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902),
+    (0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928),
+    (0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661),
+    (0.0, 1.5, -4.0, 2.5),
+)
+
+
+def interp_weights(theta: float):
+    return [sum(r * theta ** (m + 1) for m, r in enumerate(row)) for row in RI]
+
+
+def rms(x: torch.Tensor) -> torch.Tensor:
+    return torch.sqrt(torch.mean(x * x))
+
+
+@dataclass
+class Tsit5Options:
+    abstol: float = 1e-6
+    reltol: float = 1e-3
+    dt: float | None = None            # fixed step (adaptive=False) or initial step
+    adaptive: bool = True
+    maxiters: int = 100000
+    dtmin: float = 0.0
+    beta1: float = 7.0 / 50.0
+    beta2: float = 2.0 / 25.0
+    gamma: float = 0.9
+    qmin: float = 0.2
+    qmax: float = 10.0
+    qoldinit: float = 1e-4
+
+
+@dataclass
+class Solution:
+    t: list
+    u: torch.Tensor                    # (len(saveat), *u0.shape)
+    stats: dict = field(default_factory=dict)
+
+
+def _initdt(f, u0, p, t0, tdist, opt: Tsit5Options, f0):
+    """Hairer & Wanner initial step (OrdinaryDiffEq ode_determine_initdt, order 5)."""
+    sk = opt.abstol + torch.abs(u0) * opt.reltol
+    d0 = rms(u0 / sk).item()
+    d1 = rms(f0 / sk).item()
+    dt0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    dt0 = min(dt0, tdist)
+    u1 = u0 + dt0 * f0
+    f1 = f(u1, p, t0 + dt0)
+    d2 = rms((f1 - f0) / sk).item() / dt0
+    mx = max(d1, d2)
+    dt1 = max(1e-6, dt0 * 1e-3) if mx <= 1e-15 else (0.01 / mx) ** (1.0 / 5.0)
+    return min(100 * dt0, dt1, tdist)
+
+
+def _step(f, u, p, t, dt, k1):
+    ks = [k1]
+    for i in range(6):
+        acc = u
+        for j, a in enumerate(A[i]):
+            acc = acc + (dt * a) * ks[j]
+        if i == 5:
+            unew = acc
+            ks.append(f(unew, p, t + dt))
+        else:
+            ks.append(f(acc, p, t + C[i] * dt))
+    return unew, ks
+
+
+def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Options | None = None) -> Solution:
+    """solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat, abstol, reltol) on device tensors.
+
+    f(u, p, t) -> du (out-of-place, ODEFunction{false}); u0 any shape (e.g. (B, N)).
+    Differentiable w.r.t. u0 and p when f is (kanode RHS objects are)."""
+    opt = opt or Tsit5Options()
+    t0, tf = float(tspan[0]), float(tspan[1])
+    if saveat is None:
+        saveat = [t0, tf]
+    elif isinstance(saveat, (int, float)):
+        n = int(round((tf - t0) / saveat))
+        saveat = [t0 + i * saveat for i in range(n + 1)]
+    saveat = [float(s) for s in saveat]
+    out = []
+    si = 0
+    while si < len(saveat) and saveat[si] <= t0 + 1e-14 * max(1.0, abs(t0)):
+        out.append(u0)
+        si += 1
+    t, u = t0, u0
+    k1 = f(u, p, t)
+    if opt.adaptive:
+        dt = opt.dt if opt.dt is not None else _initdt(f, u0, p, t0, tf - t0, opt, k1)
+    else:
+        if opt.dt is None:
+            raise ValueError("fixed-step Tsit5 needs opt.dt")
+        dt = opt.dt
+    qold = opt.qoldinit
+    naccept = nreject = nf = 0
+    for _ in range(opt.maxiters):
+        if t >= tf - 1e-14 * max(1.0, abs(tf)):
+            break
+        dt = min(dt, tf - t)
+        unew, ks = _step(f, u, p, t, dt, k1)
+        nf += 6
+        if opt.adaptive:
+            utilde = dt * sum(b * k for b, k in zip(BTILDE, ks))
+            sk = opt.abstol + torch.maximum(torch.abs(u), torch.abs(unew)) * opt.reltol
+            EEst = rms(utilde.detach() / sk.detach()).item()
+            q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
+            if EEst > 1.0 and dt > opt.dtmin:
+                nreject += 1
+                dt = dt / min(1.0 / opt.qmin, q11 / opt.gamma)
+                continue
+            q = q11 / (qold ** opt.beta2)
+            q = max(1.0 / opt.qmax, min(1.0 / opt.qmin, q / opt.gamma))
+            if 1.0 <= q <= 1.0:   # qsteady_min / qsteady_max
+                q = 1.0
+            dtnew = dt / q if q > 0 else dt * opt.qmax
+            qold = max(EEst, opt.qoldinit)
+        else:
+            dtnew = dt
+        # saveat points inside (t, t + dt] from the dense output
+        tn = t + dt
+        while si < len(saveat) and saveat[si] <= tn + 1e-12 * max(1.0, abs(tn)):
+            ts = saveat[si]
+            if abs(ts - tn) <= 1e-12 * max(1.0, abs(tn)):
+                out.append(unew)
+            else:
+                w = interp_weights((ts - t) / dt)
+                out.append(u + dt * sum(wi * k for wi, k in zip(w, ks)))
+            si += 1
+        t, u, k1 = tn, unew, ks[6]
+        naccept += 1
+        dt = dtnew
+    else:
+        raise RuntimeError("Tsit5: maxiters reached")
+    return Solution(saveat[:len(out)], torch.stack(out), dict(naccept=naccept, nreject=nreject, nf=nf + 1))

@@ -1,0 +1,100 @@
+"""Training loop pieces around the HIP RHS/VJP.
+
+    Adam        — Flux 0.14 legacy `Adam(η, β=(0.9,0.999), ϵ=1e-8)` + `update!`
+                  (LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:167,201;
+                  Flux pinned at Lotka-Volterra/Manifest.toml:841)
+    mse_loss    — `mean(abs2, X .- pred)` (LV_driver_KANODE.jl:197-203, Fisher-KPP_Source.jl:107-109)
+    reg_loss    — L1 + entropy on the flat p (LV_driver_KANODE.jl:187-194)
+    Trainer     — one iteration = forward Tsit5 solve, loss, discrete adjoint
+                  (the HIP VJP per stage), ONE all-reduce of [∂L/∂p ; L] across the
+                  trajectory shards (RCCL over xGMI with backend "nccl"; gloo on CPU),
+                  then the identical Adam step on every rank.
+"""
+from __future__ import annotations
+
+import torch
+
+from .ode import Solution, Tsit5Options, solve
+
+
+class Adam:
+    """Flux.Optimise.Adam (legacy API):  mt = β1 mt + (1-β1) Δ;  vt = β2 vt + (1-β2) Δ²;
+    Δ = mt / (1-β1^t) / (√(vt / (1-β2^t)) + ϵ) · η;  x .-= Δ."""
+
+    def __init__(self, eta: float = 1e-3, beta=(0.9, 0.999), eps: float = 1e-8):
+        self.eta, self.beta, self.eps = eta, beta, eps
+        self.state = {}
+
+    def apply(self, x: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+        b1, b2 = self.beta
+        st = self.state.get(id(x))
+        if st is None:
+            st = [torch.zeros_like(x), torch.zeros_like(x), [b1, b2]]
+            self.state[id(x)] = st
+        mt, vt, bp = st
+        mt.mul_(b1).add_(d, alpha=1 - b1)
+        vt.mul_(b2).addcmul_(d, d, value=1 - b2)
+        step = mt / (1 - bp[0]) / (torch.sqrt(vt / (1 - bp[1])) + self.eps) * self.eta
+        bp[0] *= b1
+        bp[1] *= b2
+        return step
+
+    def update(self, x: torch.Tensor, d: torch.Tensor) -> None:
+        """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ)."""
+        with torch.no_grad():
+            x.sub_(self.apply(x, d))
+
+
+def mse_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    return torch.mean((target - pred) ** 2)
+
+
+def reg_loss(p: torch.Tensor, act_reg: float = 1.0, entropy_reg: float = 1.0) -> torch.Tensor:
+    l1 = torch.abs(p)
+    a = torch.sum(l1)
+    e = l1 / a
+    return a * act_reg + (-torch.sum(e * torch.log(e))) * entropy_reg
+
+
+class Trainer:
+    """KAN-ODE training on a shard of trajectories.
+
+    rhs(u, p, t) -> du must be differentiable (kanode.ChainRHS / FisherKPPRHS are:
+    their backward is the HIP VJP).  `target` has the layout of the saved solution
+    (len(saveat), *u0.shape).  `group` is a torch.distributed process group (or None)."""
+
+    def __init__(self, rhs, u0, tspan, saveat, target, p0, eta: float = 5e-4, solver: Tsit5Options | None = None,
+                 sparse_reg: float = 0.0, group=None):
+        self.rhs, self.u0, self.tspan, self.saveat, self.target = rhs, u0, tspan, saveat, target
+        self.p = p0.detach().clone()
+        self.opt = Adam(eta)
+        self.solver = solver or Tsit5Options()
+        self.sparse_reg = sparse_reg
+        self.group = group
+        self.history = []
+
+    def predict(self, p) -> Solution:
+        return solve(self.rhs, self.u0, self.tspan, p, self.saveat, self.solver)
+
+    def loss_and_grad(self):
+        p = self.p.detach().requires_grad_(True)
+        sol = self.predict(p)
+        loss = mse_loss(sol.u, self.target)
+        if self.sparse_reg:
+            loss = loss + reg_loss(p, self.sparse_reg, 0.0)
+        (g,) = torch.autograd.grad(loss, p)
+        return loss.detach(), g.detach(), sol
+
+    def step(self) -> float:
+        loss, g, _ = self.loss_and_grad()
+        if self.group is not None:
+            import torch.distributed as dist
+            ws = dist.get_world_size(self.group)
+            buf = torch.cat([g.reshape(-1), loss.reshape(1).to(g.dtype)])   # one collective per step
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            buf /= ws
+            g, loss = buf[:-1].reshape(g.shape), buf[-1]
+        self.opt.update(self.p, g)
+        lv = float(loss)
+        self.history.append(lv)
+        return lv

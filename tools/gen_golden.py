@@ -178,5 +178,27 @@ def main() -> None:
     print(f"total {total / 1024:.1f} KiB")
 
 
-if __name__ == "__main__":
+
+
+def gen_lv_truth() -> None:
+    """LV ground truth (LV_driver_KANODE.jl:110-127): lotka!(u, p=[1.5,1,1,3]) from u0=[1,1]
+    over (0, 14), saveat 0.1 (141 samples; the first 35 are the training cut), solved with
+    scipy DOP853 at rtol=atol=1e-12 (the driver uses Tsit5 at 1e-12)."""
+    from scipy.integrate import solve_ivp
+    a, b, c, d = 1.5, 1.0, 1.0, 3.0
+
+    def lotka(t, u):
+        return [a * u[0] - b * u[0] * u[1], c * u[0] * u[1] - d * u[1]]
+
+    t = np.round(np.arange(0, 141) * 0.1, 10)
+    sol = solve_ivp(lotka, (0.0, 14.0), [1.0, 1.0], method="DOP853", t_eval=t, rtol=1e-12, atol=1e-12)
+    np.savez(os.path.join(OUT, "lv_truth.npz"), t=t, X=sol.y, end_index=np.array(35))
+    print("lv_truth: X", sol.y.shape)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lv_truth":
+    gen_lv_truth()
+
+
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
