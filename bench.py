@@ -168,7 +168,7 @@ def main() -> None:
                    "parallelism": f"trajectory-sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "fk_rhs_pair_kernel", "kernel_ms": kern_ms,
+                     "kernel": "fk_rhs_kernel<double,SOFTSIGN,REC_CORR,10>", "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes},
     }
 

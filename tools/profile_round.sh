@@ -1,0 +1,27 @@
+#!/usr/bin/env bash
+# Round profiling on the GPU box -> gpurun_out/profile_$TAG/ (copied into profiles/$TAG by the caller):
+#   1. bench.py (the driver's command)                    -> bench.json
+#   2. rocprofv3 --kernel-trace --stats of the same bench -> kernel_stats.csv
+#   3. separate --pmc passes (no trace domains with PMC):  FETCH_SIZE, WRITE_SIZE, VALU counters
+#   4. tools/traffic.py -> traffic.json (gfx950: FETCH_SIZE x2 for 16-B/lane streaming reads)
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp
+TAG=${TAG:-r01}
+OUT=gpurun_out/profile_$TAG; mkdir -p $OUT
+echo "== bench"
+timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 3; }
+cat $OUT/bench.json
+echo "== kernel trace"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+  python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 3; }
+cp $OUT/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
+for w in fk_rhs fk_vjp; do
+  for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F64"; do
+    n=$(echo $c | cut -d' ' -f1)
+    timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $OUT/pmc_${w}_$n -o run --output-format csv -- \
+      python3 tools/prof_kernel.py --what $w --reps 5 > $OUT/pmc_${w}_$n.log 2>&1 || { echo "pmc $w $n failed"; tail -5 $OUT/pmc_${w}_$n.log; exit 3; }
+  done
+done
+python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
+python3 tools/traffic.py $OUT > $OUT/traffic.json
+cat $OUT/pmc_summary.txt $OUT/traffic.json
