@@ -97,6 +97,8 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vjp", action="store_true")
+    ap.add_argument("--no-table", action="store_true",
+                    help="per-point basis recurrence instead of the piecewise-polynomial table (kan_pp.hip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,7 +116,9 @@ def main() -> None:
     dx = 1.0 / (nx - 1)
     B = args.batch
     kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
-    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev)
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev,
+                              table=False if args.no_table else None)
+    table = rhs.hd.pointwise_table
     p_np = kan1.setup(np.random.default_rng(0))[0].astype(np.float64)
     p = torch.as_tensor(p_np, device=dev)
     u = fk_ics(B, nx, dx, seed=1000 + rank, device=dev)
@@ -149,7 +153,7 @@ def main() -> None:
     value = total_evals / elapsed
     alg_bytes = 8.0 * (rhs.P + B * (nx + nx))       # p + u in + du out, per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.workload, B)
+    traffic = load_traffic(f"{args.workload}:{'table' if table else 'recurrence'}", B)
 
     out = {
         "metric": METRIC,
@@ -165,10 +169,13 @@ def main() -> None:
         "dtype": "f64",
         "data": "synthetic (reference IC family randomised per trajectory; random-init KAN params)",
         "config": {"workload": "fisher_kpp_256", "nx": nx, "batch_per_gpu": B, "kan": "KDense(1,1,10) softsign rbf",
+                   "kan_eval": "piecewise-polynomial table" if table else "basis recurrence",
                    "parallelism": f"trajectory-sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "fk_rhs_kernel<double,SOFTSIGN,REC_CORR,10>", "kernel_ms": kern_ms,
+                     "kernel": ("fk_pp_build_kernel + fk_rhs_pp_kernel<SOFTSIGN,RBF>" if table
+                                else "fk_rhs_kernel<double,SOFTSIGN,REC_CORR,10>"),
+                     "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes},
     }
 

@@ -128,6 +128,17 @@ kanode_status kanode_knots(const kanode_handle* h, int32_t layer, float* grid_ou
  * device calls with batch <= max_batch; required before hipGraph capture). */
 kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
 
+/* Evaluation-strategy switches (no reference counterpart: they select between
+ * HIP kernels computing the same function).
+ *   KANODE_OPT_POINTWISE_TABLE (POINTWISE rhs, f64): 1 = evaluate kan1_.(u)
+ *     through the per-launch piecewise-polynomial table (default where admissible:
+ *     rbf/rswaf basis, even nx), 0 = the per-point basis recurrence.  Setting 1
+ *     where inadmissible returns KANODE_ERR_UNSUPPORTED.
+ * kanode_get_option returns the current value, or -1 for an unknown option. */
+typedef enum { KANODE_OPT_POINTWISE_TABLE = 1 } kanode_option;
+kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
+int64_t kanode_get_option(const kanode_handle* h, int32_t option);
+
 /* --- the RHS and its VJP (device pointers, async on stream) ----------------- */
 /* du[N,B] = f(u[N,B]; p) */
 kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch, void* stream);

@@ -59,6 +59,22 @@ struct LayerConst {
     double Dl[kMaxGrid];      // Δ_j
 };
 
+// Piecewise-polynomial form of a pointwise KDense(1,1,G) (kan_pp.hip): φ(u) on
+// [lo, -lo) cut into `ni` intervals of width w (a power of two), each a degree-9
+// polynomial in t = 2(x - k) - 1, x = u/w + ni/2.  Built per launch from p.
+constexpr int kPPCoef = 10;
+constexpr int kPPChecks = 3;
+constexpr int kPPMaxIntervals = 512;
+struct PPConst {
+    int32_t ni;                       // intervals (power of two, multiple of 16)
+    int32_t enabled;                  // host admissibility (f64, rbf/rswaf, even Nx)
+    double w, inv_w, x0, lo;          // width, 1/w, ni/2, -ni·w/2
+    double tol;                       // acceptance: |poly - direct| <= tol·Σ|terms| at the checks
+    double xi[kPPCoef];               // Chebyshev nodes cos(π(2m+1)/20)
+    double tchk[kPPChecks];           // acceptance points in t
+    double Q[kPPCoef][kPPCoef];       // node values -> monomial coefficients in t
+};
+
 // Every kernel that evaluates fp64 exponentials stages the table in LDS once.
 #define KAN_EXP_TABLE_LDS(name)                                                         \
     __shared__ double name[256];                                                        \

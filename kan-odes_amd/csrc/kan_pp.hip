@@ -1,0 +1,381 @@
+// kan_pp.hip — Fisher-KPP RHS through a piecewise-polynomial form of the pointwise KAN (gfx950).
+//
+//   rc_kanode(u, p, t) = D*lap*u + kan1_.(u)       PDE examples/Fisher-KPP_Source.jl:95-98
+//
+// kan1 is a scalar function of u alone, φ(u) = Σ_j C_j B_j(N(u)) + W swish(u)
+// (kdense.jl:116-124), fixed for the whole launch.  Instead of G basis functions
+// per grid point (2 exp + Horner sweeps + swish ≈ 120 fp64 VALU per point), each
+// launch first tabulates φ as a degree-9 polynomial on each interval of width w
+// (interpolated at Chebyshev nodes from the direct formula, then accepted only if
+// it matches the direct formula to tol·Σ|terms| at three check points), and the
+// RHS kernel evaluates one Horner polynomial from LDS: ≈25 VALU per point, which
+// leaves the kernel bound by HBM (one read of u, one write of du).
+//
+// Points outside the tabulated range, and points in an interval that failed its
+// acceptance test (marked NaN), take the direct formula (pp_direct) — the exact
+// reference arithmetic, register-light, rarely executed.
+//
+// Error: interpolation <= ~1e-16 of Σ|C_j| at w <= 0.16 h (host rule, kanode_abi.cpp);
+// measured <= 1.3e-15 of the scale over 2M points, the fp64 rounding floor of the
+// direct 11-term sum itself.
+#include "kan_common.hpp"
+#include "kan_kernels.hpp"
+#include "kan_lap.hpp"
+
+namespace kan {
+
+constexpr int kPPPerBlock = 16;                      // intervals built per block
+constexpr int kPPEvals = kPPCoef + kPPChecks;        // direct evaluations per interval
+
+// φ(u) by the reference's formula: normalizer, Σ_j C_j basis((n - g_j)/h) in
+// ascending j, + W swish(u).  `sc` returns Σ|terms|.  NORM / BASIS >= 0 fix the
+// normalizer / basis at compile time (-1: runtime switch).
+template <int NORM, int BASIS, typename TC, typename TG>
+__device__ __forceinline__ double pp_direct(const Math<double>& M, const LayerConst& lc, const TC* __restrict__ C,
+                                            const TG* __restrict__ grid, double u, double& sc) {
+    const double n = normalize<NORM, double>(M, lc.norm, u);
+    const int basis = BASIS >= 0 ? BASIS : lc.basis;
+    const double invh = (double)lc.invh;
+    const int G = lc.G;
+    double s = 0.0, a = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < G; ++j) {
+        double aux;
+        const double y = (n - (double)grid[j]) * invh;
+        const double t = (double)C[j] * basis_direct<double>(M, basis, y, aux);
+        s = s + t;
+        a = a + kabs(t);
+    }
+    if (lc.use_base) {
+        const double t = (double)C[G] * swish<double>(M, u);
+        s = s + t;
+        a = a + kabs(t);
+    }
+    sc = a;
+    return s;
+}
+
+// One block builds kPPPerBlock intervals: 13 direct evaluations each (10 nodes +
+// 3 checks), node values -> monomial coefficients (Q, host-built), acceptance.
+// Table layout: [kPPCoef/2][ni] pairs (a_2c, a_2c+1), so lanes at neighbouring
+// intervals read neighbouring 16-byte LDS words.
+__global__ void __launch_bounds__(kBlock)
+fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
+                   const double* __restrict__ p, double* __restrict__ table) {
+    __shared__ double sQ[kPPCoef * kPPCoef];
+    __shared__ double sT[kPPEvals];              // nodes, then check points
+    __shared__ double sC[kMaxGrid + 1];          // C_0..C_{G-1}, W
+    __shared__ double sG[kMaxGrid];              // knots
+    __shared__ double fv[kPPPerBlock][kPPEvals];
+    __shared__ double sv[kPPPerBlock][kPPChecks];
+    __shared__ double cf[kPPPerBlock][kPPCoef];
+    __shared__ int bad[kPPPerBlock];
+    const LayerConst& lc = *lcp;
+    const PPConst& pc = *pcp;
+    const int tid = threadIdx.x;
+    // every constant the block needs, loaded in one round (no dependent global loads later)
+    if (tid < kPPCoef * kPPCoef) sQ[tid] = (&pc.Q[0][0])[tid];
+    if (tid < kPPEvals) sT[tid] = tid < kPPCoef ? pc.xi[tid] : pc.tchk[tid - kPPCoef];
+    if (tid <= lc.G) sC[tid] = (tid < lc.G || lc.use_base) ? p[tid] : 0.0;
+    if (tid < lc.G) sG[tid] = (double)lc.grid[tid];
+    if (tid < kPPPerBlock) bad[tid] = 0;
+    KAN_EXP_TABLE_LDS(tab);   // its __syncthreads publishes the constants too
+    const Math<double> M{tab};
+    const int k0 = blockIdx.x * kPPPerBlock;
+    if (tid < kPPPerBlock * kPPEvals) {
+        const int kl = tid / kPPEvals, m = tid - kl * kPPEvals;
+        const double c = pc.lo + ((double)(k0 + kl) + 0.5) * pc.w;   // exact: w is a power of two
+        double sc;
+        fv[kl][m] = pp_direct<NORM_RUNTIME, -1>(M, lc, sC, sG, ::fma(sT[m], 0.5 * pc.w, c), sc);
+        if (m >= kPPCoef) sv[kl][m - kPPCoef] = sc;
+    }
+    __syncthreads();
+    if (tid < kPPPerBlock * kPPCoef) {
+        // a = Q (f - f_0) + f_0 e_0: the constant is carried exactly, Q only sees the variation
+        const int kl = tid / kPPCoef, i = tid - kl * kPPCoef;
+        const double f0 = fv[kl][0];
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < kPPCoef; ++m) s = ::fma(sQ[i * kPPCoef + m], fv[kl][m] - f0, s);
+        cf[kl][i] = i == 0 ? s + f0 : s;
+    }
+    __syncthreads();
+    if (tid < kPPPerBlock * kPPChecks) {
+        const int kl = tid / kPPChecks, c = tid - kl * kPPChecks;
+        const double t = sT[kPPCoef + c];
+        double y = cf[kl][kPPCoef - 1];
+#pragma unroll
+        for (int i = kPPCoef - 2; i >= 0; --i) y = ::fma(y, t, cf[kl][i]);
+        if (!(kabs(y - fv[kl][kPPCoef + c]) <= pc.tol * sv[kl][c])) bad[kl] = 1;
+    }
+    __syncthreads();
+    if (tid < kPPPerBlock * kPPCoef) {
+        const int kl = tid / kPPCoef, i = tid - kl * kPPCoef;
+        const int64_t k = k0 + kl;
+        table[((int64_t)(i >> 1) * pc.ni + k) * 2 + (i & 1)] = bad[kl] ? __builtin_nan("") : cf[kl][i];
+    }
+}
+
+// φ(u) from the LDS table; ok = false outside [lo, -lo) or in a rejected interval.
+__device__ __forceinline__ double pp_eval(const double2* __restrict__ tl, int ni, double inv_w, double x0, double u,
+                                          bool& ok) {
+    const double x = ::fma(u, inv_w, x0);
+    const bool in = (x >= 0.0) && (x < (double)ni);     // false for NaN
+    const double xc = in ? x : 0.0;
+    const double fl = __builtin_floor(xc);
+    const int k = (int)fl;
+    const double t = ::fma(2.0, xc - fl, -1.0);           // exact
+    const double2* __restrict__ e = tl + k;
+    const double2 c8 = e[4 * ni], c6 = e[3 * ni], c4 = e[2 * ni], c2 = e[ni], c0 = e[0];
+    double y = ::fma(c8.y, t, c8.x);
+    y = ::fma(y, t, c6.y);
+    y = ::fma(y, t, c6.x);
+    y = ::fma(y, t, c4.y);
+    y = ::fma(y, t, c4.x);
+    y = ::fma(y, t, c2.y);
+    y = ::fma(y, t, c2.x);
+    y = ::fma(y, t, c0.y);
+    y = ::fma(y, t, c0.x);
+    ok = in && (y == y);
+    return y;
+}
+
+// RHS of the point pair (i, i+1) of one trajectory row `ub` -> `db`.
+template <int NORM, int BASIS>
+__device__ __forceinline__ void pp_pair_finish(const Math<double>& M, const LayerConst& lc,
+                                               const double* __restrict__ p, const double2* __restrict__ tl, int ni,
+                                               double inv_w, double x0, double cd, double co, int Nx, int i,
+                                               double2 v, double um, double up, double* __restrict__ db) {
+    bool ok0, ok1;
+    double k0 = pp_eval(tl, ni, inv_w, x0, v.x, ok0);
+    double k1 = pp_eval(tl, ni, inv_w, x0, v.y, ok1);
+#ifndef KAN_PP_NO_SLOW
+    if (__builtin_expect(!(ok0 && ok1), 0)) {
+        double sc;
+        if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v.x, sc);
+        if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v.y, sc);
+    }
+#endif
+    double l0, l1;
+    if (Nx >= 4) {
+        lap_pair<double>(um, v.x, v.y, up, i, Nx, cd, co, l0, l1);
+    } else {
+        l0 = lap3<double>(um, v.x, v.y, i, Nx, cd, co);
+        l1 = lap3<double>(v.x, v.y, up, i + 1, Nx, cd, co);
+    }
+    double2 o;
+    o.x = l0 + k0;
+    o.y = l1 + k1;
+    *reinterpret_cast<double2*>(db + i) = o;
+}
+
+// Point pairs (Nx even): 2^tpt_log2 threads per trajectory, 256 >> tpt_log2
+// trajectories per block, blocks grid-stride over trajectories.  SHORT (Nx/2 <=
+// 256): one pair per thread per trajectory, two trajectories per iteration (both
+// rows' loads issued before either is used).  Dynamic LDS: the table,
+// [kPPCoef/2][ni] double2.
+#ifndef KAN_PP_WPE
+#define KAN_PP_WPE 1
+#endif
+#ifndef KAN_PP_UNR
+#define KAN_PP_UNR 2
+#endif
+template <int NORM, int BASIS, bool SHORT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+fk_rhs_pp_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                 const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co, int Nx,
+                 int tpt_log2, const double* __restrict__ u, double* __restrict__ du, int64_t B) {
+    extern __shared__ double2 tl[];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    const Math<double> M{tab};
+    const LayerConst& lc = *lcp;
+    const int tpt = 1 << tpt_log2;
+    const int tpb = kBlock >> tpt_log2;
+    const int lt = threadIdx.x & (tpt - 1);
+    const int units = Nx >> 1;
+    const int64_t b0 = (int64_t)blockIdx.x * tpb + (threadIdx.x >> tpt_log2);
+    const int64_t bstride = (int64_t)gridDim.x * tpb;
+    if constexpr (SHORT) {
+        if (lt >= units) return;
+        const int i = 2 * lt;
+        const int im = i > 0 ? i - 1 : Nx - 1;
+        const int ip = i + 2 < Nx ? i + 2 : 0;
+        int64_t b = b0;
+        for (; KAN_PP_UNR == 2 && b + bstride < B; b += 2 * bstride) {
+            const double* __restrict__ ua = u + b * Nx;
+            const double* __restrict__ uc = ua + bstride * Nx;
+            const double2 va = *reinterpret_cast<const double2*>(ua + i);
+            const double2 vc = *reinterpret_cast<const double2*>(uc + i);
+            const double uma = ua[im], upa = ua[ip], umc = uc[im], upc = uc[ip];
+            pp_pair_finish<NORM, BASIS>(M, lc, p, tl, ni, inv_w, x0, cd, co, Nx, i, va, uma, upa, du + b * Nx);
+            pp_pair_finish<NORM, BASIS>(M, lc, p, tl, ni, inv_w, x0, cd, co, Nx, i, vc, umc, upc,
+                                        du + (b + bstride) * Nx);
+        }
+        for (; b < B; b += bstride) {
+            const double* __restrict__ ua = u + b * Nx;
+            pp_pair_finish<NORM, BASIS>(M, lc, p, tl, ni, inv_w, x0, cd, co, Nx, i,
+                                        *reinterpret_cast<const double2*>(ua + i), ua[im], ua[ip], du + b * Nx);
+        }
+        return;
+    }
+    for (int64_t b = b0; b < B; b += bstride) {
+        const double* __restrict__ ub = u + b * Nx;
+        for (int q = lt; q < units; q += tpt) {
+            const int i = 2 * q;
+            pp_pair_finish<NORM, BASIS>(M, lc, p, tl, ni, inv_w, x0, cd, co, Nx, i,
+                                        *reinterpret_cast<const double2*>(ub + i), ub[i > 0 ? i - 1 : Nx - 1],
+                                        ub[i + 2 < Nx ? i + 2 : 0], du + b * Nx);
+        }
+    }
+}
+
+// Whole-wave rotations (DPP wave_ror:1 / wave_rol:1, GFX9 family): lane i receives
+// lane (i-1) mod 64 / (i+1) mod 64.  Two 32-bit moves per double, no LDS.
+__device__ __forceinline__ double wave_ror1(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x13C, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x13C, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_rol1(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x134, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x134, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+typedef double kd2 __attribute__((ext_vector_type(2)));
+
+#ifndef KAN_PP_NT
+#define KAN_PP_NT 1
+#endif
+__device__ __forceinline__ kd2 ld_stream(const double* p) {
+#if KAN_PP_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const kd2*>(p));
+#else
+    return *reinterpret_cast<const kd2*>(p);
+#endif
+}
+__device__ __forceinline__ void st_stream(double* p, kd2 v) {
+#if KAN_PP_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<kd2*>(p));
+#else
+    *reinterpret_cast<kd2*>(p) = v;
+#endif
+}
+
+// Nx = 128·NP: one wave per trajectory row.  Lane l holds the pairs (128k + 2l,
+// 128k + 2l + 1), k < NP, each a fully coalesced 1 KB wave load; the stencil
+// neighbours u[128k + 2l - 1] and u[128k + 2l + 2] are the neighbouring lanes'
+// values (wave rotations), the periodic wrap included: u is read from HBM once, by
+// streaming (nontemporal) loads, and du written once by streaming stores.
+template <int NORM, int BASIS, int NP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                      const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
+                      const double* __restrict__ u, double* __restrict__ du, int64_t B) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    const Math<double> M{tab};
+    const LayerConst& lc = *lcp;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
+    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+        const double* __restrict__ ub = u + b * Nx;
+        double* __restrict__ db = du + b * Nx;
+        kd2 v[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[k] = ld_stream(ub + 128 * k + 2 * lane);
+        double rr[NP], rl[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            rr[k] = wave_ror1(v[k].y);
+            rl[k] = wave_rol1(v[k].x);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+            const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+            const int i = 128 * k + 2 * lane;
+            bool ok0, ok1;
+            double k0 = pp_eval(tl, ni, inv_w, x0, v[k].x, ok0);
+            double k1 = pp_eval(tl, ni, inv_w, x0, v[k].y, ok1);
+            if (__builtin_expect(!(ok0 && ok1), 0)) {
+                double sc;
+                if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[k].x, sc);
+                if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[k].y, sc);
+            }
+            double l0, l1;
+            lap_pair<double>(um, v[k].x, v[k].y, up, i, Nx, cd, co, l0, l1);
+            kd2 o;
+            o.x = l0 + k0;
+            o.y = l1 + k1;
+            st_stream(db + i, o);
+        }
+    }
+}
+
+// Resident blocks per CU x CUs (one wave of blocks: each block stages the table once).
+#ifndef KAN_PP_GRIDMULT
+#define KAN_PP_GRIDMULT 1
+#endif
+template <typename K>
+static int pp_grid_cap(K kernel, size_t lds) {
+    int dev = 0, cus = 256, nb = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, lds) != hipSuccess || nb < 1) nb = 4;
+    return nb * cus * KAN_PP_GRIDMULT;
+}
+
+hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
+                              double* table, hipStream_t st) {
+    if (hpc.ni <= 0 || hpc.ni % kPPPerBlock || hpc.ni > kPPMaxIntervals) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fk_pp_build_kernel, dim3(hpc.ni / kPPPerBlock), dim3(kBlock), 0, st, lc, pc, p, table);
+    return hipGetLastError();
+}
+
+hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
+                            double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
+                            hipStream_t st) {
+    if (Nx < 2 || (Nx & 1)) return hipErrorInvalidValue;
+    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, st);
+    if (e != hipSuccess) return e;
+    const int units = Nx / 2;
+    const int tl = ceil_log2(units < kBlock ? units : kBlock);
+    const int tpb = kBlock >> tl;
+    const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+#define KAN_PP_WAVE(NORM, BASIS, NP)                                                                             \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
+        const int grid = grid_for(B, kBlock / kWave, cap);                                                       \
+        hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B);                  \
+    } while (0)
+#define KAN_PP_PAIR(NORM, BASIS, SHORT)                                                                          \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_rhs_pp_kernel<NORM, BASIS, SHORT>, lds);                                 \
+        const int grid = grid_for(B, tpb, cap);                                                                  \
+        hipLaunchKernelGGL((fk_rhs_pp_kernel<NORM, BASIS, SHORT>), dim3(grid), dim3(kBlock), lds, st, lc, p,     \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, Nx, tl, u, du, B);          \
+    } while (0)
+#define KAN_PP_GO(NORM, BASIS)                                                                                   \
+    do {                                                                                                         \
+        if (Nx == 256) KAN_PP_WAVE(NORM, BASIS, 2);                                                              \
+        else if (Nx == 128) KAN_PP_WAVE(NORM, BASIS, 1);                                                         \
+        else if (Nx == 512) KAN_PP_WAVE(NORM, BASIS, 4);                                                         \
+        else if (units <= kBlock) KAN_PP_PAIR(NORM, BASIS, true);                                                \
+        else KAN_PP_PAIR(NORM, BASIS, false);                                                                    \
+    } while (0)
+    if (hlc.basis == BASIS_RBF && hlc.norm == NORM_SOFTSIGN) KAN_PP_GO(NORM_SOFTSIGN, BASIS_RBF);
+    else if (hlc.basis == BASIS_RBF && hlc.norm == NORM_TANH_FAST) KAN_PP_GO(NORM_TANH_FAST, BASIS_RBF);
+    else KAN_PP_GO(NORM_RUNTIME, -1);
+#undef KAN_PP_GO
+#undef KAN_PP_PAIR
+#undef KAN_PP_WAVE
+    return hipGetLastError();
+}
+
+}  // namespace kan

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 
 #include "kan_device.hpp"
 #include "kan_kernels.hpp"
@@ -48,6 +49,11 @@ struct kanode_handle {
     void* ws = nullptr;               // chain activations / gradients
     size_t ws_bytes = 0;
     int64_t reserved_batch = 0;
+    // piecewise-polynomial pointwise RHS (kan_pp.hip)
+    kan::PPConst hpc{};
+    kan::PPConst* dpc = nullptr;
+    double* dtable = nullptr;
+    bool pp_on = false;
     // host staging (device buffers) for *_host calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -148,6 +154,52 @@ kanode_status make_layer_const(kanode_handle* h, const kanode_layer_spec& s, int
         if (ok) lc.path = exact ? kan::PATH_REC : kan::PATH_REC_CORR;
     }
     return KANODE_OK;
+}
+
+// Piecewise-polynomial table constants for a pointwise KDense(1,1,G) (kan_pp.hip).
+// Interval width: the largest power of two <= 0.16·h_u, h_u the knot spacing seen
+// in u (h / max N'(u)), capped at 1/16; with degree 9 the Chebyshev interpolation
+// error of a Gaussian of width h_u is then <= ~1e-16 of |C|.  ni <= 512 intervals
+// centred on 0 (so softsign's kink at 0 is an interval edge).
+void make_pp_const(const LayerConst& lc, int dtype, int64_t nx, kan::PPConst& pc) {
+    std::memset(&pc, 0, sizeof(pc));
+    pc.enabled = dtype == KANODE_F64 && (lc.basis == KANODE_BASIS_RBF || lc.basis == KANODE_BASIS_RSWAF) &&
+                 nx >= 2 && nx % 2 == 0;
+    const double slope = (lc.norm == KANODE_NORM_SIGMOID || lc.norm == KANODE_NORM_SIGMOID_FAST) ? 0.25 : 1.0;
+    const double hu = (1.0 / (double)lc.invh) / slope;
+    double w = 1.0 / 16.0;
+    while (w > 0.16 * hu && w > 0x1p-20) w *= 0.5;
+    int ni = kan::kPPMaxIntervals;
+    while (ni > 16 && ni * w > 8.0) ni >>= 1;   // domain at most [-4, 4)
+    pc.ni = ni;
+    pc.w = w;
+    pc.inv_w = 1.0 / w;
+    pc.x0 = ni / 2;
+    pc.lo = -(ni / 2) * w;
+    pc.tol = 2e-14;
+    const int N = kan::kPPCoef;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int m = 0; m < N; ++m) pc.xi[m] = (double)std::cos(pi * (2 * m + 1) / (2.0L * N));
+    pc.tchk[0] = -1.0;
+    pc.tchk[1] = 0.0;
+    pc.tchk[2] = 1.0;
+    // Q = (Chebyshev -> monomial) · DCT, in long double
+    long double T[kan::kPPCoef][kan::kPPCoef] = {};
+    T[0][0] = 1;
+    T[1][1] = 1;
+    for (int l = 2; l < N; ++l) {
+        for (int i = 1; i < N; ++i) T[l][i] = 2 * T[l - 1][i - 1];
+        for (int i = 0; i < N; ++i) T[l][i] -= T[l - 2][i];
+    }
+    for (int i = 0; i < N; ++i)
+        for (int m = 0; m < N; ++m) {
+            long double s = 0;
+            for (int l = 0; l < N; ++l) {
+                const long double d = (2.0L / N) * std::cos(pi * l * (2 * m + 1) / (2.0L * N)) * (l == 0 ? 0.5L : 1.0L);
+                s += T[l][i] * d;
+            }
+            pc.Q[i][m] = (double)s;
+        }
 }
 
 int64_t layer_P(const LayerConst& lc) {
@@ -256,6 +308,13 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
     if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
         const double dx2 = h->spec.dx * h->spec.dx;
         const T cd = (T)(h->spec.diffusion * (-2.0 / dx2)), co = (T)(h->spec.diffusion * (1.0 / dx2));
+        if constexpr (std::is_same<T, double>::value) {
+            if (h->pp_on) {
+                HIP_TRY(h, kan::launch_fk_rhs_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co, (int)h->spec.nx, u, du,
+                                                 B, st));
+                return KANODE_OK;
+            }
+        }
         HIP_TRY(h, kan::launch_fk_rhs<T>(h->hlc[0], h->dlc, p, cd, co, (int)h->spec.nx, u, du, B, st));
         return KANODE_OK;
     }
@@ -414,6 +473,16 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
         return bail(fail(h, KANODE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)));
     if ((e = hipMemcpy(h->dlc, h->hlc, sizeof(LayerConst) * h->n_layers, hipMemcpyHostToDevice)) != hipSuccess)
         return bail(fail(h, KANODE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)));
+    if (spec->rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN) {
+        make_pp_const(h->hlc[0], spec->dtype, spec->nx, h->hpc);
+        if (h->hpc.enabled) {
+            if ((e = hipMalloc(&h->dpc, sizeof(kan::PPConst))) != hipSuccess ||
+                (e = hipMemcpy(h->dpc, &h->hpc, sizeof(kan::PPConst), hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMalloc(&h->dtable, sizeof(double) * kan::kPPCoef * h->hpc.ni)) != hipSuccess)
+                return bail(fail(h, KANODE_ERR_HIP, std::string("pp table: ") + hipGetErrorString(e)));
+            h->pp_on = true;
+        }
+    }
     h->slab_bytes = (size_t)kSlabBlocks * (size_t)std::max(h->max_layer_P, 1) * h->esize;
     if ((e = hipMalloc(&h->slab, h->slab_bytes)) != hipSuccess)
         return bail(fail(h, KANODE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)));
@@ -428,6 +497,8 @@ void kanode_destroy(kanode_handle* h) {
     if (h->slab) (void)hipFree(h->slab);
     if (h->ws) (void)hipFree(h->ws);
     if (h->stage) (void)hipFree(h->stage);
+    if (h->dpc) (void)hipFree(h->dpc);
+    if (h->dtable) (void)hipFree(h->dtable);
     delete h;
 }
 
@@ -461,6 +532,28 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch) {
     }
     h->reserved_batch = std::max(h->reserved_batch, max_batch);
     return KANODE_OK;
+}
+
+kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value) {
+    if (!h) return KANODE_ERR_INVALID_ARG;
+    switch (option) {
+    case KANODE_OPT_POINTWISE_TABLE:
+        if (value != 0 && value != 1) return fail(h, KANODE_ERR_INVALID_ARG, "POINTWISE_TABLE takes 0 or 1");
+        if (value == 1 && !h->hpc.enabled)
+            return fail(h, KANODE_ERR_UNSUPPORTED,
+                        "POINTWISE_TABLE needs a pointwise f64 RHS with rbf/rswaf basis and even nx");
+        h->pp_on = value == 1;
+        return KANODE_OK;
+    }
+    return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
+}
+
+int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
+    if (!h) return -1;
+    switch (option) {
+    case KANODE_OPT_POINTWISE_TABLE: return h->pp_on ? 1 : 0;
+    }
+    return -1;
 }
 
 kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch, void* stream) {

@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkanode.so")
+LIB_PATH = os.environ.get("KANODE_LIB") or os.path.join(_HERE, "libkanode.so")   # override: experiments only
 
 MAX_LAYERS = 8
 MAX_GRID = 32
@@ -48,6 +48,8 @@ class SpecC(C.Structure):
 # (name, restype, argtypes) for every symbol include/kanode.h declares
 _P = C.c_void_p
 _H = C.c_void_p
+OPT_POINTWISE_TABLE = 1   # kanode_option
+
 SIGNATURES = [
     ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),
     ("kanode_destroy", None, [_H]),
@@ -59,6 +61,8 @@ SIGNATURES = [
     ("kanode_state_length", C.c_int64, [_H]),
     ("kanode_knots", C.c_int, [_H, C.c_int32, _P]),
     ("kanode_reserve", C.c_int, [_H, C.c_int64]),
+    ("kanode_set_option", C.c_int, [_H, C.c_int32, C.c_int64]),
+    ("kanode_get_option", C.c_int64, [_H, C.c_int32]),
     ("kanode_rhs", C.c_int, [_H, _P, _P, _P, C.c_int64, _P]),
     ("kanode_vjp", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64, _P]),
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),

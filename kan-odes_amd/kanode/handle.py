@@ -123,6 +123,16 @@ class KanodeHandle:
     def reserve(self, max_batch: int) -> None:
         L.check(L.lib().kanode_reserve(self._h, int(max_batch)), self._h, "kanode_reserve")
 
+    @property
+    def pointwise_table(self) -> bool:
+        """POINTWISE rhs: kan1_.(u) through the per-launch polynomial table (kan_pp.hip)."""
+        return L.lib().kanode_get_option(self._h, L.OPT_POINTWISE_TABLE) == 1
+
+    @pointwise_table.setter
+    def pointwise_table(self, on: bool) -> None:
+        L.check(L.lib().kanode_set_option(self._h, L.OPT_POINTWISE_TABLE, 1 if on else 0), self._h,
+                "kanode_set_option")
+
     # -- RHS -----------------------------------------------------------------
     def rhs(self, p: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """du (B, N_out) = f(u (B, N); p)."""

@@ -85,7 +85,8 @@ def fisher_kpp_laplacian(nx: int, dx: float) -> np.ndarray:
 class FisherKPPRHS:
     """rc_kanode: du = D * lap * u + KDense(1,1,G).(u) pointwise, u (B, Nx) [Julia u[Nx, B]]."""
 
-    def __init__(self, kan1, nx: int, dx: float, D: float = 0.01, dtype=torch.float64, device=None):
+    def __init__(self, kan1, nx: int, dx: float, D: float = 0.01, dtype=torch.float64, device=None,
+                 table: bool | None = None):
         layer = kan1[0] if hasattr(kan1, "layers") else kan1
         cfg = layer.cfg if hasattr(layer, "cfg") else layer
         if not isinstance(cfg, LayerCfg) or cfg.in_dims != 1 or cfg.out_dims != 1:
@@ -93,6 +94,8 @@ class FisherKPPRHS:
         self.cfg, self.nx, self.dx, self.D = cfg, int(nx), float(dx), float(D)
         self.hd = KanodeHandle([cfg], dtype=dtype, rhs_kind="pointwise_periodic_laplacian", nx=nx,
                                diffusion=D, dx=dx, device=device)
+        if table is not None:   # None: the library default (table where admissible)
+            self.hd.pointwise_table = table
         self.P, self.N = self.hd.P, self.hd.N
 
     def __call__(self, u: torch.Tensor, p: torch.Tensor, t=None) -> torch.Tensor:

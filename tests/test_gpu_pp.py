@@ -1,0 +1,137 @@
+"""Piecewise-polynomial Fisher-KPP RHS (kan_pp.hip) vs the CPU oracle.
+
+The table path evaluates kan1_.(u) (PDE examples/Fisher-KPP_Source.jl:96) from a
+per-launch degree-9 interpolant of the reference formula; these tests pin it to the
+oracle's direct formula over dense sweeps of u (interval edges, the kink of
+softsign at 0, the table's range limits, out-of-range and non-finite inputs), for
+every normalizer and the rbf / rswaf bases, and check that disabling it selects
+the per-point recurrence kernels.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import RTOL, assert_close, device, fk_scale, t
+from oracle import oracle as O
+
+import kanode
+from kanode import KanodeError
+
+pytestmark = pytest.mark.gpu
+
+# KAN-only tolerance: D = 0 makes du = kan1_.(u) exactly; the table must match the
+# direct formula to 1e-14 of Σ|C_j| + |W||u| (measured ~1.3e-15, the rounding floor).
+PP_RTOL = 1e-14
+
+
+def rhs_for(nx, normalizer="softsign", G=10, basis="rbf", D=0.0, dx=0.01, table=None, dtype=torch.float64):
+    kan1 = kanode.Chain(kanode.KDense(1, 1, G, normalizer=normalizer, basis_func=basis, allow_fast_activation=False))
+    return kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=dtype, device=device(), table=table)
+
+
+def sweep(nx=256, lo=-6.0, hi=6.0, n=256 * 64, seed=0):
+    """u covering [lo, hi] densely plus every interval edge of a w = 2^-k grid."""
+    rng = np.random.default_rng(seed)
+    edges = np.arange(-4.0, 4.0 + 1e-12, 1.0 / 128)
+    pts = np.concatenate([np.linspace(lo, hi, n - 6 * edges.size - 8), edges, np.nextafter(edges, -np.inf),
+                          np.nextafter(edges, np.inf), edges + 1e-9, edges - 1e-9, rng.uniform(-1, 1, edges.size),
+                          [0.0, -0.0, 4.0, -4.0, np.nextafter(4.0, 0), np.nextafter(-4.0, -np.inf), 1e-300, -1e-300]])
+    pts = np.resize(pts, (pts.size + nx - 1) // nx * nx)
+    return pts.reshape(-1, nx)
+
+
+def kan_scale(p, u):
+    return np.sum(np.abs(p[:-1])) + abs(p[-1]) * np.abs(u)
+
+
+def test_table_default_and_option_errors():
+    assert rhs_for(256).hd.pointwise_table
+    assert not rhs_for(256, table=False).hd.pointwise_table
+    assert not rhs_for(255).hd.pointwise_table                      # odd nx: recurrence kernels
+    assert not rhs_for(256, basis="iqf").hd.pointwise_table         # iqf: poles near the axis
+    assert not rhs_for(256, dtype=torch.float32).hd.pointwise_table
+    with pytest.raises(KanodeError):
+        rhs_for(256, dtype=torch.float32, table=True)
+    with pytest.raises(KanodeError):
+        rhs_for(255, table=True)
+
+
+@pytest.mark.parametrize("normalizer,basis,G", [
+    ("softsign", "rbf", 10), ("tanh_fast", "rbf", 5), ("tanh", "rbf", 10), ("sigmoid", "rbf", 10),
+    ("sigmoid_fast", "rbf", 7), ("identity", "rbf", 10), ("softsign", "rswaf", 10), ("softsign", "rbf", 32),
+    ("tanh_fast", "rbf", 2),
+])
+def test_table_matches_direct_formula(normalizer, basis, G):
+    rng = np.random.default_rng(G * 31 + len(normalizer))
+    spec = O.LayerSpec(1, 1, G, normalizer, basis)
+    p = rng.uniform(-1, 1, G + 1)
+    u = sweep()
+    rhs = rhs_for(256, normalizer, G, basis)
+    assert rhs.hd.pointwise_table
+    got = rhs.rhs(t(u), t(p))
+    ref = O.fk_rhs(spec, p, 0.0, 0.01, u)
+    assert_close(got, ref, kan_scale(p, u), PP_RTOL, f"{normalizer}/{basis}/G={G}")
+
+
+def test_table_and_recurrence_agree_with_laplacian():
+    rng = np.random.default_rng(5)
+    nx, dx, D = 256, 1.0 / 255, 0.01
+    p = rng.uniform(-1, 1, 11)
+    u = rng.uniform(-0.2, 1.2, (64, nx))
+    ref = O.fk_rhs(O.LayerSpec(1, 1, 10, "softsign"), p, D, dx, u)
+    sc = fk_scale(p, D, dx, u)
+    for table in (True, False):
+        rhs = rhs_for(nx, D=D, dx=dx, table=table)
+        assert rhs.hd.pointwise_table == table
+        assert_close(rhs.rhs(t(u), t(p)), ref, sc, RTOL[torch.float64], f"table={table}")
+
+
+def test_table_out_of_range_and_nonfinite():
+    """|u| >= 4 is outside the table: the kernel's direct slow path (and NaN stays NaN)."""
+    rng = np.random.default_rng(9)
+    p = rng.uniform(-1, 1, 11)
+    u = rng.uniform(4.0, 40.0, (3, 256)) * rng.choice([-1.0, 1.0], (3, 256))
+    u[1, 7] = np.nan
+    u[2, 100] = np.inf
+    u[2, 101] = -np.inf
+    rhs = rhs_for(256)
+    got = rhs.rhs(t(u), t(p)).cpu().numpy()
+    ref = O.fk_rhs(O.LayerSpec(1, 1, 10, "softsign"), p, 0.0, 0.01, u)
+    fin = np.isfinite(ref)          # 0·lap of an inf neighbour is NaN in both
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert fin.sum() > 700
+    assert_close(got[fin], ref[fin], kan_scale(p, u[fin]), PP_RTOL, "out of range")
+
+
+def test_table_rebuilt_per_launch():
+    """Same handle, new p: the table is rebuilt from p on every call."""
+    rng = np.random.default_rng(13)
+    u = rng.uniform(-1, 1.5, (8, 256))
+    rhs = rhs_for(256)
+    spec = O.LayerSpec(1, 1, 10, "softsign")
+    for k in range(3):
+        p = rng.uniform(-1, 1, 11) * (k + 1)
+        assert_close(rhs.rhs(t(u), t(p)), O.fk_rhs(spec, p, 0.0, 0.01, u), kan_scale(p, u), PP_RTOL, f"p#{k}")
+
+
+def test_table_graph_capture():
+    """Build + evaluate are two launches with no allocation: capturable."""
+    rng = np.random.default_rng(17)
+    nx, B = 256, 32
+    p = t(rng.uniform(-1, 1, 11))
+    u = t(rng.uniform(0, 1, (B, nx)))
+    rhs = rhs_for(nx, D=0.01, dx=1.0 / 255)
+    out = torch.empty_like(u)
+    rhs.hd.reserve(B)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        rhs.rhs(u, p, out)     # warm-up on the capture stream
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rhs.rhs(u, p, out)
+    p.mul_(0.5)
+    g.replay()
+    torch.cuda.synchronize()
+    ref = O.fk_rhs(O.LayerSpec(1, 1, 10, "softsign"), p.cpu().numpy(), 0.01, 1.0 / 255, u.cpu().numpy())
+    assert_close(out, ref, fk_scale(p.cpu().numpy(), 0.01, 1.0 / 255, u.cpu().numpy()), RTOL[torch.float64], "graph")
