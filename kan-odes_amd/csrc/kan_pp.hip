@@ -22,9 +22,11 @@
 #include "kan_kernels.hpp"
 #include "kan_lap.hpp"
 
+#include <cstdlib>
+
 namespace kan {
 
-constexpr int kPPPerBlock = 16;                      // intervals built per block
+constexpr int kPPPerBlock = 4;                       // intervals built per block (13·4·4 = 208 lanes)
 constexpr int kPPEvals = kPPCoef + kPPChecks;        // direct evaluations per interval
 
 // φ(u) by the reference's formula: normalizer, Σ_j C_j basis((n - g_j)/h) in
@@ -57,6 +59,9 @@ __device__ __forceinline__ double pp_direct(const Math<double>& M, const LayerCo
 
 // One block builds kPPPerBlock intervals: 13 direct evaluations each (10 nodes +
 // 3 checks), node values -> monomial coefficients (Q, host-built), acceptance.
+// Each evaluation is split over a quad of lanes (terms j ≡ sub mod 4, combined in
+// a fixed order) so the dependent chain is ~3 exponentials, not G+1: the build is
+// latency-bound and sits between two dependent launches.
 // Table layout: [kPPCoef/2][ni] pairs (a_2c, a_2c+1), so lanes at neighbouring
 // intervals read neighbouring 16-byte LDS words.
 __global__ void __launch_bounds__(kBlock)
@@ -73,21 +78,45 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
     const LayerConst& lc = *lcp;
     const PPConst& pc = *pcp;
     const int tid = threadIdx.x;
+    const int G = lc.G;
     // every constant the block needs, loaded in one round (no dependent global loads later)
     if (tid < kPPCoef * kPPCoef) sQ[tid] = (&pc.Q[0][0])[tid];
     if (tid < kPPEvals) sT[tid] = tid < kPPCoef ? pc.xi[tid] : pc.tchk[tid - kPPCoef];
-    if (tid <= lc.G) sC[tid] = (tid < lc.G || lc.use_base) ? p[tid] : 0.0;
-    if (tid < lc.G) sG[tid] = (double)lc.grid[tid];
+    if (tid <= G) sC[tid] = (tid < G || lc.use_base) ? p[tid] : 0.0;
+    if (tid < G) sG[tid] = (double)lc.grid[tid];
     if (tid < kPPPerBlock) bad[tid] = 0;
     KAN_EXP_TABLE_LDS(tab);   // its __syncthreads publishes the constants too
     const Math<double> M{tab};
     const int k0 = blockIdx.x * kPPPerBlock;
-    if (tid < kPPPerBlock * kPPEvals) {
-        const int kl = tid / kPPEvals, m = tid - kl * kPPEvals;
+    {
+        // evaluation e = tid / 4 (all lanes of a quad take part in the shuffles)
+        const int e = tid >> 2, sub = tid & 3;
+        const bool live = e < kPPPerBlock * kPPEvals;
+        const int kl = live ? e / kPPEvals : 0, m = live ? e - kl * kPPEvals : 0;
         const double c = pc.lo + ((double)(k0 + kl) + 0.5) * pc.w;   // exact: w is a power of two
-        double sc;
-        fv[kl][m] = pp_direct<NORM_RUNTIME, -1>(M, lc, sC, sG, ::fma(sT[m], 0.5 * pc.w, c), sc);
-        if (m >= kPPCoef) sv[kl][m - kPPCoef] = sc;
+        const double u = ::fma(sT[m], 0.5 * pc.w, c);
+        const double n = normalize<NORM_RUNTIME, double>(M, lc.norm, u);
+        const double invh = (double)lc.invh;
+        double s = 0.0, a = 0.0;
+        for (int j = sub; j <= G; j += 4) {
+            double t;
+            if (j < G) {
+                double aux;
+                t = sC[j] * basis_direct<double>(M, lc.basis, (n - sG[j]) * invh, aux);
+            } else {
+                t = lc.use_base ? sC[G] * swish<double>(M, u) : 0.0;
+            }
+            s = s + t;
+            a = a + kabs(t);
+        }
+        s = s + __shfl_xor(s, 1, 4);
+        a = a + __shfl_xor(a, 1, 4);
+        s = s + __shfl_xor(s, 2, 4);
+        a = a + __shfl_xor(a, 2, 4);
+        if (live && sub == 0) {
+            fv[kl][m] = s;
+            if (m >= kPPCoef) sv[kl][m - kPPCoef] = a;
+        }
     }
     __syncthreads();
     if (tid < kPPPerBlock * kPPCoef) {
@@ -275,18 +304,28 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                       const double* __restrict__ u, double* __restrict__ du, int64_t B) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
+    int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    // the first row's loads are in flight while the block stages its table
+    kd2 v[NP];
+    if (b < B) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[k] = ld_stream(u + b * Nx + 128 * k + 2 * lane);
+    }
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
-        const double* __restrict__ ub = u + b * Nx;
-        double* __restrict__ db = du + b * Nx;
-        kd2 v[NP];
+    for (; b < B; b += rstride) {
+        // software pipeline: the next row's loads are issued before this row's math
+        const int64_t bn = b + rstride;
+        kd2 vn[NP];
+        if (bn < B) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = ld_stream(ub + 128 * k + 2 * lane);
+            for (int k = 0; k < NP; ++k) vn[k] = ld_stream(u + bn * Nx + 128 * k + 2 * lane);
+        }
+        double* __restrict__ db = du + b * Nx;
         double rr[NP], rl[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -313,19 +352,21 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             o.y = l1 + k1;
             st_stream(db + i, o);
         }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[k] = vn[k];
     }
 }
 
-// Resident blocks per CU x CUs (one wave of blocks: each block stages the table once).
-#ifndef KAN_PP_GRIDMULT
-#define KAN_PP_GRIDMULT 1
-#endif
+// Persistent grid: min(resident blocks per CU, 4) x CUs, each block stages the table
+// once.  4 blocks (16 waves) per CU streamed fastest in the grid sweep (tools/pp_grid.sh:
+// 98.7 us at 1024 blocks vs 101.4 us at the 6-block occupancy limit); the nontemporal
+// copy microbenchmark peaks at the same shape.  KANODE_PP_GRID overrides (tuning only).
 template <typename K>
 static int pp_grid_cap(K kernel, size_t lds) {
     int dev = 0, cus = 256, nb = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, lds) != hipSuccess || nb < 1) nb = 4;
-    return nb * cus * KAN_PP_GRIDMULT;
+    return (nb < 4 ? nb : 4) * cus;
 }
 
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
@@ -349,7 +390,8 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
-        const int grid = grid_for(B, kBlock / kWave, cap);                                                       \
+        static const int ovr = getenv("KANODE_PP_GRID") ? atoi(getenv("KANODE_PP_GRID")) : 0;                   \
+        const int grid = grid_for(B, kBlock / kWave, ovr > 0 ? ovr : cap);                                       \
         hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B);                  \
     } while (0)
