@@ -173,7 +173,7 @@ def main() -> None:
                    "parallelism": f"trajectory-sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("fk_pp_build_kernel + fk_rhs_pp_kernel<SOFTSIGN,RBF>" if table
+                     "kernel": ("fk_pp_build_kernel + fk_rhs_pp_wave_kernel<SOFTSIGN,RBF,2>" if table
                                 else "fk_rhs_kernel<double,SOFTSIGN,REC_CORR,10>"),
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes},

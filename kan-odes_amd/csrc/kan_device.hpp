@@ -65,6 +65,8 @@ struct LayerConst {
 constexpr int kPPCoef = 10;
 constexpr int kPPChecks = 3;
 constexpr int kPPMaxIntervals = 512;
+constexpr int kPPMaxFns = 3;
+enum PPFn : int { PP_PHI = 0, PP_DPHI = 1, PP_SWISH = 2 };   // tabulated functions (slot = id)
 struct PPConst {
     int32_t ni;                       // intervals (power of two, multiple of 16)
     int32_t enabled;                  // host admissibility (f64, rbf/rswaf, even Nx)

@@ -16,12 +16,18 @@ template <typename T>
 hipError_t launch_fk_vjp(const LayerConst& hlc, const LayerConst* lc, const T* p, T cd, T co, int Nx,
                          const T* u, const T* lam, T* lamJ, T* dp, T* slab, int slab_blocks, int64_t B,
                          hipStream_t st);
-// piecewise-polynomial Fisher-KPP RHS (kan_pp.hip): builds the table from p into
-// `table` (kPPCoef·ni doubles), then evaluates the RHS from it (fp64, Nx even)
+// piecewise-polynomial Fisher-KPP RHS / VJP (kan_pp.hip).  `tables` holds
+// kPPMaxFns slots of kPPCoef·ni doubles (slot = PPFn id); the build fills the listed
+// functions from p, the RHS then reads slot PP_PHI (fp64, Nx even).
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
-                              double* table, hipStream_t st);
+                              double* tables, const int* fns, int nfn, hipStream_t st);
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
+                            hipStream_t st);
+bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx);
+hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                            const double* p, double* tables, double cd, double co, int Nx, const double* u,
+                            const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
                             hipStream_t st);
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,

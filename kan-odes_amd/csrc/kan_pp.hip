@@ -57,16 +57,25 @@ __device__ __forceinline__ double pp_direct(const Math<double>& M, const LayerCo
     return s;
 }
 
-// One block builds kPPPerBlock intervals: 13 direct evaluations each (10 nodes +
-// 3 checks), node values -> monomial coefficients (Q, host-built), acceptance.
+// One block builds kPPPerBlock intervals of one tabulated function (blockIdx.y
+// picks it from `fns`): 13 direct evaluations per interval (10 nodes + 3 checks),
+// node values -> monomial coefficients (Q, host-built), acceptance.
+//   PP_PHI    φ(u)  = Σ_j C_j B_j(N(u)) + W swish(u)                 (kdense.jl:116-124)
+//   PP_DPHI   φ'(u) = N'(u) Σ_j ∂B_j C_j / h + W swish'(u)  — the rrule chain of
+//             utils.jl:15-21 and NNlib's Ω-form derivatives, i.e. x̄/λ of the pullback
+//   PP_SWISH  swish(u)                                               (the dW weight)
 // Each evaluation is split over a quad of lanes (terms j ≡ sub mod 4, combined in
 // a fixed order) so the dependent chain is ~3 exponentials, not G+1: the build is
 // latency-bound and sits between two dependent launches.
-// Table layout: [kPPCoef/2][ni] pairs (a_2c, a_2c+1), so lanes at neighbouring
-// intervals read neighbouring 16-byte LDS words.
+// Table layout per function: [kPPCoef/2][ni] pairs (a_2c, a_2c+1), so lanes at
+// neighbouring intervals read neighbouring 16-byte LDS words.
+struct PPFns {
+    int fn[kPPMaxFns];
+};
+
 __global__ void __launch_bounds__(kBlock)
 fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
-                   const double* __restrict__ p, double* __restrict__ table) {
+                   const double* __restrict__ p, double* __restrict__ tables, PPFns fns) {
     __shared__ double sQ[kPPCoef * kPPCoef];
     __shared__ double sT[kPPEvals];              // nodes, then check points
     __shared__ double sC[kMaxGrid + 1];          // C_0..C_{G-1}, W
@@ -79,6 +88,8 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
     const PPConst& pc = *pcp;
     const int tid = threadIdx.x;
     const int G = lc.G;
+    const int fn = fns.fn[blockIdx.y];
+    double* __restrict__ table = tables + (int64_t)fn * kPPCoef * pc.ni;
     // every constant the block needs, loaded in one round (no dependent global loads later)
     if (tid < kPPCoef * kPPCoef) sQ[tid] = (&pc.Q[0][0])[tid];
     if (tid < kPPEvals) sT[tid] = tid < kPPCoef ? pc.xi[tid] : pc.tchk[tid - kPPCoef];
@@ -97,25 +108,55 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
         const double u = ::fma(sT[m], 0.5 * pc.w, c);
         const double n = normalize<NORM_RUNTIME, double>(M, lc.norm, u);
         const double invh = (double)lc.invh;
-        double s = 0.0, a = 0.0;
-        for (int j = sub; j <= G; j += 4) {
-            double t;
-            if (j < G) {
-                double aux;
-                t = sC[j] * basis_direct<double>(M, lc.basis, (n - sG[j]) * invh, aux);
-            } else {
-                t = lc.use_base ? sC[G] * swish<double>(M, u) : 0.0;
+        double s = 0.0, a = 0.0, base = 0.0;    // spline-part sum, Σ|spline terms|, base term
+        if (fn != PP_SWISH) {
+            for (int j = sub; j < G; j += 4) {
+                double aux = 0.0;
+                const double y = (n - sG[j]) * invh;
+                const double phi = basis_direct<double>(M, lc.basis, y, aux);
+                const double t = fn == PP_PHI ? sC[j] * phi
+                                              : basis_pull<double>(lc.basis, lc.iqf_quirk, y, phi, aux, sC[j]) * invh;
+                s = s + t;
+                a = a + kabs(t);
             }
-            s = s + t;
-            a = a + kabs(t);
+        }
+        if (sub == 3) {
+            double sw, dsw;
+            swish_and_grad<double>(M, u, sw, dsw);
+            base = fn == PP_SWISH ? sw : (lc.use_base ? sC[G] * (fn == PP_PHI ? sw : dsw) : 0.0);
         }
         s = s + __shfl_xor(s, 1, 4);
         a = a + __shfl_xor(a, 1, 4);
         s = s + __shfl_xor(s, 2, 4);
         a = a + __shfl_xor(a, 2, 4);
+        base = __shfl(base, 3, 4);
         if (live && sub == 0) {
-            fv[kl][m] = s;
-            if (m >= kPPCoef) sv[kl][m - kPPCoef] = a;
+            // acceptance scale: Σ|terms| at the point, floored at 4·w·(the function's natural
+            // magnitude: Σ|C| (/h) + |W|, or 1 + |u| for swish).  The node -> monomial
+            // conversion rounds at ~|Q|·eps·(variation over the interval, ~w·|f'|), so
+            // where every term vanishes (swish(0) = 0) the floor keeps a correct fit from
+            // being rejected; it admits absolute errors <= 2.5e-15 of that magnitude.
+            double csum = 0.0;
+            for (int j = 0; j < G; ++j) csum += kabs(sC[j]);
+            const double wabs = lc.use_base ? kabs(sC[G]) : 0.0;
+            double v, sc, ref;
+            if (fn == PP_PHI) {
+                v = s + base;
+                sc = a + kabs(base);
+                ref = csum + wabs;
+            } else if (fn == PP_DPHI) {
+                const double dn = dnormalize<NORM_RUNTIME, double>(lc.norm, n);
+                v = dn * s + base;
+                sc = dn * a + kabs(base);
+                ref = csum * invh + wabs;
+            } else {
+                v = base;
+                sc = kabs(base);
+                ref = 1.0 + kabs(u);
+            }
+            sc += 4.0 * pc.w * ref;
+            fv[kl][m] = v;
+            if (m >= kPPCoef) sv[kl][m - kPPCoef] = sc;
         }
     }
     __syncthreads();
@@ -357,6 +398,201 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// VJP of the Fisher-KPP RHS (the pullback SciMLSensitivity requests per stage):
+//   λᵀJ = (D lap)ᵀλ + λ ⊙ φ'(u)      lap symmetric; φ' = the rrule chain (utils.jl:15-21)
+//   dC_j += Σ λ B_j(N(u)),  dW += Σ λ swish(u)
+// φ'(u) and swish(u) come from the PP_DPHI / PP_SWISH tables (same interval index);
+// the G basis values for dC from the Gaussian recurrence (kan_device.hpp), in the
+// form g = λ·E0, dC_j += g·kc_j, g *= R.
+
+// φ'(u) and swish(u) by the reference formulas (slow path: out of range / rejected).
+template <int NORM, int BASIS>
+__device__ __forceinline__ void pp_direct_dphi_sw(const Math<double>& M, const LayerConst& lc,
+                                                  const double* __restrict__ p, double u, double& dphi,
+                                                  double& sw) {
+    const double n = normalize<NORM, double>(M, lc.norm, u);
+    const int basis = BASIS >= 0 ? BASIS : lc.basis;
+    const double invh = (double)lc.invh;
+    const int G = lc.G;
+    double s = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < G; ++j) {
+        double aux = 0.0;
+        const double y = (n - (double)lc.grid[j]) * invh;
+        const double phi = basis_direct<double>(M, basis, y, aux);
+        s = s + basis_pull<double>(basis, lc.iqf_quirk, y, phi, aux, p[j]) * invh;
+    }
+    double dsw;
+    swish_and_grad<double>(M, u, sw, dsw);
+    dphi = dnormalize<NORM, double>(lc.norm, n) * s + (lc.use_base ? p[G] * dsw : 0.0);
+}
+
+// Two tables sharing one interval index: φ'(u) from td, swish(u) from ts.
+__device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const double2* __restrict__ ts, int ni,
+                                         double inv_w, double x0, double u, double& d, double& s) {
+    const double x = ::fma(u, inv_w, x0);
+    const bool in = (x >= 0.0) && (x < (double)ni);
+    const double xc = in ? x : 0.0;
+    const double fl = __builtin_floor(xc);
+    const int k = (int)fl;
+    const double t = ::fma(2.0, xc - fl, -1.0);
+    const double2* __restrict__ a = td + k;
+    const double2* __restrict__ b = ts + k;
+    const double2 a8 = a[4 * ni], a6 = a[3 * ni], a4 = a[2 * ni], a2 = a[ni], a0 = a[0];
+    const double2 b8 = b[4 * ni], b6 = b[3 * ni], b4 = b[2 * ni], b2 = b[ni], b0 = b[0];
+    double y = ::fma(a8.y, t, a8.x), z = ::fma(b8.y, t, b8.x);
+    y = ::fma(y, t, a6.y);
+    z = ::fma(z, t, b6.y);
+    y = ::fma(y, t, a6.x);
+    z = ::fma(z, t, b6.x);
+    y = ::fma(y, t, a4.y);
+    z = ::fma(z, t, b4.y);
+    y = ::fma(y, t, a4.x);
+    z = ::fma(z, t, b4.x);
+    y = ::fma(y, t, a2.y);
+    z = ::fma(z, t, b2.y);
+    y = ::fma(y, t, a2.x);
+    z = ::fma(z, t, b2.x);
+    y = ::fma(y, t, a0.y);
+    z = ::fma(z, t, b0.y);
+    y = ::fma(y, t, a0.x);
+    z = ::fma(z, t, b0.x);
+    d = y;
+    s = z;
+    return in && (y == y) && (z == z);
+}
+
+// One point of the pullback: returns λ φ'(x); accumulates the dC moments and dW.
+// With v_j = λ E0 R^j and the knot correction kc_j = K_j (1 + τ' e_j + τ'² e_j²/2):
+//     Σ_points λ B_j = K_j (S0_j + e_j S1_j + e_j²/2 S2_j),
+//     S0_j = Σ v_j,  S1_j = Σ v_j τ',  S2_j = Σ v_j τ'²
+// so the loop over knots needs no per-knot constants (they would not fit in SGPRs
+// next to the rest of the kernel).  S1/S2 carry weights |τ' e_j| <= 1.1e-6 and
+// (τ' e_j)²/2 <= 6e-13 of S0 (G=10), so they run in fp32 on their own fp32 power
+// chain: their rounding reaches dC at < 1e-13 relative.
+template <int NORM, int PATH, int GT>
+__device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const LayerConst& lc,
+                                               const double* __restrict__ p, const RecScalars<double>& rc,
+                                               const double2* __restrict__ td, const double2* __restrict__ ts,
+                                               int ni, double inv_w, double x0, double x, double l,
+                                               double (&S0)[GT], float (&S1)[GT], float (&S2)[GT], double& dW) {
+    double dphi, sw;
+    if (__builtin_expect(!pp_eval2(td, ts, ni, inv_w, x0, x, dphi, sw), 0))
+        pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, x, dphi, sw);
+    dW = ::fma(l, sw, dW);
+    const double n = normalize<NORM, double>(M, lc.norm, x);
+    double z0, E0, R, taup;
+    rec_anchor<double>(M, rc, n, z0, E0, R, taup);
+    double v = l * E0;
+    float v32 = (float)v, R32 = (float)R;
+    const float t32 = (float)taup, t2 = t32 * t32;
+#pragma unroll
+    for (int j = 0; j < GT; ++j) {
+        S0[j] = S0[j] + v;
+        v = v * R;
+        if constexpr (PATH == PATH_REC_CORR) {
+            S1[j] = fmaf(v32, t32, S1[j]);
+            S2[j] = fmaf(v32, t2, S2[j]);
+            v32 = v32 * R32;
+        }
+    }
+    return l * dphi;
+}
+
+// Nx = 128·NP, one wave per trajectory row (as fk_rhs_pp_wave_kernel): u and λ by
+// nontemporal 16-B loads, λ's stencil neighbours by wave rotation, λᵀJ by
+// nontemporal stores; per-thread dC/dW registers, block-summed into the slab row
+// of this block (ordered: bitwise reproducible for a given grid).  Dynamic LDS:
+// the PP_DPHI and PP_SWISH tables, [2][kPPCoef/2][ni] double2.
+template <int NORM, int PATH, int GT, int NP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))   // LDS allows 3 blocks/CU
+fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                      const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
+                      const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
+                      double* __restrict__ slab, int64_t B) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    __shared__ double red[(kBlock / kWave) * (GT + 1)];
+    const int tsz = (kPPCoef / 2) * ni;   // double2 per table
+    for (int i = threadIdx.x; i < tsz; i += kBlock) {
+        tl[i] = tables[PP_DPHI * tsz + i];
+        tl[tsz + i] = tables[PP_SWISH * tsz + i];
+    }
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    const Math<double> M{tab};
+    const double2* __restrict__ td = tl;
+    const double2* __restrict__ ts = tl + tsz;
+    const LayerConst& lc = *lcp;
+    const RecScalars<double> rc(lc);
+    double S0[GT];
+    float S1[GT], S2[GT];
+#pragma unroll
+    for (int j = 0; j < GT; ++j) {
+        S0[j] = 0.0;
+        S1[j] = S2[j] = 0.0f;
+    }
+    double dW = 0.0;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
+    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+        kd2 uv[NP], lv[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            uv[k] = ld_stream(u + b * Nx + 128 * k + 2 * lane);
+            lv[k] = ld_stream(lam + b * Nx + 128 * k + 2 * lane);
+        }
+        double rr[NP], rl[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            rr[k] = wave_ror1(lv[k].y);
+            rl[k] = wave_rol1(lv[k].x);
+        }
+        double la[NP][2];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+            const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+            lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, la[k][0], la[k][1]);
+        }
+        // a real loop over the row's pairs (not unrolled): only one pair's table reads
+        // and exponentials are live next to the 40 accumulator VGPRs
+#pragma unroll 1
+        for (int k = 0; k < NP; ++k) {
+            kd2 uk = uv[0], lk = lv[0];
+            double a0 = la[0][0], a1 = la[0][1];
+#pragma unroll
+            for (int q = 1; q < NP; ++q) {
+                if (k == q) {
+                    uk = uv[q];
+                    lk = lv[q];
+                    a0 = la[q][0];
+                    a1 = la[q][1];
+                }
+            }
+            const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0, S1,
+                                                           S2, dW);
+            __builtin_amdgcn_sched_barrier(0);
+            const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.y, lk.y, S0, S1,
+                                                           S2, dW);
+            kd2 o;
+            o.x = a0 + x0b;
+            o.y = a1 + x1b;
+            st_stream(lamJ + b * Nx + 128 * k + 2 * lane, o);
+        }
+    }
+    const int P = GT + (lc.use_base ? 1 : 0);
+    double acc[GT + 1];
+#pragma unroll
+    for (int j = 0; j < GT; ++j) {
+        const double e = lc.e[j];
+        acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+                                       : lc.K[j] * S0[j];
+    }
+    acc[GT] = dW;
+    block_sum_to<double, GT + 1>(acc, P, red, slab + (int64_t)blockIdx.x * P);
+}
+
 // Persistent grid: min(resident blocks per CU, 4) x CUs, each block stages the table
 // once.  4 blocks (16 waves) per CU streamed fastest in the grid sweep (tools/pp_grid.sh:
 // 98.7 us at 1024 blocks vs 101.4 us at the 6-block occupancy limit); the nontemporal
@@ -370,9 +606,13 @@ static int pp_grid_cap(K kernel, size_t lds) {
 }
 
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
-                              double* table, hipStream_t st) {
-    if (hpc.ni <= 0 || hpc.ni % kPPPerBlock || hpc.ni > kPPMaxIntervals) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(fk_pp_build_kernel, dim3(hpc.ni / kPPPerBlock), dim3(kBlock), 0, st, lc, pc, p, table);
+                              double* tables, const int* fns, int nfn, hipStream_t st) {
+    if (hpc.ni <= 0 || hpc.ni % kPPPerBlock || hpc.ni > kPPMaxIntervals || nfn < 1 || nfn > kPPMaxFns)
+        return hipErrorInvalidValue;
+    PPFns f{};
+    for (int i = 0; i < nfn; ++i) f.fn[i] = fns[i];
+    hipLaunchKernelGGL(fk_pp_build_kernel, dim3(hpc.ni / kPPPerBlock, nfn), dim3(kBlock), 0, st, lc, pc, p, tables,
+                       f);
     return hipGetLastError();
 }
 
@@ -380,7 +620,8 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
                             hipStream_t st) {
     if (Nx < 2 || (Nx & 1)) return hipErrorInvalidValue;
-    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, st);
+    const int fn_phi = PP_PHI;
+    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st);
     if (e != hipSuccess) return e;
     const int units = Nx / 2;
     const int tl = ceil_log2(units < kBlock ? units : kBlock);
@@ -418,6 +659,75 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
 #undef KAN_PP_PAIR
 #undef KAN_PP_WAVE
     return hipGetLastError();
+}
+
+// The table VJP covers the recurrence configurations the Fisher-KPP drivers use.
+bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx) {
+    const bool shape = Nx == 128 || Nx == 256 || Nx == 512;
+    const bool cfg = hlc.basis == BASIS_RBF && hlc.path != PATH_DIRECT &&
+                     ((hlc.G == 10 && (hlc.norm == NORM_SOFTSIGN || hlc.norm == NORM_TANH_FAST)) ||
+                      (hlc.G == 5 && (hlc.norm == NORM_SOFTSIGN || hlc.norm == NORM_TANH_FAST)));
+    return shape && cfg;
+}
+
+template <int NORM, int PATH, int GT>
+static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const double* p, const double* tables,
+                               double cd, double co, int Nx, const double* u, const double* lam, double* lamJ,
+                               double* slab, int slab_blocks, int64_t B, int& grid, hipStream_t st) {
+    const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+#define KAN_VJP_WAVE(NP)                                                                                          \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP>, lds);                            \
+        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p, \
+                           (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B);      \
+    } while (0)
+    if (Nx == 256) KAN_VJP_WAVE(2);
+    else if (Nx == 128) KAN_VJP_WAVE(1);
+    else KAN_VJP_WAVE(4);
+#undef KAN_VJP_WAVE
+    return hipGetLastError();
+}
+
+hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                            const double* p, double* tables, double cd, double co, int Nx, const double* u,
+                            const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
+                            hipStream_t st) {
+    if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
+    const int fns[2] = {PP_DPHI, PP_SWISH};
+    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st);
+    if (e != hipSuccess) return e;
+    int grid = 0;
+    if (hlc.path == PATH_REC_CORR) {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN)
+            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC_CORR, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                                slab_blocks, B, grid, st);
+        else if (hlc.G == 10)
+            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC_CORR, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                                 slab_blocks, B, grid, st);
+        else if (hlc.norm == NORM_SOFTSIGN)
+            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC_CORR, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                               slab_blocks, B, grid, st);
+        else
+            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC_CORR, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                                slab_blocks, B, grid, st);
+    } else {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN)
+            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                           slab_blocks, B, grid, st);
+        else if (hlc.G == 10)
+            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                            slab_blocks, B, grid, st);
+        else if (hlc.norm == NORM_SOFTSIGN)
+            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                          slab_blocks, B, grid, st);
+        else
+            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
+                                                           slab_blocks, B, grid, st);
+    }
+    if (e != hipSuccess || !dp) return e;
+    return launch_slab_reduce<double>(slab, grid, hlc.G + (hlc.use_base ? 1 : 0), dp, st);
 }
 
 }  // namespace kan

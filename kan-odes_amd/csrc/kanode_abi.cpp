@@ -352,6 +352,14 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
             }
             out = (T*)h->ws;
         }
+        if constexpr (std::is_same<T, double>::value) {
+            if (h->pp_on && kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx)) {
+                HIP_TRY(h, kan::launch_fk_vjp_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
+                                                 (int)h->spec.nx, u, lam, out, dp, (double*)h->slab, kSlabBlocks, B,
+                                                 st));
+                return KANODE_OK;
+            }
+        }
         HIP_TRY(h, kan::launch_fk_vjp<T>(h->hlc[0], h->dlc, p, cd, co, (int)h->spec.nx, u, lam, out, dp, (T*)h->slab,
                                          kSlabBlocks, B, st));
         return KANODE_OK;
@@ -478,7 +486,7 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
         if (h->hpc.enabled) {
             if ((e = hipMalloc(&h->dpc, sizeof(kan::PPConst))) != hipSuccess ||
                 (e = hipMemcpy(h->dpc, &h->hpc, sizeof(kan::PPConst), hipMemcpyHostToDevice)) != hipSuccess ||
-                (e = hipMalloc(&h->dtable, sizeof(double) * kan::kPPCoef * h->hpc.ni)) != hipSuccess)
+                (e = hipMalloc(&h->dtable, sizeof(double) * kan::kPPMaxFns * kan::kPPCoef * h->hpc.ni)) != hipSuccess)
                 return bail(fail(h, KANODE_ERR_HIP, std::string("pp table: ") + hipGetErrorString(e)));
             h->pp_on = true;
         }

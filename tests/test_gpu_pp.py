@@ -135,3 +135,50 @@ def test_table_graph_capture():
     torch.cuda.synchronize()
     ref = O.fk_rhs(O.LayerSpec(1, 1, 10, "softsign"), p.cpu().numpy(), 0.01, 1.0 / 255, u.cpu().numpy())
     assert_close(out, ref, fk_scale(p.cpu().numpy(), 0.01, 1.0 / 255, u.cpu().numpy()), RTOL[torch.float64], "graph")
+
+
+def vjp_scales(p, D, dx, u, lam):
+    """λᵀJ and dp scales of tests/test_gpu_fk.py (Σ|terms| proxies)."""
+    scJ = fk_scale(np.abs(p) * 10, D, dx, np.abs(lam)) * (1 + np.abs(u))
+    return scJ
+
+
+@pytest.mark.parametrize("nx", [128, 256, 512])
+@pytest.mark.parametrize("normalizer,G", [("softsign", 10), ("tanh_fast", 10), ("softsign", 5), ("tanh_fast", 5)])
+def test_table_vjp_matches_oracle(nx, normalizer, G):
+    """fk_vjp_pp_wave_kernel (φ', swish tables + dC recurrence) vs the oracle pullback."""
+    rng = np.random.default_rng(nx + G)
+    D, dx, B = 0.01, 1.0 / (nx - 1), 6
+    spec = O.LayerSpec(1, 1, G, normalizer)
+    p = rng.uniform(-1, 1, G + 1)
+    u = rng.uniform(-0.5, 1.5, (B, nx))
+    u[0, :16] = rng.uniform(-9, 9, 16)                    # out of the table's range: direct path
+    lam = rng.normal(size=u.shape)
+    rhs = rhs_for(nx, normalizer, G, D=D, dx=dx)
+    assert rhs.hd.pointwise_table
+    lamJ, dp = rhs.vjp(t(u), t(p), t(lam))
+    rJ, rdp = O.fk_vjp(spec, p, D, dx, u, lam)
+    assert_close(lamJ, rJ, vjp_scales(p, D, dx, u, lam), RTOL[torch.float64], "lamJ")
+    _, dpa = O.fk_vjp(spec, p, D, dx, u, np.abs(lam))
+    assert_close(dp, rdp, np.abs(dpa), 1e-12, "dp")
+    # the per-point recurrence kernel gives the same pullback
+    rec = rhs_for(nx, normalizer, G, D=D, dx=dx, table=False)
+    lamJ2, dp2 = rec.vjp(t(u), t(p), t(lam))
+    assert_close(lamJ, lamJ2.cpu().numpy(), vjp_scales(p, D, dx, u, lam), 2 * RTOL[torch.float64], "table vs rec")
+
+
+def test_table_vjp_nonfinite_and_reproducible():
+    rng = np.random.default_rng(21)
+    nx, D, dx = 256, 0.01, 1.0 / 255
+    p = rng.uniform(-1, 1, 11)
+    u = rng.uniform(0, 1, (64, nx))
+    lam = rng.normal(size=u.shape)
+    rhs = rhs_for(nx, D=D, dx=dx)
+    a = rhs.vjp(t(u), t(p), t(lam))
+    b = rhs.vjp(t(u), t(p), t(lam))
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])        # ordered reductions: bitwise
+    u[3, 10] = np.nan
+    lamJ, dp = rhs.vjp(t(u), t(p), t(lam))
+    rJ, _ = O.fk_vjp(O.LayerSpec(1, 1, 10, "softsign"), p, D, dx, u, lam)
+    assert np.array_equal(np.isnan(lamJ.cpu().numpy()), np.isnan(rJ))
+    assert torch.isnan(dp).all()

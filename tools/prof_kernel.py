@@ -20,7 +20,7 @@ from bench import fk_ics  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="fk_rhs", choices=["fk_rhs", "fk_vjp", "lv_rhs", "lv_vjp"])
+    ap.add_argument("--what", default="fk_rhs", choices=["fk_rhs", "fk_rhs_rec", "fk_vjp", "lv_rhs", "lv_vjp"])
     ap.add_argument("--batch", type=int, default=131072)
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
@@ -28,7 +28,8 @@ def main():
     if a.what.startswith("fk"):
         nx, dx = 256, 1 / 255
         kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
-        rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=0.01, device=dev)
+        rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=0.01, device=dev,
+                                  table=False if a.what == "fk_rhs_rec" else None)
         p = torch.as_tensor(kan1.setup(np.random.default_rng(0))[0].astype(np.float64), device=dev)
         u = fk_ics(a.batch, nx, dx, 1, dev)
     else:
@@ -41,7 +42,7 @@ def main():
     dp = torch.zeros_like(p)
     rhs.hd.reserve(a.batch)
     for _ in range(a.reps):
-        if a.what.endswith("rhs"):
+        if "rhs" in a.what:
             rhs.rhs(u, p, out)
         else:
             rhs.hd.vjp(p, u, lam, dp=dp)

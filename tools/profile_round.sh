@@ -1,13 +1,22 @@
 #!/usr/bin/env bash
-# Round profiling on the GPU box -> gpurun_out/profile_$TAG/ (copied into profiles/$TAG by the caller):
-#   1. bench.py (the driver's command)                    -> bench.json
-#   2. rocprofv3 --kernel-trace --stats of the same bench -> kernel_stats.csv
-#   3. separate --pmc passes (no trace domains with PMC):  FETCH_SIZE, WRITE_SIZE, VALU counters
+# Round evidence on the GPU box -> gpurun_out/profile_$TAG/ (copied into profiles/$TAG by the caller):
+#   0. pytest -m gpu (whole suite) and __graft_entry__.smoke()
+#   1. bench.py (the driver's command, with cpu_baseline)  -> bench.json
+#   2. rocprofv3 --kernel-trace --stats of the same bench    -> kernel_stats.csv
+#   3. separate --pmc passes (no trace domains with PMC): FETCH_SIZE, WRITE_SIZE, VALU counters
 #   4. tools/traffic.py -> traffic.json (gfx950: FETCH_SIZE x2 for 16-B/lane streaming reads)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/profile_$TAG; mkdir -p $OUT
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  echo "== pytest -m gpu"
+  timeout -k 10 900 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 3; }
+  tail -2 $OUT/pytest_gpu.log
+  echo "== smoke"
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 3; }
+  tail -2 $OUT/smoke.log
+fi
 echo "== bench"
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 3; }
 cat $OUT/bench.json
@@ -15,8 +24,8 @@ echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
   python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 3; }
 cp $OUT/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
-for w in fk_rhs fk_vjp; do
-  for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F64"; do
+for w in fk_rhs fk_rhs_rec fk_vjp; do
+  for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_LDS"; do
     n=$(echo $c | cut -d' ' -f1)
     timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $OUT/pmc_${w}_$n -o run --output-format csv -- \
       python3 tools/prof_kernel.py --what $w --reps 5 > $OUT/pmc_${w}_$n.log 2>&1 || { echo "pmc $w $n failed"; tail -5 $OUT/pmc_${w}_$n.log; exit 3; }

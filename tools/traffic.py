@@ -19,8 +19,13 @@ def mean_counter(path, kernel_sub, counter):
 
 
 root = sys.argv[1]
+NX = 256
+# (pmc pass name, kernel-name substring, traffic.json key, algorithmic 8-byte words per trajectory)
+PASSES = (("fk_rhs", "fk_rhs_pp_wave_kernel", "fisher_kpp_256:table", 2 * NX),
+          ("fk_rhs_rec", "fk_rhs_kernel", "fisher_kpp_256:recurrence", 2 * NX),
+          ("fk_vjp", "fk_vjp_kernel", "fisher_kpp_256_vjp", 3 * NX))
 out = {}
-for w, kern, batch in (("fk_rhs", "fk_rhs_kernel", 131072), ("fk_vjp", "fk_vjp_kernel", 131072)):
+for w, kern, key, words in PASSES:
     f = glob.glob(os.path.join(root, f"pmc_{w}_FETCH_SIZE", "**", "*counter_collection.csv"), recursive=True)
     wr = glob.glob(os.path.join(root, f"pmc_{w}_WRITE_SIZE", "**", "*counter_collection.csv"), recursive=True)
     if not f or not wr:
@@ -29,10 +34,10 @@ for w, kern, batch in (("fk_rhs", "fk_rhs_kernel", 131072), ("fk_vjp", "fk_vjp_k
     write = mean_counter(wr[0], kern, "WRITE_SIZE")
     if fetch is None or write is None:
         continue
-    nx = 256
-    alg = 8.0 * (11 + batch * (2 * nx if w == "fk_rhs" else 3 * nx))
+    batch = 131072
+    alg = 8.0 * (11 + batch * words)
     hbm = (2.0 * fetch + write) * 1024.0
-    out["fisher_kpp_256" if w == "fk_rhs" else "fisher_kpp_256_vjp"] = {
+    out[key] = {
         "batch": batch, "kernel": kern, "fetch_size_kib": fetch, "write_size_kib": write,
         "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": hbm / alg,
         "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), WRITE_SIZE as is",
