@@ -23,7 +23,7 @@ NX = 256
 # (pmc pass name, kernel-name substring, traffic.json key, algorithmic 8-byte words per trajectory)
 PASSES = (("fk_rhs", "fk_rhs_pp_wave_kernel", "fisher_kpp_256:table", 2 * NX),
           ("fk_rhs_rec", "fk_rhs_kernel", "fisher_kpp_256:recurrence", 2 * NX),
-          ("fk_vjp", "fk_vjp_kernel", "fisher_kpp_256_vjp", 3 * NX))
+          ("fk_vjp", "fk_vjp_pp_wave_kernel", "fisher_kpp_256_vjp", 3 * NX))
 out = {}
 for w, kern, key, words in PASSES:
     f = glob.glob(os.path.join(root, f"pmc_{w}_FETCH_SIZE", "**", "*counter_collection.csv"), recursive=True)
