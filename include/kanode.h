@@ -142,6 +142,29 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option);
 /* --- the RHS and its VJP (device pointers, async on stream) ----------------- */
 /* du[N,B] = f(u[N,B]; p) */
 kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch, void* stream);
+
+/* Runge-Kutta stage (OrdinaryDiffEqTsit5 perform_step!: the stage broadcast plus the dudt
+ * call, and after the last stage the embedded-error residual of calculate_residuals):
+ *     y  = u + Σ_{j<n_prev} c[j]·k[j]            (formed in registers where the kernel allows)
+ *     du = f(y; p)
+ *     y_out (nullable) <- y
+ *     want_error: *error_sumsq = Σ_i (e_i / (abstol + reltol·max(|u_i|, |y_i|)))²,
+ *                 e = Σ_{j<n_prev} ec[j]·k[j] + ec[n_prev]·du,  over all N·B entries
+ * k, y_out, du are device [N,B] arrays of the state dtype; error_sumsq is a device double.
+ * n_prev = 0 makes this kanode_rhs (plus the optional copy / error). */
+#define KANODE_MAX_STAGES 8
+typedef struct {
+    int32_t n_prev;
+    const void* k[KANODE_MAX_STAGES];
+    double c[KANODE_MAX_STAGES];
+    void* y_out;
+    int32_t want_error;
+    double ec[KANODE_MAX_STAGES + 1];
+    double abstol, reltol;
+    void* error_sumsq;
+} kanode_stage;
+kanode_status kanode_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* stage, void* du,
+                               int64_t batch, void* stream);
 /* lam_J[N,B] = (∂f/∂u)ᵀ lam   (nullable: skip)
  * dp[P]     += Σ_b (∂f/∂p)ᵀ lam  (nullable: skip) */
 kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,

@@ -16,6 +16,25 @@ template <typename T>
 hipError_t launch_fk_vjp(const LayerConst& hlc, const LayerConst* lc, const T* p, T cd, T co, int Nx,
                          const T* u, const T* lam, T* lamJ, T* dp, T* slab, int slab_blocks, int64_t B,
                          hipStream_t st);
+// Runge-Kutta stage arguments (kanode_rhs_stage): y = u + Σ_{j<nk} c_j k_j; optional
+// embedded error e = Σ_{j<nk} ec_j k_j + ec_nk du, Σ (e / (abstol + reltol·max(|u|,|y|)))².
+constexpr int kMaxStages = 8;
+template <typename T>
+struct StageArgs {
+    const T* k[kMaxStages];
+    double c[kMaxStages];
+    double ec[kMaxStages + 1];
+    double abstol, reltol;
+    int nk;
+};
+template <typename T>
+hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st);
+// per-block partials into `slab` (<= slab_blocks rows), then out[0] = ordered total
+template <typename T>
+hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageArgs<T>& sa, double* slab,
+                              int slab_blocks, double* out, int64_t n, hipStream_t st);
+hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, hipStream_t st);
+
 // piecewise-polynomial Fisher-KPP RHS / VJP (kan_pp.hip).  `tables` holds
 // kPPMaxFns slots of kPPCoef·ni doubles (slot = PPFn id); the build fills the listed
 // functions from p, the RHS then reads slot PP_PHI (fp64, Nx even).
@@ -25,6 +44,12 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
                             hipStream_t st);
 bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx);
+bool fk_stage_pp_supported(const PPConst& hpc, int Nx);
+// fused stage: du = f(u + Σ c_j k_j), optional y_out, optional error total into err_out[0]
+hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                              const double* p, double* table, double cd, double co, int Nx, const double* u,
+                              const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
+                              double* err_out, double* du, int64_t B, hipStream_t st);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,

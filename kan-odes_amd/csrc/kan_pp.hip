@@ -593,6 +593,97 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     block_sum_to<double, GT + 1>(acc, P, red, slab + (int64_t)blockIdx.x * P);
 }
 
+// Runge-Kutta stage, fused (kanode_rhs_stage): the stage input y = u + Σ_j c_j k_j is
+// formed in registers from nontemporal loads of u and the k_j, the stencil
+// neighbours of y come from the wave rotations, du = f(y) as above.  Optionally y
+// is written (the adjoint's saved input; Tsit5's u_new) and the embedded error
+// Σ (e/sk)², e = Σ ec_j k_j + ec_nk du, sk = abstol + reltol·max(|u|,|y|), is
+// block-summed into err_slab[blockIdx.x] (ordered: reproducible).
+template <int NORM, int BASIS, int NP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                        const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
+                        const double* __restrict__ u, StageArgs<double> sa, double* __restrict__ y_out,
+                        double* __restrict__ err_slab, double* __restrict__ du, int64_t B) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    __shared__ double red[kBlock / kWave];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    const Math<double> M{tab};
+    const LayerConst& lc = *lcp;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool want_err = err_slab != nullptr;
+    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
+    double eacc = 0.0;
+    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+        const int64_t rb = b * Nx + 2 * lane;
+        kd2 uv[NP], y[NP], e[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            uv[k] = ld_stream(u + rb + 128 * k);
+            y[k] = uv[k];
+            e[k] = kd2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int j = 0; j < kMaxStages; ++j) {
+            if (j < sa.nk) {
+                const double cj = sa.c[j], ej = sa.ec[j];
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    const kd2 kj = ld_stream(sa.k[j] + rb + 128 * k);
+                    y[k].x = ::fma(cj, kj.x, y[k].x);
+                    y[k].y = ::fma(cj, kj.y, y[k].y);
+                    if (want_err) {
+                        e[k].x = ::fma(ej, kj.x, e[k].x);
+                        e[k].y = ::fma(ej, kj.y, e[k].y);
+                    }
+                }
+            }
+        }
+        double rr[NP], rl[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            rr[k] = wave_ror1(y[k].y);
+            rl[k] = wave_rol1(y[k].x);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+            const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+            const int i = 128 * k + 2 * lane;
+            bool ok0, ok1;
+            double k0 = pp_eval(tl, ni, inv_w, x0, y[k].x, ok0);
+            double k1 = pp_eval(tl, ni, inv_w, x0, y[k].y, ok1);
+            if (__builtin_expect(!(ok0 && ok1), 0)) {
+                double sc;
+                if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].x, sc);
+                if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].y, sc);
+            }
+            double l0, l1;
+            lap_pair<double>(um, y[k].x, y[k].y, up, i, Nx, cd, co, l0, l1);
+            kd2 o;
+            o.x = l0 + k0;
+            o.y = l1 + k1;
+            st_stream(du + b * Nx + i, o);
+            if (y_out) st_stream(y_out + b * Nx + i, y[k]);
+            if (want_err) {
+                const double en = sa.ec[sa.nk];
+                const double ex = ::fma(en, o.x, e[k].x), ey = ::fma(en, o.y, e[k].y);
+                const double sx = ::fma(sa.reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), sa.abstol);
+                const double sy = ::fma(sa.reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), sa.abstol);
+                const double rx = ex / sx, ry = ey / sy;
+                eacc = ::fma(rx, rx, eacc);
+                eacc = ::fma(ry, ry, eacc);
+            }
+        }
+    }
+    if (want_err) {
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+    }
+}
+
 // Persistent grid: min(resident blocks per CU, 4) x CUs, each block stages the table
 // once.  4 blocks (16 waves) per CU streamed fastest in the grid sweep (tools/pp_grid.sh:
 // 98.7 us at 1024 blocks vs 101.4 us at the 6-block occupancy limit); the nontemporal
@@ -659,6 +750,43 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
 #undef KAN_PP_PAIR
 #undef KAN_PP_WAVE
     return hipGetLastError();
+}
+
+bool fk_stage_pp_supported(const PPConst& hpc, int Nx) { return hpc.enabled && (Nx == 128 || Nx == 256 || Nx == 512); }
+
+hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                              const double* p, double* table, double cd, double co, int Nx, const double* u,
+                              const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
+                              double* err_out, double* du, int64_t B, hipStream_t st) {
+    if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
+    const int fn_phi = PP_PHI;
+    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st);
+    if (e != hipSuccess) return e;
+    const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+    int grid = 0;
+    double* slab = err_out ? err_slab : nullptr;
+#define KAN_STAGE_WAVE(NORM, BASIS, NP)                                                                          \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_stage_pp_wave_kernel<NORM, BASIS, NP>, lds);                             \
+        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        hipLaunchKernelGGL((fk_stage_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p, \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, sa, y_out, slab, du, B);  \
+    } while (0)
+#define KAN_STAGE_GO(NORM, BASIS)                                                                                \
+    do {                                                                                                         \
+        if (Nx == 256) KAN_STAGE_WAVE(NORM, BASIS, 2);                                                           \
+        else if (Nx == 128) KAN_STAGE_WAVE(NORM, BASIS, 1);                                                      \
+        else KAN_STAGE_WAVE(NORM, BASIS, 4);                                                                     \
+    } while (0)
+    if (hlc.basis == BASIS_RBF && hlc.norm == NORM_SOFTSIGN) KAN_STAGE_GO(NORM_SOFTSIGN, BASIS_RBF);
+    else if (hlc.basis == BASIS_RBF && hlc.norm == NORM_TANH_FAST) KAN_STAGE_GO(NORM_TANH_FAST, BASIS_RBF);
+    else KAN_STAGE_GO(NORM_RUNTIME, -1);
+#undef KAN_STAGE_GO
+#undef KAN_STAGE_WAVE
+    e = hipGetLastError();
+    if (e != hipSuccess || !err_out) return e;
+    return launch_stage_error_final(err_slab, grid, err_out, st);
 }
 
 // The table VJP covers the recurrence configurations the Fisher-KPP drivers use.

@@ -1,0 +1,89 @@
+// kan_stage.hip — Runge-Kutta stage plumbing around any RHS (gfx950).
+//
+// OrdinaryDiffEqTsit5's perform_step! forms each stage input
+//     y = uprev + dt·Σ_j a_sj k_j                    (broadcast over the state)
+// calls the RHS on it, and after the last stage forms the embedded error
+//     utilde = dt·Σ_j btilde_j k_j,   EEst = RMS(utilde / (abstol + reltol·max(|uprev|, |u|)))
+// (OrdinaryDiffEq 6.89 calculate_residuals + ODE_DEFAULT_NORM; third-party, restated).
+// These generic kernels serve every RHS kind; the Fisher-KPP table path fuses the
+// same arithmetic into its streaming kernel instead (kan_pp.hip).
+#include "kan_common.hpp"
+#include "kan_kernels.hpp"
+
+namespace kan {
+
+// y = u + Σ_{j<nk} c_j k_j, elementwise (fma, ascending j)
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+stage_lincomb_kernel(const T* __restrict__ u, StageArgs<T> sa, T* __restrict__ y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        T v = u[i];
+#pragma unroll
+        for (int j = 0; j < kMaxStages; ++j)
+            if (j < sa.nk) v = kfma<T>((T)sa.c[j], sa.k[j][i], v);
+        y[i] = v;
+    }
+}
+
+// per-block Σ (e/sk)² with e = Σ_j ec_j k_j + ec_nk du, sk = abstol + reltol·max(|u|,|y|)
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+stage_error_kernel(const T* __restrict__ u, const T* __restrict__ y, const T* __restrict__ du, StageArgs<T> sa,
+                   double* __restrict__ slab, int64_t n) {
+    __shared__ double red[kBlock / kWave];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        double e = 0.0;
+#pragma unroll
+        for (int j = 0; j < kMaxStages; ++j)
+            if (j < sa.nk) e = ::fma(sa.ec[j], (double)sa.k[j][i], e);
+        e = ::fma(sa.ec[sa.nk], (double)du[i], e);
+        const double sk = ::fma(sa.reltol, fmax(kabs((double)u[i]), kabs((double)y[i])), sa.abstol);
+        const double r = e / sk;
+        acc = ::fma(r, r, acc);
+    }
+    const double v[1] = {acc};
+    block_sum_to<double, 1>(v, 1, red, slab + blockIdx.x);
+}
+
+// out[0] = Σ_b slab[b], fixed order (one block)
+__global__ void __launch_bounds__(kBlock) stage_error_final_kernel(const double* __restrict__ slab, int nblk,
+                                                                   double* __restrict__ out) {
+    __shared__ double red[kBlock / kWave];
+    double acc = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += kBlock) acc += slab[b];
+    const double v[1] = {acc};
+    block_sum_to<double, 1>(v, 1, red, out);
+}
+
+hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(stage_error_final_kernel, dim3(1), dim3(kBlock), 0, st, slab, nblk, out);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st) {
+    const int grid = grid_for(n, kBlock, kGridCap);
+    hipLaunchKernelGGL((stage_lincomb_kernel<T>), dim3(grid), dim3(kBlock), 0, st, u, sa, y, n);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageArgs<T>& sa, double* slab,
+                              int slab_blocks, double* out, int64_t n, hipStream_t st) {
+    const int grid = grid_for(n, kBlock, slab_blocks);
+    hipLaunchKernelGGL((stage_error_kernel<T>), dim3(grid), dim3(kBlock), 0, st, u, y, du, sa, slab, n);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_stage_error_final(slab, grid, out, st);
+}
+
+template hipError_t launch_stage_lincomb<double>(const double*, const StageArgs<double>&, double*, int64_t,
+                                                 hipStream_t);
+template hipError_t launch_stage_lincomb<float>(const float*, const StageArgs<float>&, float*, int64_t, hipStream_t);
+template hipError_t launch_stage_error<double>(const double*, const double*, const double*, const StageArgs<double>&,
+                                               double*, int, double*, int64_t, hipStream_t);
+template hipError_t launch_stage_error<float>(const float*, const float*, const float*, const StageArgs<float>&,
+                                              double*, int, double*, int64_t, hipStream_t);
+
+}  // namespace kan

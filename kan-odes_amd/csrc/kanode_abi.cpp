@@ -54,6 +54,9 @@ struct kanode_handle {
     kan::PPConst* dpc = nullptr;
     double* dtable = nullptr;
     bool pp_on = false;
+    // stage input y for kanode_rhs_stage's unfused path
+    void* stage_ws = nullptr;
+    size_t stage_ws_bytes = 0;
     // host staging (device buffers) for *_host calls
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -392,6 +395,58 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
     return KANODE_OK;
 }
 
+template <typename T>
+kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* sg, T* du, int64_t B,
+                      hipStream_t st) {
+    if (sg->n_prev < 0 || sg->n_prev > KANODE_MAX_STAGES)
+        return fail(h, KANODE_ERR_INVALID_ARG, "n_prev must be in [0, KANODE_MAX_STAGES]");
+    if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "stage needs an RHS with N_in == N_out");
+    if (sg->want_error && !sg->error_sumsq) return fail(h, KANODE_ERR_INVALID_ARG, "want_error needs error_sumsq");
+    kan::StageArgs<T> sa{};
+    sa.nk = sg->n_prev;
+    for (int j = 0; j < sg->n_prev; ++j) {
+        if (!sg->k[j]) return fail(h, KANODE_ERR_INVALID_ARG, "null stage vector k[" + std::to_string(j) + "]");
+        sa.k[j] = (const T*)sg->k[j];
+        sa.c[j] = sg->c[j];
+    }
+    for (int j = 0; j <= sg->n_prev; ++j) sa.ec[j] = sg->want_error ? sg->ec[j] : 0.0;
+    sa.abstol = sg->abstol;
+    sa.reltol = sg->reltol;
+    double* err_out = sg->want_error ? (double*)sg->error_sumsq : nullptr;
+    if constexpr (std::is_same<T, double>::value) {
+        if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on &&
+            kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx)) {
+            const double dx2 = h->spec.dx * h->spec.dx;
+            const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+            HIP_TRY(h, kan::launch_fk_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
+                                               (int)h->spec.nx, u, sa, (double*)sg->y_out, (double*)h->slab,
+                                               kSlabBlocks, err_out, du, B, st));
+            return KANODE_OK;
+        }
+    }
+    // unfused: y materialised (into y_out or the handle's stage workspace), RHS, error pass
+    const int64_t n = h->n_in * B;
+    T* y = (T*)sg->y_out;
+    if (!y) {
+        const size_t need = (size_t)n * sizeof(T);
+        if (need > h->stage_ws_bytes) {
+            if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "stage workspace too small during capture");
+            HIP_TRY(h, hipStreamSynchronize(st));
+            if (h->stage_ws) HIP_TRY(h, hipFree(h->stage_ws));
+            h->stage_ws = nullptr;
+            h->stage_ws_bytes = 0;
+            HIP_TRY(h, hipMalloc(&h->stage_ws, need));
+            h->stage_ws_bytes = need;
+        }
+        y = (T*)h->stage_ws;
+    }
+    HIP_TRY(h, kan::launch_stage_lincomb<T>(u, sa, y, n, st));
+    kanode_status s = rhs_t<T>(h, p, y, du, B, st);
+    if (s != KANODE_OK) return s;
+    if (err_out) HIP_TRY(h, kan::launch_stage_error<T>(u, y, du, sa, (double*)h->slab, kSlabBlocks, err_out, n, st));
+    return KANODE_OK;
+}
+
 kanode_status check_handle(kanode_handle* h) {
     if (!h) return KANODE_ERR_INVALID_ARG;
     hipError_t e = hipSetDevice(h->spec.device);
@@ -506,6 +561,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->stage) (void)hipFree(h->stage);
     if (h->dpc) (void)hipFree(h->dpc);
+    if (h->stage_ws) (void)hipFree(h->stage_ws);
     if (h->dtable) (void)hipFree(h->dtable);
     delete h;
 }
@@ -573,6 +629,20 @@ kanode_status kanode_rhs(kanode_handle* h, const void* p, const void* u, void* d
     hipStream_t st = (hipStream_t)stream;
     if (h->spec.dtype == KANODE_F64) return rhs_t<double>(h, (const double*)p, (const double*)u, (double*)du, batch, st);
     return rhs_t<float>(h, (const float*)p, (const float*)u, (float*)du, batch, st);
+}
+
+kanode_status kanode_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* stage, void* du,
+                               int64_t batch, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (!stage) return fail(h, KANODE_ERR_INVALID_ARG, "null stage");
+    if (batch < 0) return fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    if (batch == 0) return KANODE_OK;
+    if (!p || !u || !du) return fail(h, KANODE_ERR_INVALID_ARG, "null p/u/du");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64) return stage_t<double>(h, (const double*)p, (const double*)u, stage, (double*)du,
+                                                            batch, st);
+    return stage_t<float>(h, (const float*)p, (const float*)u, stage, (float*)du, batch, st);
 }
 
 kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,

@@ -45,6 +45,24 @@ class SpecC(C.Structure):
     ]
 
 
+MAX_STAGES = 8
+
+
+class StageC(C.Structure):
+    """kanode_stage (include/kanode.h): Runge-Kutta stage input and fused error."""
+    _fields_ = [
+        ("n_prev", C.c_int32),
+        ("k", C.c_void_p * MAX_STAGES),
+        ("c", C.c_double * MAX_STAGES),
+        ("y_out", C.c_void_p),
+        ("want_error", C.c_int32),
+        ("ec", C.c_double * (MAX_STAGES + 1)),
+        ("abstol", C.c_double),
+        ("reltol", C.c_double),
+        ("error_sumsq", C.c_void_p),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/kanode.h declares
 _P = C.c_void_p
 _H = C.c_void_p
@@ -64,6 +82,7 @@ SIGNATURES = [
     ("kanode_set_option", C.c_int, [_H, C.c_int32, C.c_int64]),
     ("kanode_get_option", C.c_int64, [_H, C.c_int32]),
     ("kanode_rhs", C.c_int, [_H, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_rhs_stage", C.c_int, [_H, _P, _P, C.POINTER(StageC), _P, C.c_int64, _P]),
     ("kanode_vjp", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64, _P]),
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
     ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),

@@ -148,6 +148,46 @@ class KanodeHandle:
                 "kanode_rhs")
         return du
 
+    def rhs_stage(self, p: torch.Tensor, u: torch.Tensor, ks, c, y_out: torch.Tensor | None = None,
+                  error=None, out: torch.Tensor | None = None):
+        """Runge-Kutta stage: du = f(u + Σ_j c_j k_j; p) (kanode_rhs_stage).
+
+        ks: sequence of (B, N) tensors; c: their coefficients; y_out: optional tensor
+        receiving the stage input; error: optional (ec, abstol, reltol, sumsq) with ec of
+        len(ks)+1 coefficients and sumsq a 1-element float64 device tensor that receives
+        Σ (e / (abstol + reltol·max(|u|,|y|)))², e = Σ ec_j k_j + ec_last du."""
+        B = u.shape[0] if u.dim() == 2 else 1
+        if len(ks) != len(c) or len(ks) > L.MAX_STAGES:
+            raise ValueError("ks and c must have equal length <= KANODE_MAX_STAGES")
+        self._check_t(p, (self.P,), "p")
+        self._check_t(u, None, "u")
+        for k in ks:
+            self._check_t(k, tuple(u.shape), "k")
+        du = torch.empty_like(u) if out is None else out
+        self._check_t(du, tuple(u.shape), "du")
+        sg = L.StageC()
+        sg.n_prev = len(ks)
+        for j, (k, cj) in enumerate(zip(ks, c)):
+            sg.k[j] = k.data_ptr()
+            sg.c[j] = float(cj)
+        if y_out is not None:
+            self._check_t(y_out, tuple(u.shape), "y_out")
+            sg.y_out = y_out.data_ptr()
+        if error is not None:
+            ec, abstol, reltol, sumsq = error
+            if len(ec) != len(ks) + 1:
+                raise ValueError("error coefficients need len(ks) + 1 entries")
+            if sumsq.dtype != torch.float64 or sumsq.device != self.device or sumsq.numel() < 1:
+                raise ValueError("sumsq must be a float64 tensor on the handle's device")
+            sg.want_error = 1
+            for j, e in enumerate(ec):
+                sg.ec[j] = float(e)
+            sg.abstol, sg.reltol = float(abstol), float(reltol)
+            sg.error_sumsq = sumsq.data_ptr()
+        L.check(L.lib().kanode_rhs_stage(self._h, _ptr(p), _ptr(u), C.byref(sg), _ptr(du), B,
+                                         _stream(self.device)), self._h, "kanode_rhs_stage")
+        return du
+
     def vjp(self, p: torch.Tensor, u: torch.Tensor, lam: torch.Tensor, want_lamJ: bool = True,
             dp: torch.Tensor | None = None, accumulate_dp: bool = True):
         """(λᵀ∂f/∂u, Σ_b λᵀ∂f/∂p).  dp (if given) is ACCUMULATED into."""

@@ -16,6 +16,11 @@ Call sites the reference uses: LV_driver_KANODE.jl:122,180-184, Fisher-KPP_Sourc
 Every RHS evaluation is one libkanode.so call (through the autograd Function),
 so `solve(...)` is differentiable: backward runs the HIP VJP kernel once per
 stage (discrete adjoint, ≡ reverse-mode AD through the solver steps).
+
+RHS objects with a `stage` method (ChainRHS, FisherKPPRHS) take the fused path:
+each stage is one kanode_rhs_stage call that forms u + dt·Σ a_sj k_j inside the
+kernel, and the last stage also returns u_new and the embedded-error sum of
+squares, so no stage broadcast or error pass runs as separate torch kernels.
 """
 from __future__ import annotations
 
@@ -70,6 +75,7 @@ class Tsit5Options:
     qmin: float = 0.2
     qmax: float = 10.0
     qoldinit: float = 1e-4
+    fused: bool = True                 # use f.stage (kanode_rhs_stage) when the RHS has one
 
 
 @dataclass
@@ -108,6 +114,25 @@ def _step(f, u, p, t, dt, k1):
     return unew, ks
 
 
+def _step_fused(f, u, p, t, dt, k1, opt: Tsit5Options):
+    """One Tsit5 step as six kanode_rhs_stage calls; returns (u_new, ks, EEst or None)."""
+    ks = [k1]
+    sumsq = None
+    for i in range(6):
+        c = [dt * a for a in A[i]]
+        if i == 5:
+            err = None
+            if opt.adaptive:
+                sumsq = torch.empty(1, dtype=torch.float64, device=u.device)
+                err = ([dt * b for b in BTILDE], opt.abstol, opt.reltol, sumsq)
+            k7, unew = f.stage(u, p, ks, c, want_y=True, error=err)
+            ks.append(k7)
+        else:
+            ks.append(f.stage(u, p, ks, c)[0])
+    eest = math.sqrt(sumsq.item() / u.numel()) if sumsq is not None else None
+    return unew, ks, eest
+
+
 def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Options | None = None) -> Solution:
     """solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat, abstol, reltol) on device tensors.
 
@@ -135,17 +160,22 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
             raise ValueError("fixed-step Tsit5 needs opt.dt")
         dt = opt.dt
     qold = opt.qoldinit
+    fused = opt.fused and hasattr(f, "stage") and u0.dim() == 2
     naccept = nreject = nf = 0
     for _ in range(opt.maxiters):
         if t >= tf - 1e-14 * max(1.0, abs(tf)):
             break
         dt = min(dt, tf - t)
-        unew, ks = _step(f, u, p, t, dt, k1)
+        if fused:
+            unew, ks, EEst = _step_fused(f, u, p, t, dt, k1, opt)
+        else:
+            unew, ks = _step(f, u, p, t, dt, k1)
         nf += 6
         if opt.adaptive:
-            utilde = dt * sum(b * k for b, k in zip(BTILDE, ks))
-            sk = opt.abstol + torch.maximum(torch.abs(u), torch.abs(unew)) * opt.reltol
-            EEst = rms(utilde.detach() / sk.detach()).item()
+            if not fused:
+                utilde = dt * sum(b * k for b, k in zip(BTILDE, ks))
+                sk = opt.abstol + torch.maximum(torch.abs(u), torch.abs(unew)) * opt.reltol
+                EEst = rms(utilde.detach() / sk.detach()).item()
             q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
             if EEst > 1.0 and dt > opt.dtmin:
                 nreject += 1

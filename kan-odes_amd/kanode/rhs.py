@@ -45,6 +45,48 @@ class _LayerFn(torch.autograd.Function):
         return None, None, pbar, xbar
 
 
+class _StageFn(torch.autograd.Function):
+    """du = f(y), y = u + Σ_j c_j k_j (one kanode_rhs_stage call); returns (du, y).
+
+    Backward: (λᵀJ, dp) = VJP at the saved y; ∂/∂y = λᵀJ + ȳ, then ∂/∂u = ∂/∂y and
+    ∂/∂k_j = c_j ∂/∂y (the stage broadcast's own pullback)."""
+
+    @staticmethod
+    def forward(ctx, hd: KanodeHandle, c, error, p, u, *ks):
+        y = torch.empty_like(u)
+        du = hd.rhs_stage(p, u, ks, c, y_out=y, error=error)
+        ctx.hd, ctx.c = hd, c
+        ctx.save_for_backward(p, y)
+        return du, y
+
+    @staticmethod
+    def backward(ctx, gdu, gy):
+        p, y = ctx.saved_tensors
+        gy_total = gy
+        dp = None
+        if gdu is not None:
+            lamJ, dp = ctx.hd.vjp(p, y, gdu.contiguous(), accumulate_dp=ctx.needs_input_grad[3])
+            gy_total = lamJ if gy is None else lamJ + gy
+        if gy_total is None:
+            gy_total = torch.zeros_like(y)
+        gks = [gy_total * cj for cj in ctx.c]
+        return (None, None, None, dp, gy_total, *gks)
+
+
+def stage_apply(hd: KanodeHandle, p: torch.Tensor, u: torch.Tensor, ks, c, want_y: bool = False, error=None):
+    """Tsit5 stage through kanode_rhs_stage: (du, y or None).  Differentiable when autograd
+    is recording (y is then written for the backward VJP); otherwise y is only written
+    when asked for."""
+    c = [float(x) for x in c]
+    ks = [k.contiguous() for k in ks]
+    if torch.is_grad_enabled() and (p.requires_grad or u.requires_grad or any(k.requires_grad for k in ks)):
+        du, y = _StageFn.apply(hd, c, error, p.contiguous(), u.contiguous(), *ks)
+        return du, y
+    y = torch.empty_like(u) if want_y else None
+    du = hd.rhs_stage(p, u.contiguous(), ks, c, y_out=y, error=error)
+    return du, y
+
+
 def rhs_apply(hd: KanodeHandle, p: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
     return _RHSFn.apply(hd, p.contiguous(), u.contiguous())
 
@@ -66,6 +108,10 @@ class ChainRHS:
 
     def __call__(self, u: torch.Tensor, p: torch.Tensor, t=None) -> torch.Tensor:
         return rhs_apply(self.hd, p, u)
+
+    def stage(self, u, p, ks, c, want_y=False, error=None):
+        """Fused Runge-Kutta stage f(u + Σ c_j k_j) (see kanode_rhs_stage)."""
+        return stage_apply(self.hd, p, u, ks, c, want_y, error)
 
     def rhs(self, u, p, out=None):
         return self.hd.rhs(p, u, out)
@@ -100,6 +146,10 @@ class FisherKPPRHS:
 
     def __call__(self, u: torch.Tensor, p: torch.Tensor, t=None) -> torch.Tensor:
         return rhs_apply(self.hd, p, u)
+
+    def stage(self, u, p, ks, c, want_y=False, error=None):
+        """Fused Runge-Kutta stage f(u + Σ c_j k_j) (see kanode_rhs_stage)."""
+        return stage_apply(self.hd, p, u, ks, c, want_y, error)
 
     def rhs(self, u, p, out=None):
         return self.hd.rhs(p, u, out)

@@ -46,6 +46,21 @@ def test_library_loads_and_reports_version():
     assert lib.kanode_status_string(L.ERR_UNSUPPORTED) == b"unsupported configuration"
 
 
+def test_stage_struct_layout_matches_c_compiler(tmp_path):
+    """kanode_stage offsets as gcc lays them out from include/kanode.h vs the ctypes mirror."""
+    import subprocess
+    fields = [f[0] for f in L.StageC._fields_]
+    src = tmp_path / "probe.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kanode.h"\nint main(void) {\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(kanode_stage, {f}));\n' for f in fields)
+                   + '  printf("%zu\\n", sizeof(kanode_stage));\n  return 0;\n}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got[:-1] == [getattr(L.StageC, f).offset for f in fields]
+    assert got[-1] == C.sizeof(L.StageC)
+
+
 def test_struct_layout_matches_header():
     # kanode_layer_spec: 6 int32 + 3 float + 1 int32 = 40 bytes; kanode_spec holds 8 of them
     assert C.sizeof(L.LayerSpecC) == 40
