@@ -2,15 +2,18 @@
 """Benchmark: KAN-ODE RHS evaluations/s on MI355X (BASELINE.json metric).
 
 Workload (default `fisher_kpp_256`, BASELINE.json configs[2] — the north-star
-target config): the Fisher-KPP source-term RHS
+target config, "≥6× strong scaling at 8 GPUs"): the Fisher-KPP source-term RHS
     du = D*lap*u + KDense(1,1,10; softsign).(u)      (PDE examples/Fisher-KPP_Source.jl:95-98)
-on a 256-point periodic grid, fp64, B synthetic trajectories per GPU (the
-reference's IC family, Fisher-KPP_Source.jl:47-49, randomised per trajectory),
-random-init parameters.  One STEP = one RHS evaluation of the whole batch (one
-kernel launch).  value = trajectories x steps x ranks / max-over-ranks wall time.
+on a 256-point periodic grid, fp64, synthetic trajectories (the reference's IC
+family, Fisher-KPP_Source.jl:47-49, randomised per trajectory), random-init
+parameters.  One STEP = one RHS evaluation of the whole batch (one `kanode_rhs`
+call: table build + RHS kernel).  value = total trajectories x steps / max-over-
+ranks wall time.
 
-Multi-GPU: one process per GPU (torchrun); trajectories shard across ranks with
-no collective on the data path (weak scaling: per-GPU batch fixed).
+Multi-GPU: one process per GPU (torchrun); the fixed total batch (default
+1,048,576 trajectories = 8 x 131,072) shards evenly across ranks with no
+collective on the data path: strong scaling, total work fixed as N grows
+(`--batch-per-gpu` switches to weak scaling).
 
 Extra JSON fields: `roofline` (dominant kernel, HIP-event timed on its stream),
 `cpu_baseline` (the CPU restatement of the reference algorithm — dense Laplacian
@@ -48,15 +51,17 @@ def fk_ics(B: int, nx: int, dx: float, seed: int, device) -> torch.Tensor:
     return (amp * (torch.tanh((x - (c - dl / 2)) / (dl / 10)) - torch.tanh((x - (c + dl / 2)) / (dl / 10))) / 2).contiguous()
 
 
-def load_traffic(workload: str, batch: int):
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
+def load_traffic(workload: str, alg_bytes: float):
+    """Per-launch HBM bytes of the dominant kernel: the committed PMC measurement
+    (profiles/traffic.json, FETCH_SIZE x2 + WRITE_SIZE) as a ratio to the algorithmic
+    bytes of the launch it was measured on, applied to this launch's algorithmic bytes."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(workload)
-        if e and int(e["batch"]) == batch:
-            return float(e["hbm_bytes_per_launch"])
+        if e:
+            return float(e["traffic_over_algorithmic"]) * alg_bytes
     except (OSError, ValueError, KeyError):
         pass
     return None
@@ -87,16 +92,65 @@ def cpu_baseline(nx, dx, D, p_np, target_s: float):
     }
 
 
+def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: float, reps: int):
+    """Wall-clock of one training epoch (BASELINE metric, second half): fixed-step Tsit5 forward
+    solve with saveat, discrete adjoint through every stage (HIP VJP), loss, Adam update
+    (kanode.Trainer.step; Fisher-KPP_Source.jl:102-109,167-201).  The CPU reference runs the
+    same epoch through the oracle (dense Nx x Nx Laplacian matvec, as the reference does) on a
+    bounded sample of B_cpu trajectories; per-trajectory times are reported for both."""
+    T = steps * dt
+    saveat = [T * i / 5 for i in range(6)]
+    solver = kanode.Tsit5Options(adaptive=False, dt=dt)
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev)
+    u0 = fk_ics(B_gpu, nx, dx, seed=7, device=dev)
+    target = (0.9 * u0).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+    tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, target, torch.as_tensor(p_np, device=dev), eta=1e-3,
+                        solver=solver)
+    tr.step()                                   # warm-up (allocations, table builds)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    gpu_s = (time.perf_counter() - t0) / reps
+    out = {"unit": "s/epoch", "gpu": gpu_s, "gpu_batch": B_gpu, "steps": steps, "dt": dt, "stages_per_step": 6,
+           "what": "fixed-step Tsit5 solve + discrete adjoint + Adam, FK256 fp64"}
+    if B_cpu > 0:
+        from oracle import oracle as O
+        from oracle.oracle_rhs import OracleFKRHS
+        cpu_rhs = OracleFKRHS(O.LayerSpec(1, 1, 10, "softsign"), D, dx, dense=True)
+        u0c = fk_ics(B_cpu, nx, dx, seed=7, device="cpu")
+        tc = kanode.Trainer(cpu_rhs, u0c, (0.0, T), saveat, (0.9 * u0c).unsqueeze(0).expand(len(saveat), -1, -1)
+                            .contiguous(), torch.as_tensor(p_np), eta=1e-3, solver=solver)
+        t0 = time.perf_counter()
+        tc.step()
+        cpu_s = time.perf_counter() - t0
+        out.update({"cpu": cpu_s, "cpu_batch": B_cpu, "cpu_cores": 1,
+                    "cpu_kind": "port (oracle: dense Laplacian matvec + scalar KAN, C; torch CPU Tsit5 driver)",
+                    "gpu_per_trajectory": gpu_s / B_gpu, "cpu_per_trajectory": cpu_s / B_cpu,
+                    "speedup_per_trajectory": (cpu_s / B_cpu) / (gpu_s / B_gpu)})
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="fisher_kpp_256", choices=["fisher_kpp_256"])
-    ap.add_argument("--batch", type=int, default=131072, help="trajectories per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--batch-total", type=int, default=1048576,
+                    help="trajectories over all ranks (strong scaling; must divide by the world size)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="weak scaling: trajectories per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=40.0,
+                    help="CPU-baseline budget; the calibrated sample lands near 1/3 of it (~10-15 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vjp", action="store_true")
+    ap.add_argument("--no-epoch", action="store_true")
+    ap.add_argument("--epoch-batch", type=int, default=4096, help="trajectories in the training-epoch leg")
+    ap.add_argument("--epoch-steps", type=int, default=50, help="fixed Tsit5 steps per epoch (dt = 1e-3)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for one rank per GPU; gloo only to rehearse the multi-rank path")
     ap.add_argument("--no-table", action="store_true",
                     help="per-point basis recurrence instead of the piecewise-polynomial table (kan_pp.hip)")
     args = ap.parse_args()
@@ -105,16 +159,24 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()) if dist else 0)
+    torch.cuda.set_device(dev)
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if dist else 0)
-    torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            tdist.init_process_group("nccl", device_id=dev)
+        else:
+            tdist.init_process_group("gloo")
 
     nx, D = 256, 0.01
     dx = 1.0 / (nx - 1)
-    B = args.batch
+    weak = args.batch_per_gpu > 0
+    if weak:
+        B = args.batch_per_gpu
+    else:
+        if args.batch_total % world:
+            raise SystemExit(f"--batch-total {args.batch_total} does not divide by {world} ranks")
+        B = args.batch_total // world
     kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
     rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev,
                               table=False if args.no_table else None)
@@ -144,7 +206,7 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -153,7 +215,7 @@ def main() -> None:
     value = total_evals / elapsed
     alg_bytes = 8.0 * (rhs.P + B * (nx + nx))       # p + u in + du out, per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(f"{args.workload}:{'table' if table else 'recurrence'}", B)
+    traffic = load_traffic(f"{args.workload}:{'table' if table else 'recurrence'}", alg_bytes)
 
     out = {
         "metric": METRIC,
@@ -164,11 +226,12 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference IC family randomised per trajectory; random-init KAN params)",
-        "config": {"workload": "fisher_kpp_256", "nx": nx, "batch_per_gpu": B, "kan": "KDense(1,1,10) softsign rbf",
+        "config": {"workload": "fisher_kpp_256", "nx": nx, "batch_total": B * world, "batch_per_gpu": B,
+                   "kan": "KDense(1,1,10) softsign rbf",
                    "kan_eval": "piecewise-polynomial table" if table else "basis recurrence",
                    "parallelism": f"trajectory-sharded x{world} (no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -204,6 +267,10 @@ def main() -> None:
         vbytes = 8.0 * (2 * rhs.P + B * (2 * nx + nx))
         out["vjp"] = {"value": B * world / (vms * 1e-3), "unit": "VJP-evals/s", "ms_per_step": vms,
                       "achieved_GBps": vbytes / (vms * 1e-3) / 1e9}
+
+    if not args.no_epoch and rank == 0:
+        out["epoch"] = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch,
+                                   0 if (args.no_cpu_baseline or world > 1) else 8, args.epoch_steps, 1e-3, 3)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(nx, dx, D, p_np, args.cpu_seconds)
