@@ -94,7 +94,8 @@ def cpu_baseline(nx, dx, D, p_np, target_s: float):
 
 def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: float, reps: int):
     """Wall-clock of one training epoch (BASELINE metric, second half): fixed-step Tsit5 forward
-    solve with saveat, discrete adjoint through every stage (HIP VJP), loss, Adam update
+    solve with saveat (dense output kept), the InterpolatingAdjoint backward solve (the reference's
+    SciMLSensitivity default; one kanode_vjp_stage per adjoint stage), loss, Adam update
     (kanode.Trainer.step; Fisher-KPP_Source.jl:102-109,167-201).  The CPU reference runs the
     same epoch through the oracle (dense Nx x Nx Laplacian matvec, as the reference does) on a
     bounded sample of B_cpu trajectories; per-trajectory times are reported for both."""
@@ -115,7 +116,7 @@ def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: fl
     torch.cuda.synchronize()
     gpu_s = (time.perf_counter() - t0) / reps
     out = {"unit": "s/epoch", "gpu": gpu_s, "gpu_batch": B_gpu, "steps": steps, "dt": dt, "stages_per_step": 6,
-           "what": "fixed-step Tsit5 solve + discrete adjoint + Adam, FK256 fp64"}
+           "what": "fixed-step Tsit5 solve + InterpolatingAdjoint + Adam, FK256 fp64"}
     if B_cpu > 0:
         from oracle import oracle as O
         from oracle.oracle_rhs import OracleFKRHS
@@ -131,6 +132,28 @@ def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: fl
                     "gpu_per_trajectory": gpu_s / B_gpu, "cpu_per_trajectory": cpu_s / B_cpu,
                     "speedup_per_trajectory": (cpu_s / B_cpu) / (gpu_s / B_gpu)})
     return out
+
+
+def lv4096_bench(dev, steps: int = 200):
+    """BASELINE configs[1]: Lotka-Volterra KAN [2,10,2] grid=5, 4096 batched ICs, fp32 — the
+    NeuralODE dudt (LV_driver_KANODE.jl:139-143,180) over the batch, as RHS evals/s."""
+    chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
+    rhs = kanode.ChainRHS(chain, dtype=torch.float32, device=dev)
+    p = torch.as_tensor(chain.setup(np.random.default_rng(0))[0] / 1e5, dtype=torch.float32, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    u = (0.5 + 1.5 * torch.rand(4096, 2, generator=g)).to(dev, torch.float32)
+    du = torch.empty_like(u)
+    rhs.hd.reserve(4096)
+    for _ in range(10):
+        rhs.rhs(u, p, du)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rhs.rhs(u, p, du)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": 4096 / dt, "unit": "RHS-evals/s", "us_per_launch": dt * 1e6, "batch": 4096, "dtype": "f32",
+            "note": "one launch per layer; launch-bound at this size (32 KB of state)"}
 
 
 def main() -> None:
@@ -267,6 +290,9 @@ def main() -> None:
         vbytes = 8.0 * (2 * rhs.P + B * (2 * nx + nx))
         out["vjp"] = {"value": B * world / (vms * 1e-3), "unit": "VJP-evals/s", "ms_per_step": vms,
                       "achieved_GBps": vbytes / (vms * 1e-3) / 1e9}
+
+    if rank == 0 and not args.no_vjp:
+        out["lv4096"] = lv4096_bench(dev)
 
     if not args.no_epoch and rank == 0:
         out["epoch"] = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch,

@@ -165,6 +165,19 @@ typedef struct {
 } kanode_stage;
 kanode_status kanode_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* stage, void* du,
                                int64_t batch, void* stream);
+
+/* Adjoint stage (SciMLSensitivity InterpolatingAdjoint with a VJP of the RHS: one RHS
+ * evaluation of the adjoint ODE, written in reversed time τ = t_f - t as
+ * dλ/dτ = λᵀ∂f/∂u, dμ/dτ = λᵀ∂f/∂p):
+ *     y    = u + Σ_{j<state->n_prev} state->c[j]·state->k[j]  (the forward dense output at t)
+ *     λs   = lam + Σ_{j<adj->n_prev} adj->c[j]·adj->k[j]      (adjoint stage input; -> adj->y_out)
+ *     lamJ = λsᵀ ∂f/∂u at y;   dp (nullable) += λsᵀ ∂f/∂p at y
+ *     adj->want_error: *adj->error_sumsq = Σ (e/sk)² over the λ entries,
+ *                      e = Σ adj->ec[j] adj->k[j] + adj->ec[n]·lamJ, sk = abstol + reltol·max(|lam|, |λs|)
+ * state->y_out and state->want_error are ignored. */
+kanode_status kanode_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
+                               const void* lam, const kanode_stage* adj, void* lamJ, void* dp, int64_t batch,
+                               void* stream);
 /* lam_J[N,B] = (∂f/∂u)ᵀ lam   (nullable: skip)
  * dp[P]     += Σ_b (∂f/∂p)ᵀ lam  (nullable: skip) */
 kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,

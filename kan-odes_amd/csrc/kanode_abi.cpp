@@ -395,6 +395,8 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
     return KANODE_OK;
 }
 
+kanode_status ensure_stage_ws(kanode_handle* h, size_t need, hipStream_t st);
+
 template <typename T>
 kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* sg, T* du, int64_t B,
                       hipStream_t st) {
@@ -428,22 +430,67 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
     const int64_t n = h->n_in * B;
     T* y = (T*)sg->y_out;
     if (!y) {
-        const size_t need = (size_t)n * sizeof(T);
-        if (need > h->stage_ws_bytes) {
-            if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "stage workspace too small during capture");
-            HIP_TRY(h, hipStreamSynchronize(st));
-            if (h->stage_ws) HIP_TRY(h, hipFree(h->stage_ws));
-            h->stage_ws = nullptr;
-            h->stage_ws_bytes = 0;
-            HIP_TRY(h, hipMalloc(&h->stage_ws, need));
-            h->stage_ws_bytes = need;
-        }
+        kanode_status s = ensure_stage_ws(h, (size_t)n * sizeof(T), st);
+        if (s != KANODE_OK) return s;
         y = (T*)h->stage_ws;
     }
     HIP_TRY(h, kan::launch_stage_lincomb<T>(u, sa, y, n, st));
     kanode_status s = rhs_t<T>(h, p, y, du, B, st);
     if (s != KANODE_OK) return s;
     if (err_out) HIP_TRY(h, kan::launch_stage_error<T>(u, y, du, sa, (double*)h->slab, kSlabBlocks, err_out, n, st));
+    return KANODE_OK;
+}
+
+// stage workspace of at least `need` bytes (the unfused stage paths)
+kanode_status ensure_stage_ws(kanode_handle* h, size_t need, hipStream_t st) {
+    if (need <= h->stage_ws_bytes) return KANODE_OK;
+    if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "stage workspace too small during capture");
+    HIP_TRY(h, hipStreamSynchronize(st));
+    if (h->stage_ws) HIP_TRY(h, hipFree(h->stage_ws));
+    h->stage_ws = nullptr;
+    h->stage_ws_bytes = 0;
+    HIP_TRY(h, hipMalloc(&h->stage_ws, need));
+    h->stage_ws_bytes = need;
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status stage_args(kanode_handle* h, const kanode_stage* sg, kan::StageArgs<T>& sa) {
+    if (sg->n_prev < 0 || sg->n_prev > KANODE_MAX_STAGES)
+        return fail(h, KANODE_ERR_INVALID_ARG, "n_prev must be in [0, KANODE_MAX_STAGES]");
+    sa = kan::StageArgs<T>{};
+    sa.nk = sg->n_prev;
+    for (int j = 0; j < sg->n_prev; ++j) {
+        if (!sg->k[j]) return fail(h, KANODE_ERR_INVALID_ARG, "null stage vector k[" + std::to_string(j) + "]");
+        sa.k[j] = (const T*)sg->k[j];
+        sa.c[j] = sg->c[j];
+    }
+    for (int j = 0; j <= sg->n_prev; ++j) sa.ec[j] = sg->want_error ? sg->ec[j] : 0.0;
+    sa.abstol = sg->abstol;
+    sa.reltol = sg->reltol;
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* state, const T* lam,
+                          const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st) {
+    if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "adjoint stage needs an RHS with N_in == N_out");
+    if (adj->want_error && !adj->error_sumsq) return fail(h, KANODE_ERR_INVALID_ARG, "want_error needs error_sumsq");
+    kan::StageArgs<T> su, sl;
+    kanode_status s = stage_args<T>(h, state, su);
+    if (s != KANODE_OK) return s;
+    s = stage_args<T>(h, adj, sl);
+    if (s != KANODE_OK) return s;
+    const int64_t n = h->n_in * B;
+    if ((s = ensure_stage_ws(h, 2 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
+    T* y = su.nk ? (T*)h->stage_ws : (T*)u;
+    T* ls = adj->y_out ? (T*)adj->y_out : (sl.nk ? (T*)h->stage_ws + n : (T*)lam);
+    if (su.nk) HIP_TRY(h, kan::launch_stage_lincomb<T>(u, su, y, n, st));
+    if (sl.nk || adj->y_out) HIP_TRY(h, kan::launch_stage_lincomb<T>(lam, sl, ls, n, st));
+    if ((s = vjp_t<T>(h, p, y, ls, lamJ, dp, B, st)) != KANODE_OK) return s;
+    if (adj->want_error)
+        HIP_TRY(h, kan::launch_stage_error<T>(lam, ls, lamJ, sl, (double*)h->slab, kSlabBlocks,
+                                              (double*)adj->error_sumsq, n, st));
     return KANODE_OK;
 }
 
@@ -643,6 +690,23 @@ kanode_status kanode_rhs_stage(kanode_handle* h, const void* p, const void* u, c
     if (h->spec.dtype == KANODE_F64) return stage_t<double>(h, (const double*)p, (const double*)u, stage, (double*)du,
                                                             batch, st);
     return stage_t<float>(h, (const float*)p, (const float*)u, stage, (float*)du, batch, st);
+}
+
+kanode_status kanode_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
+                               const void* lam, const kanode_stage* adj, void* lamJ, void* dp, int64_t batch,
+                               void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (!state || !adj) return fail(h, KANODE_ERR_INVALID_ARG, "null stage");
+    if (batch < 0) return fail(h, KANODE_ERR_INVALID_ARG, "batch < 0");
+    if (batch == 0) return KANODE_OK;
+    if (!p || !u || !lam || !lamJ) return fail(h, KANODE_ERR_INVALID_ARG, "null p/u/lam/lamJ");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return vjp_stage_t<double>(h, (const double*)p, (const double*)u, state, (const double*)lam, adj,
+                                   (double*)lamJ, (double*)dp, batch, st);
+    return vjp_stage_t<float>(h, (const float*)p, (const float*)u, state, (const float*)lam, adj, (float*)lamJ,
+                              (float*)dp, batch, st);
 }
 
 kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,

@@ -10,10 +10,12 @@ from .handle import KanodeHandle, LayerCfg
 from .layers import Chain, KDense, glorot_uniform, linrange_f32
 from .rhs import ChainRHS, FisherKPPRHS, fisher_kpp_laplacian, layer_apply, rhs_apply
 from .ode import Solution, Tsit5Options, solve
+from .adjoint import DenseRecord, interpolating_adjoint
 from .train import Adam, Trainer, mse_loss, reg_loss
 from . import checkpoint
 
 __all__ = [
+    "DenseRecord", "interpolating_adjoint",
     "KanodeError", "LIB_PATH", "lib", "KanodeHandle", "LayerCfg", "Chain", "KDense", "glorot_uniform",
     "linrange_f32", "ChainRHS", "FisherKPPRHS", "fisher_kpp_laplacian", "layer_apply", "rhs_apply",
     "Solution", "Tsit5Options", "solve", "Adam", "Trainer", "mse_loss", "reg_loss", "checkpoint",

@@ -83,6 +83,7 @@ SIGNATURES = [
     ("kanode_get_option", C.c_int64, [_H, C.c_int32]),
     ("kanode_rhs", C.c_int, [_H, _P, _P, _P, C.c_int64, _P]),
     ("kanode_rhs_stage", C.c_int, [_H, _P, _P, C.POINTER(StageC), _P, C.c_int64, _P]),
+    ("kanode_vjp_stage", C.c_int, [_H, _P, _P, C.POINTER(StageC), _P, C.POINTER(StageC), _P, _P, C.c_int64, _P]),
     ("kanode_vjp", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64, _P]),
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
     ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),

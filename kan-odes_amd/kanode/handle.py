@@ -148,6 +148,51 @@ class KanodeHandle:
                 "kanode_rhs")
         return du
 
+    @staticmethod
+    def _stage_struct(ks, c, y_out=None, error=None) -> "L.StageC":
+        if len(ks) != len(c) or len(ks) > L.MAX_STAGES:
+            raise ValueError("ks and c must have equal length <= KANODE_MAX_STAGES")
+        sg = L.StageC()
+        sg.n_prev = len(ks)
+        for j, (k, cj) in enumerate(zip(ks, c)):
+            sg.k[j] = k.data_ptr()
+            sg.c[j] = float(cj)
+        if y_out is not None:
+            sg.y_out = y_out.data_ptr()
+        if error is not None:
+            ec, abstol, reltol, sumsq = error
+            if len(ec) != len(ks) + 1:
+                raise ValueError("error coefficients need len(ks) + 1 entries")
+            if sumsq.dtype != torch.float64 or sumsq.numel() < 1:
+                raise ValueError("sumsq must be a float64 device tensor")
+            sg.want_error = 1
+            for j, e in enumerate(ec):
+                sg.ec[j] = float(e)
+            sg.abstol, sg.reltol = float(abstol), float(reltol)
+            sg.error_sumsq = sumsq.data_ptr()
+        return sg
+
+    def vjp_stage(self, p, u, ks, c, lam, lks, lc, lam_out=None, error=None, dp=None):
+        """Adjoint stage (kanode_vjp_stage): with y = u + Σ c_j k_j (forward dense output) and
+        λs = lam + Σ lc_j lk_j (adjoint stage input, written to lam_out if given), returns
+        (λsᵀ∂f/∂u at y, dp) with dp accumulated (+=) — a fresh zero vector when dp is None."""
+        B = u.shape[0] if u.dim() == 2 else 1
+        self._check_t(p, (self.P,), "p")
+        for x, nm in [(u, "u"), (lam, "lam")] + [(k, "k") for k in ks] + [(k, "lk") for k in lks]:
+            self._check_t(x, tuple(u.shape), nm)
+        if lam_out is not None:
+            self._check_t(lam_out, tuple(u.shape), "lam_out")
+        if error is not None and error[3].device != self.device:
+            raise ValueError("sumsq must live on the handle's device")
+        su = self._stage_struct(ks, c)
+        sl = self._stage_struct(lks, lc, lam_out, error)
+        lamJ = torch.empty_like(u)
+        if dp is None:
+            dp = torch.zeros_like(p)
+        L.check(L.lib().kanode_vjp_stage(self._h, _ptr(p), _ptr(u), C.byref(su), _ptr(lam), C.byref(sl), _ptr(lamJ),
+                                         _ptr(dp), B, _stream(self.device)), self._h, "kanode_vjp_stage")
+        return lamJ, dp
+
     def rhs_stage(self, p: torch.Tensor, u: torch.Tensor, ks, c, y_out: torch.Tensor | None = None,
                   error=None, out: torch.Tensor | None = None):
         """Runge-Kutta stage: du = f(u + Σ_j c_j k_j; p) (kanode_rhs_stage).

@@ -133,11 +133,16 @@ def _step_fused(f, u, p, t, dt, k1, opt: Tsit5Options):
     return unew, ks, eest
 
 
-def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Options | None = None) -> Solution:
-    """solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat, abstol, reltol) on device tensors.
+def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Options | None = None,
+          sensealg: str = "discrete", dense_record=None) -> Solution:
+    """solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat, abstol, reltol, sensealg) on device tensors.
 
     f(u, p, t) -> du (out-of-place, ODEFunction{false}); u0 any shape (e.g. (B, N)).
-    Differentiable w.r.t. u0 and p when f is (kanode RHS objects are)."""
+    Differentiable w.r.t. u0 and p when f is (kanode RHS objects are):
+      sensealg="discrete"              reverse mode through every stage (discrete adjoint);
+      sensealg="interpolating_adjoint" SciMLSensitivity's InterpolatingAdjoint, the reference's
+                                       default (kanode.adjoint; f needs `vjp_stage`).
+    dense_record: an adjoint.DenseRecord that receives every accepted step."""
     opt = opt or Tsit5Options()
     t0, tf = float(tspan[0]), float(tspan[1])
     if saveat is None:
@@ -146,6 +151,11 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
         n = int(round((tf - t0) / saveat))
         saveat = [t0 + i * saveat for i in range(n + 1)]
     saveat = [float(s) for s in saveat]
+    if sensealg not in ("discrete", "interpolating_adjoint"):
+        raise ValueError(f"unknown sensealg {sensealg!r}")
+    if sensealg == "interpolating_adjoint" and torch.is_grad_enabled() and (p.requires_grad or u0.requires_grad):
+        from .adjoint import solve_interpolating_adjoint
+        return solve_interpolating_adjoint(f, u0, tspan, p, saveat, opt)
     out = []
     si = 0
     while si < len(saveat) and saveat[si] <= t0 + 1e-14 * max(1.0, abs(t0)):
@@ -199,6 +209,8 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
                 w = interp_weights((ts - t) / dt)
                 out.append(u + dt * sum(wi * k for wi, k in zip(w, ks)))
             si += 1
+        if dense_record is not None:
+            dense_record.add(t, dt, u, ks)
         t, u, k1 = tn, unew, ks[6]
         naccept += 1
         dt = dtnew

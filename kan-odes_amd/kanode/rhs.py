@@ -113,6 +113,10 @@ class ChainRHS:
         """Fused Runge-Kutta stage f(u + Σ c_j k_j) (see kanode_rhs_stage)."""
         return stage_apply(self.hd, p, u, ks, c, want_y, error)
 
+    def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
+        """Adjoint stage (see kanode_vjp_stage): (λsᵀ∂f/∂u, λsᵀ∂f/∂p) at u + Σ c_j k_j."""
+        return self.hd.vjp_stage(p, u, ks, c, lam, lks, lc, lam_out, error)
+
     def rhs(self, u, p, out=None):
         return self.hd.rhs(p, u, out)
 
@@ -150,6 +154,10 @@ class FisherKPPRHS:
     def stage(self, u, p, ks, c, want_y=False, error=None):
         """Fused Runge-Kutta stage f(u + Σ c_j k_j) (see kanode_rhs_stage)."""
         return stage_apply(self.hd, p, u, ks, c, want_y, error)
+
+    def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
+        """Adjoint stage (see kanode_vjp_stage): (λsᵀ∂f/∂u, λsᵀ∂f/∂p) at u + Σ c_j k_j."""
+        return self.hd.vjp_stage(p, u, ks, c, lam, lks, lc, lam_out, error)
 
     def rhs(self, u, p, out=None):
         return self.hd.rhs(p, u, out)

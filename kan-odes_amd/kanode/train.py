@@ -64,7 +64,7 @@ class Trainer:
     (len(saveat), *u0.shape).  `group` is a torch.distributed process group (or None)."""
 
     def __init__(self, rhs, u0, tspan, saveat, target, p0, eta: float = 5e-4, solver: Tsit5Options | None = None,
-                 sparse_reg: float = 0.0, group=None):
+                 sparse_reg: float = 0.0, group=None, sensealg: str | None = None):
         self.rhs, self.u0, self.tspan, self.saveat, self.target = rhs, u0, tspan, saveat, target
         self.p = p0.detach().clone()
         self.opt = Adam(eta)
@@ -72,9 +72,12 @@ class Trainer:
         self.sparse_reg = sparse_reg
         self.group = group
         self.history = []
+        # the reference's default (NeuralODE: InterpolatingAdjoint(autojacvec = ZygoteVJP())) where the
+        # RHS provides the adjoint stage, else reverse mode through the solver steps
+        self.sensealg = sensealg or ("interpolating_adjoint" if hasattr(rhs, "vjp_stage") else "discrete")
 
     def predict(self, p) -> Solution:
-        return solve(self.rhs, self.u0, self.tspan, p, self.saveat, self.solver)
+        return solve(self.rhs, self.u0, self.tspan, p, self.saveat, self.solver, sensealg=self.sensealg)
 
     def loss_and_grad(self):
         p = self.p.detach().requires_grad_(True)

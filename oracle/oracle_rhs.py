@@ -27,12 +27,44 @@ class _OracleChainFn(torch.autograd.Function):
         return None, torch.as_tensor(pb), torch.as_tensor(xb.reshape(u.shape))
 
 
+def _vjp_stage(vjp, u, ks, c, lam, lks, lc, lam_out, error):
+    """CPU restatement of kanode_vjp_stage around an oracle VJP (same arithmetic order as the
+    kernel's stage combination: fma over j ascending)."""
+    y = u.clone()
+    for cj, kj in zip(c, ks):
+        y = torch.addcmul(y, kj, torch.full_like(kj, cj))
+    ls = lam.clone()
+    for cj, kj in zip(lc, lks):
+        ls = torch.addcmul(ls, kj, torch.full_like(kj, cj))
+    lamJ, dp = vjp(y, ls)
+    if lam_out is not None:
+        lam_out.copy_(ls)
+    if error is not None:
+        ec, abstol, reltol, sumsq = error
+        e = torch.zeros_like(lam)
+        for ej, kj in zip(ec[:-1], lks):
+            e = e + ej * kj
+        e = e + ec[-1] * lamJ
+        sk = abstol + reltol * torch.maximum(lam.abs(), ls.abs())
+        sumsq.fill_(float(((e / sk) ** 2).sum()))
+    return lamJ, dp
+
+
 class OracleChainRHS:
     def __init__(self, specs):
         self.specs = specs
 
     def __call__(self, u, p, t=None):
         return _OracleChainFn.apply(self.specs, p, u)
+
+    def vjp(self, y, p, lam):
+        s = self.specs
+        xb, pb = O.chain_vjp(s, p.detach().numpy(), y.detach().numpy().reshape(-1, s[0].in_dims),
+                             lam.detach().numpy().reshape(-1, s[-1].out_dims))
+        return torch.as_tensor(xb.reshape(y.shape)), torch.as_tensor(pb)
+
+    def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
+        return _vjp_stage(lambda y, ls: self.vjp(y, p, ls), u, ks, c, lam, lks, lc, lam_out, error)
 
 
 class _OracleFKFn(torch.autograd.Function):
@@ -56,3 +88,11 @@ class OracleFKRHS:
 
     def __call__(self, u, p, t=None):
         return _OracleFKFn.apply(self.spec, self.D, self.dx, self.dense, p, u)
+
+    def vjp(self, y, p, lam):
+        lj, dp = O.fk_vjp(self.spec, p.detach().numpy(), self.D, self.dx, y.detach().numpy(),
+                          np.ascontiguousarray(lam.detach().numpy()))
+        return torch.as_tensor(lj), torch.as_tensor(dp)
+
+    def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
+        return _vjp_stage(lambda y, ls: self.vjp(y, p, ls), u, ks, c, lam, lks, lc, lam_out, error)
