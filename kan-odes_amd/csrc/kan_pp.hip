@@ -318,6 +318,9 @@ typedef double kd2 __attribute__((ext_vector_type(2)));
 #ifndef KAN_PP_NT
 #define KAN_PP_NT 1
 #endif
+#ifndef KAN_PP_ROWS
+#define KAN_PP_ROWS 1
+#endif
 __device__ __forceinline__ kd2 ld_stream(const double* p) {
 #if KAN_PP_NT
     return __builtin_nontemporal_load(reinterpret_cast<const kd2*>(p));
@@ -345,56 +348,71 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                       const double* __restrict__ u, double* __restrict__ du, int64_t B) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
+    constexpr int R = KAN_PP_ROWS;   // rows per wave per pipeline step
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
     int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    // the first row's loads are in flight while the block stages its table
-    kd2 v[NP];
-    if (b < B) {
+    // the first rows' loads are in flight while the block stages its table
+    kd2 v[R][NP];
 #pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = ld_stream(u + b * Nx + 128 * k + 2 * lane);
+    for (int r = 0; r < R; ++r) {
+        const int64_t br = b + r * rstride;
+        if (br < B) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[r][k] = ld_stream(u + br * Nx + 128 * k + 2 * lane);
+        }
     }
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
-    for (; b < B; b += rstride) {
-        // software pipeline: the next row's loads are issued before this row's math
-        const int64_t bn = b + rstride;
-        kd2 vn[NP];
-        if (bn < B) {
+    for (; b < B; b += R * rstride) {
+        // software pipeline: the next R rows' loads are issued before these rows' math
+        kd2 vn[R][NP];
 #pragma unroll
-            for (int k = 0; k < NP; ++k) vn[k] = ld_stream(u + bn * Nx + 128 * k + 2 * lane);
-        }
-        double* __restrict__ db = du + b * Nx;
-        double rr[NP], rl[NP];
+        for (int r = 0; r < R; ++r) {
+            const int64_t bn = b + (R + r) * rstride;
+            if (bn < B) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            rr[k] = wave_ror1(v[k].y);
-            rl[k] = wave_rol1(v[k].x);
-        }
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
-            const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
-            const int i = 128 * k + 2 * lane;
-            bool ok0, ok1;
-            double k0 = pp_eval(tl, ni, inv_w, x0, v[k].x, ok0);
-            double k1 = pp_eval(tl, ni, inv_w, x0, v[k].y, ok1);
-            if (__builtin_expect(!(ok0 && ok1), 0)) {
-                double sc;
-                if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[k].x, sc);
-                if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[k].y, sc);
+                for (int k = 0; k < NP; ++k) vn[r][k] = ld_stream(u + bn * Nx + 128 * k + 2 * lane);
             }
-            double l0, l1;
-            lap_pair<double>(um, v[k].x, v[k].y, up, i, Nx, cd, co, l0, l1);
-            kd2 o;
-            o.x = l0 + k0;
-            o.y = l1 + k1;
-            st_stream(db + i, o);
         }
 #pragma unroll
-        for (int k = 0; k < NP; ++k) v[k] = vn[k];
+        for (int r = 0; r < R; ++r) {
+            const int64_t br = b + r * rstride;
+            if (R > 1 && br >= B) break;
+            double* __restrict__ db = du + br * Nx;
+            double rr[NP], rl[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                rr[k] = wave_ror1(v[r][k].y);
+                rl[k] = wave_rol1(v[r][k].x);
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+                const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+                const int i = 128 * k + 2 * lane;
+                bool ok0, ok1;
+                double k0 = pp_eval(tl, ni, inv_w, x0, v[r][k].x, ok0);
+                double k1 = pp_eval(tl, ni, inv_w, x0, v[r][k].y, ok1);
+                if (__builtin_expect(!(ok0 && ok1), 0)) {
+                    double sc;
+                    if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[r][k].x, sc);
+                    if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, v[r][k].y, sc);
+                }
+                double l0, l1;
+                lap_pair<double>(um, v[r][k].x, v[r][k].y, up, i, Nx, cd, co, l0, l1);
+                kd2 o;
+                o.x = l0 + k0;
+                o.y = l1 + k1;
+                st_stream(db + i, o);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int k = 0; k < NP; ++k) v[r][k] = vn[r][k];
     }
 }
 
@@ -722,7 +740,8 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
-        static const int ovr = getenv("KANODE_PP_GRID") ? atoi(getenv("KANODE_PP_GRID")) : 0;                   \
+        const char* ovs = getenv("KANODE_PP_GRID");   /* experiments: grid override */             \
+        const int ovr = ovs ? atoi(ovs) : 0;                                                                     \
         const int grid = grid_for(B, kBlock / kWave, ovr > 0 ? ovr : cap);                                       \
         hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B);                  \

@@ -11,7 +11,7 @@ TAG=${TAG:-r01}
 OUT=gpurun_out/profile_$TAG; mkdir -p $OUT
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   echo "== pytest -m gpu"
-  timeout -k 10 900 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 3; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 3; }
   tail -2 $OUT/pytest_gpu.log
   echo "== smoke"
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 3; }
