@@ -183,6 +183,63 @@ kanode_status kanode_vjp_stage(kanode_handle* h, const void* p, const void* u, c
 kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J, void* dp,
                          int64_t batch, void* stream);
 
+/* --- the integrator around the RHS ------------------
+ * solve(ODEProblem(f, u0, (t0, tf), p), Tsit5(); saveat, abstol, reltol[, dt, adaptive])
+ *     (LV_driver_KANODE.jl:122,180-184; Fisher-KPP_Source.jl:102-103), run as a
+ *     native host loop issuing stream-ordered kernels: every stage is one
+ *     kanode_rhs_stage (the stage combination formed inside the RHS kernel), the
+ *     RHS tables are built once per solve (p is constant within it), saveat values
+ *     come from the dense output on the device.  Semantics restate OrdinaryDiffEqTsit5
+ *     1.1.0 / OrdinaryDiffEq 6.89 (third-party, pinned at Lotka-Volterra/Manifest.toml):
+ *     Tsitouras 5(4) with FSAL, error norm = RMS over ALL N*B state entries (a batched
+ *     state is one ODE), PI controller, Hairer-Wanner initial step, saveat from the
+ *     free 4th-order interpolant.
+ *   adaptive = 1: one 8-byte device->host read of the error norm per step (the
+ *     accept/reject decision); adaptive = 0 (fixed dt): no host synchronisation at
+ *     all, so the whole solve can be captured into a hipGraph (reserve + a reused
+ *     kanode_solution first).
+ * kanode_adjoint_tsit5 is SciMLSensitivity 7.69's InterpolatingAdjoint (the NeuralODE
+ * default; the reference's gradients): the adjoint ODE [λ; μ] integrated backward
+ * with Tsit5 at the same tolerances, u(t) from the forward dense output, λ += ∂L/∂u
+ * at every saveat time (tstops, FSAL re-evaluated after each jump); every adjoint
+ * stage is one kanode_vjp_stage. */
+typedef struct {
+    double abstol, reltol;          /* 1e-6, 1e-3 */
+    double dt;                      /* adaptive = 0: the fixed step; adaptive = 1: initial step, 0 = Hairer-Wanner */
+    int32_t adaptive;               /* 1 */
+    int64_t maxiters;               /* 100000 */
+    double dtmin;                   /* 0 */
+    double beta1, beta2, gamma;     /* 7/50, 2/25, 9/10 */
+    double qmin, qmax, qoldinit;    /* 1/5, 10, 1e-4 */
+} kanode_solver_options;
+void kanode_solver_options_default(kanode_solver_options* opt);
+
+typedef struct {
+    int64_t naccept, nreject, nf;   /* accepted / rejected steps, RHS (or VJP) evaluations */
+} kanode_solve_stats;
+
+/* Dense output of one forward solve (device memory owned by the object: u_n and the
+ * 7 stage vectors of every accepted step).  Reusable: passing an existing object to
+ * kanode_solve_tsit5 reuses its storage when large enough. */
+typedef struct kanode_solution kanode_solution;
+void kanode_solution_free(kanode_solution* sol);
+int64_t kanode_solution_steps(const kanode_solution* sol);
+
+/* u_save[n_save, N, B] (device) <- u(saveat[j]); saveat (host, ascending, within
+ * [t0, tf]).  dense: NULL = no dense output kept; else *dense (NULL or an object to
+ * reuse) receives it, for kanode_adjoint_tsit5. */
+kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch, double t0,
+                                 double tf, const double* saveat, int64_t n_save, void* u_save,
+                                 const kanode_solver_options* opt, kanode_solution** dense,
+                                 kanode_solve_stats* stats, void* stream);
+
+/* Given the forward solution `dense` (same h, p, batch) and dl_du[n_save, N, B] (device;
+ * ∂L/∂u at the forward saveat times), writes du0[N, B] = dL/du0 and dp[P] = dL/dp
+ * (both device, overwritten).  Either output may be NULL. */
+kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,
+                                   const void* dl_du, void* du0, void* dp, const kanode_solver_options* opt,
+                                   kanode_solve_stats* stats, void* stream);
+
 /* host-pointer variants (synchronous) */
 kanode_status kanode_rhs_host(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch);
 kanode_status kanode_vjp_host(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J,

@@ -35,25 +35,34 @@ hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageAr
                               int slab_blocks, double* out, int64_t n, hipStream_t st);
 hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, hipStream_t st);
 
-// piecewise-polynomial Fisher-KPP RHS / VJP (kan_pp.hip).  `tables` holds
+// piecewise-polynomial Fisher-KPP RHS / VJP (kan_pp.hip).  build = false reuses the
+// tables of an earlier launch with the same p (the integrator holds them per solve).  `tables` holds
 // kPPMaxFns slots of kPPCoef·ni doubles (slot = PPFn id); the build fills the listed
 // functions from p, the RHS then reads slot PP_PHI (fp64, Nx even).
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
                               double* tables, const int* fns, int nfn, hipStream_t st);
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
-                            hipStream_t st);
+                            hipStream_t st, bool build = true);
 bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx);
 bool fk_stage_pp_supported(const PPConst& hpc, int Nx);
 // fused stage: du = f(u + Σ c_j k_j), optional y_out, optional error total into err_out[0]
 hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                               const double* p, double* table, double cd, double co, int Nx, const double* u,
                               const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
-                              double* err_out, double* du, int64_t B, hipStream_t st);
+                              double* err_out, double* du, int64_t B, hipStream_t st, bool build = true);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
-                            hipStream_t st);
+                            hipStream_t st, bool build = true);
+// adjoint stage, fused (kanode_vjp_stage): y = u + Σ su.c_j su.k_j, λs = lam + Σ sl.c_j sl.k_j
+// in registers (λs -> lam_out if non-null), λᵀJ at y, dp (= if dp_assign, else +=), the λ
+// error total -> err_out[0] when non-null (sl.ec / abstol / reltol)
+hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                  const double* p, double* tables, double cd, double co, int Nx, const double* u,
+                                  const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
+                                  double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
+                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build = true);
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                              hipStream_t st);

@@ -523,12 +523,17 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 // nontemporal stores; per-thread dC/dW registers, block-summed into the slab row
 // of this block (ordered: bitwise reproducible for a given grid).  Dynamic LDS:
 // the PP_DPHI and PP_SWISH tables, [2][kPPCoef/2][ni] double2.
-template <int NORM, int PATH, int GT, int NP>
+// STG (kanode_vjp_stage, the adjoint stage): the forward dense output y = u + Σ su.c_j su.k_j
+// and the adjoint stage input λs = lam + Σ sl.c_j sl.k_j are formed in registers (λs written
+// to lam_out when non-null); with err_slab the λ error Σ (e/sk)², e = Σ sl.ec_j sl.k_j +
+// sl.ec_nk λᵀJ, sk = abstol + reltol·max(|lam|,|λs|), is block-summed into err_slab[block].
+template <int NORM, int PATH, int GT, int NP, bool STG>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))   // LDS allows 3 blocks/CU
 fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                       const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
-                      double* __restrict__ slab, int64_t B) {
+                      double* __restrict__ slab, int64_t B, StageArgs<double> su, StageArgs<double> sl,
+                      double* __restrict__ lam_out, double* __restrict__ err_slab) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[(kBlock / kWave) * (GT + 1)];
@@ -551,14 +556,56 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         S1[j] = S2[j] = 0.0f;
     }
     double dW = 0.0;
+    const bool want_err = STG && err_slab != nullptr;
+    double eacc = 0.0;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
     for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
-        kd2 uv[NP], lv[NP];
+        const int64_t rb = b * Nx + 2 * lane;
+        kd2 uv[NP], lv[NP], l0[NP], ev[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            uv[k] = ld_stream(u + b * Nx + 128 * k + 2 * lane);
-            lv[k] = ld_stream(lam + b * Nx + 128 * k + 2 * lane);
+            uv[k] = ld_stream(u + rb + 128 * k);
+            lv[k] = ld_stream(lam + rb + 128 * k);
+        }
+        if constexpr (STG) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                l0[k] = lv[k];
+                ev[k] = kd2{0.0, 0.0};
+            }
+#pragma unroll
+            for (int j = 0; j < kMaxStages; ++j) {
+                if (j < su.nk) {
+                    const double cj = su.c[j];
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) {
+                        const kd2 kj = ld_stream(su.k[j] + rb + 128 * k);
+                        uv[k].x = ::fma(cj, kj.x, uv[k].x);
+                        uv[k].y = ::fma(cj, kj.y, uv[k].y);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kMaxStages; ++j) {
+                if (j < sl.nk) {
+                    const double cj = sl.c[j], ej = sl.ec[j];
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) {
+                        const kd2 kj = ld_stream(sl.k[j] + rb + 128 * k);
+                        lv[k].x = ::fma(cj, kj.x, lv[k].x);
+                        lv[k].y = ::fma(cj, kj.y, lv[k].y);
+                        if (want_err) {
+                            ev[k].x = ::fma(ej, kj.x, ev[k].x);
+                            ev[k].y = ::fma(ej, kj.y, ev[k].y);
+                        }
+                    }
+                }
+            }
+            if (lam_out) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) st_stream(lam_out + rb + 128 * k, lv[k]);
+            }
         }
         double rr[NP], rl[NP];
 #pragma unroll
@@ -577,7 +624,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         // and exponentials are live next to the 40 accumulator VGPRs
 #pragma unroll 1
         for (int k = 0; k < NP; ++k) {
-            kd2 uk = uv[0], lk = lv[0];
+            kd2 uk = uv[0], lk = lv[0], l0k = l0[0], ek = ev[0];
             double a0 = la[0][0], a1 = la[0][1];
 #pragma unroll
             for (int q = 1; q < NP; ++q) {
@@ -586,6 +633,10 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                     lk = lv[q];
                     a0 = la[q][0];
                     a1 = la[q][1];
+                    if constexpr (STG) {
+                        l0k = l0[q];
+                        ek = ev[q];
+                    }
                 }
             }
             const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0, S1,
@@ -596,7 +647,16 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             kd2 o;
             o.x = a0 + x0b;
             o.y = a1 + x1b;
-            st_stream(lamJ + b * Nx + 128 * k + 2 * lane, o);
+            st_stream(lamJ + rb + 128 * k, o);
+            if (want_err) {
+                const double en = sl.ec[sl.nk];
+                const double ex = ::fma(en, o.x, ek.x), ey = ::fma(en, o.y, ek.y);
+                const double sx = ::fma(sl.reltol, fmax(kabs(l0k.x), kabs(lk.x)), sl.abstol);
+                const double sy = ::fma(sl.reltol, fmax(kabs(l0k.y), kabs(lk.y)), sl.abstol);
+                const double rx = ex / sx, ry = ey / sy;
+                eacc = ::fma(rx, rx, eacc);
+                eacc = ::fma(ry, ry, eacc);
+            }
         }
     }
     const int P = GT + (lc.use_base ? 1 : 0);
@@ -609,6 +669,35 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     }
     acc[GT] = dW;
     block_sum_to<double, GT + 1>(acc, P, red, slab + (int64_t)blockIdx.x * P);
+    if (want_err) {
+        __syncthreads();   // red is reused
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+    }
+}
+
+// dp[q] (= or +=) Σ_b slab[b·P + q] for q < P (block q), and err_out[0] = Σ_b err_slab[b]
+// (block P): the adjoint stage's reductions in one launch, fixed order.
+__global__ void __launch_bounds__(kBlock)
+vjp_finish_kernel(const double* __restrict__ slab, int64_t nblk, int64_t P, double* __restrict__ dp, int assign,
+                  const double* __restrict__ err_slab, double* __restrict__ err_out) {
+    __shared__ double red[kBlock / kWave];
+    const int64_t q = blockIdx.x;
+    double s = 0.0;
+    if (q < P) {
+        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[b * P + q];
+    } else {
+        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += err_slab[b];
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        if (q < P) dp[q] = assign ? t : dp[q] + t;
+        else err_out[0] = t;
+    }
 }
 
 // Runge-Kutta stage, fused (kanode_rhs_stage): the stage input y = u + Σ_j c_j k_j is
@@ -727,11 +816,13 @@ hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PP
 
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
-                            hipStream_t st) {
+                            hipStream_t st, bool build) {
     if (Nx < 2 || (Nx & 1)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
-    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st);
-    if (e != hipSuccess) return e;
+    if (build) {
+        hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st);
+        if (e != hipSuccess) return e;
+    }
     const int units = Nx / 2;
     const int tl = ceil_log2(units < kBlock ? units : kBlock);
     const int tpb = kBlock >> tl;
@@ -776,11 +867,11 @@ bool fk_stage_pp_supported(const PPConst& hpc, int Nx) { return hpc.enabled && (
 hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                               const double* p, double* table, double cd, double co, int Nx, const double* u,
                               const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
-                              double* err_out, double* du, int64_t B, hipStream_t st) {
+                              double* err_out, double* du, int64_t B, hipStream_t st, bool build) {
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
-    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st)) != hipSuccess) return e;
     const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
     int grid = 0;
     double* slab = err_out ? err_slab : nullptr;
@@ -817,18 +908,20 @@ bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx) {
     return shape && cfg;
 }
 
-template <int NORM, int PATH, int GT>
+template <int NORM, int PATH, int GT, bool STG>
 static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const double* p, const double* tables,
                                double cd, double co, int Nx, const double* u, const double* lam, double* lamJ,
-                               double* slab, int slab_blocks, int64_t B, int& grid, hipStream_t st) {
+                               double* slab, int slab_blocks, int64_t B, int& grid, const StageArgs<double>& su,
+                               const StageArgs<double>& sl, double* lam_out, double* err_slab, hipStream_t st) {
     const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
 #define KAN_VJP_WAVE(NP)                                                                                          \
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
-        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP>, lds);                            \
+        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds);                       \
         grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
-        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p, \
-                           (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B);      \
+        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kBlock), lds, st,  \
+                           lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
+                           su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr);               \
     } while (0)
     if (Nx == 256) KAN_VJP_WAVE(2);
     else if (Nx == 128) KAN_VJP_WAVE(1);
@@ -837,44 +930,66 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
     return hipGetLastError();
 }
 
+template <bool STG>
+static hipError_t fk_vjp_pp_dispatch(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const double* p,
+                                     const double* tables, double cd, double co, int Nx, const double* u,
+                                     const double* lam, double* lamJ, double* slab, int slab_blocks, int64_t B,
+                                     int& grid, const StageArgs<double>& su, const StageArgs<double>& sl,
+                                     double* lam_out, double* err_slab, hipStream_t st) {
+#define KAN_VJP_GO(NORM, PATH, GT)                                                                               \
+    return fk_vjp_pp_go<NORM, PATH, GT, STG>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, slab_blocks, B, \
+                                             grid, su, sl, lam_out, err_slab, st)
+    if (hlc.path == PATH_REC_CORR) {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_VJP_GO(NORM_SOFTSIGN, PATH_REC_CORR, 10);
+        else if (hlc.G == 10) KAN_VJP_GO(NORM_TANH_FAST, PATH_REC_CORR, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_VJP_GO(NORM_SOFTSIGN, PATH_REC_CORR, 5);
+        else KAN_VJP_GO(NORM_TANH_FAST, PATH_REC_CORR, 5);
+    } else {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_VJP_GO(NORM_SOFTSIGN, PATH_REC, 10);
+        else if (hlc.G == 10) KAN_VJP_GO(NORM_TANH_FAST, PATH_REC, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_VJP_GO(NORM_SOFTSIGN, PATH_REC, 5);
+        else KAN_VJP_GO(NORM_TANH_FAST, PATH_REC, 5);
+    }
+#undef KAN_VJP_GO
+}
+
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
-                            hipStream_t st) {
+                            hipStream_t st, bool build) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
-    hipError_t e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st)) != hipSuccess) return e;
     int grid = 0;
-    if (hlc.path == PATH_REC_CORR) {
-        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN)
-            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC_CORR, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                                slab_blocks, B, grid, st);
-        else if (hlc.G == 10)
-            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC_CORR, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                                 slab_blocks, B, grid, st);
-        else if (hlc.norm == NORM_SOFTSIGN)
-            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC_CORR, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                               slab_blocks, B, grid, st);
-        else
-            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC_CORR, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                                slab_blocks, B, grid, st);
-    } else {
-        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN)
-            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                           slab_blocks, B, grid, st);
-        else if (hlc.G == 10)
-            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC, 10>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                            slab_blocks, B, grid, st);
-        else if (hlc.norm == NORM_SOFTSIGN)
-            e = fk_vjp_pp_go<NORM_SOFTSIGN, PATH_REC, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                          slab_blocks, B, grid, st);
-        else
-            e = fk_vjp_pp_go<NORM_TANH_FAST, PATH_REC, 5>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab,
-                                                           slab_blocks, B, grid, st);
-    }
+    const StageArgs<double> none{};
+    e = fk_vjp_pp_dispatch<false>(hpc, hlc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, slab_blocks, B, grid, none,
+                                  none, nullptr, nullptr, st);
     if (e != hipSuccess || !dp) return e;
     return launch_slab_reduce<double>(slab, grid, hlc.G + (hlc.use_base ? 1 : 0), dp, st);
+}
+
+hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                  const double* p, double* tables, double cd, double co, int Nx, const double* u,
+                                  const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
+                                  double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
+                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build) {
+    if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
+    const int fns[2] = {PP_DPHI, PP_SWISH};
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st)) != hipSuccess) return e;
+    int grid = 0;
+    // slab: [grid][P] dC/dW partials, then [grid] error partials (grid <= slab_blocks / 2)
+    const int cap = slab_blocks / 2;
+    e = fk_vjp_pp_dispatch<true>(hpc, hlc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, cap, B, grid, su, sl,
+                                 lam_out, err_out ? slab : nullptr, st);
+    if (e != hipSuccess) return e;
+    const int P = hlc.G + (hlc.use_base ? 1 : 0);
+    if (!dp && !err_out) return hipSuccess;
+    hipLaunchKernelGGL(vjp_finish_kernel, dim3((unsigned)(dp ? P : 0) + (err_out ? 1 : 0)), dim3(kBlock), 0, st,
+                       slab, (int64_t)grid, (int64_t)P, dp, dp_assign ? 1 : 0,
+                       slab + (int64_t)grid * (hlc.G + 1), err_out);
+    return hipGetLastError();
 }
 
 }  // namespace kan

@@ -19,6 +19,7 @@
 
 #include "kan_device.hpp"
 #include "kan_kernels.hpp"
+#include "kanode_internal.hpp"
 
 using kan::LayerConst;
 
@@ -54,6 +55,9 @@ struct kanode_handle {
     kan::PPConst* dpc = nullptr;
     double* dtable = nullptr;
     bool pp_on = false;
+    // table reuse inside one integrator solve (p constant): build each table set once
+    bool hold_tables = false;
+    bool built_phi = false, built_vjp = false;
     // stage input y for kanode_rhs_stage's unfused path
     void* stage_ws = nullptr;
     size_t stage_ws_bytes = 0;
@@ -68,6 +72,14 @@ namespace {
 kanode_status fail(kanode_handle* h, kanode_status s, const std::string& msg) {
     if (h) h->err = msg;
     return s;
+}
+
+// true when the launch must (re)build its table set; under hold_tables only the first does
+bool table_build(kanode_handle* h, bool& built) {
+    if (!h->hold_tables) return true;
+    if (built) return false;
+    built = true;
+    return true;
 }
 
 #define HIP_TRY(h, expr)                                                                         \
@@ -314,7 +326,7 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
         if constexpr (std::is_same<T, double>::value) {
             if (h->pp_on) {
                 HIP_TRY(h, kan::launch_fk_rhs_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co, (int)h->spec.nx, u, du,
-                                                 B, st));
+                                                 B, st, table_build(h, h->built_phi)));
                 return KANODE_OK;
             }
         }
@@ -359,7 +371,7 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
             if (h->pp_on && kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx)) {
                 HIP_TRY(h, kan::launch_fk_vjp_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                  (int)h->spec.nx, u, lam, out, dp, (double*)h->slab, kSlabBlocks, B,
-                                                 st));
+                                                 st, table_build(h, h->built_vjp)));
                 return KANODE_OK;
             }
         }
@@ -422,7 +434,7 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
             const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
             HIP_TRY(h, kan::launch_fk_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                (int)h->spec.nx, u, sa, (double*)sg->y_out, (double*)h->slab,
-                                               kSlabBlocks, err_out, du, B, st));
+                                               kSlabBlocks, err_out, du, B, st, table_build(h, h->built_phi)));
             return KANODE_OK;
         }
     }
@@ -473,7 +485,7 @@ kanode_status stage_args(kanode_handle* h, const kanode_stage* sg, kan::StageArg
 
 template <typename T>
 kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* state, const T* lam,
-                          const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st) {
+                          const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st, bool dp_assign = false) {
     if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "adjoint stage needs an RHS with N_in == N_out");
     if (adj->want_error && !adj->error_sumsq) return fail(h, KANODE_ERR_INVALID_ARG, "want_error needs error_sumsq");
     kan::StageArgs<T> su, sl;
@@ -482,6 +494,20 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
     s = stage_args<T>(h, adj, sl);
     if (s != KANODE_OK) return s;
     const int64_t n = h->n_in * B;
+    if constexpr (std::is_same<T, double>::value) {
+        // Fisher-KPP table path: the whole adjoint stage in one streaming kernel + one reduction
+        if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on && lamJ &&
+            kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx)) {
+            const double dx2 = h->spec.dx * h->spec.dx;
+            const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+            HIP_TRY(h, kan::launch_fk_vjp_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
+                                                   (int)h->spec.nx, u, su, lam, sl, (double*)adj->y_out, lamJ, dp,
+                                                   dp_assign, adj->want_error ? (double*)adj->error_sumsq : nullptr,
+                                                   (double*)h->slab, kSlabBlocks, B, st, table_build(h, h->built_vjp)));
+            return KANODE_OK;
+        }
+    }
+    if (dp && dp_assign) HIP_TRY(h, hipMemsetAsync(dp, 0, (size_t)h->P * sizeof(T), st));
     if ((s = ensure_stage_ws(h, 2 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
     T* y = su.nk ? (T*)h->stage_ws : (T*)u;
     T* ls = adj->y_out ? (T*)adj->y_out : (sl.nk ? (T*)h->stage_ws + n : (T*)lam);
@@ -829,3 +855,29 @@ kanode_status kanode_edge_activations(kanode_handle* h, int32_t layer, const voi
 }
 
 }  // extern "C"
+
+// ---- internal entry points for the integrator (kanode_solve.cpp) ----------------
+kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg) { return fail(h, s, msg); }
+int kanode_internal_dtype(const kanode_handle* h) { return h->spec.dtype; }
+int64_t kanode_internal_state_length(const kanode_handle* h) { return h->n_in; }
+bool kanode_internal_square(const kanode_handle* h) { return h->n_in == h->n_out; }
+void kanode_internal_hold_tables(kanode_handle* h, bool on) {
+    h->hold_tables = on;
+    h->built_phi = h->built_vjp = false;
+}
+double* kanode_internal_scratch(kanode_handle* h) { return (double*)h->slab; }
+int kanode_internal_scratch_rows(const kanode_handle*) { return kSlabBlocks; }
+kanode_status kanode_internal_check(kanode_handle* h) { return check_handle(h); }
+kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
+                                        const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
+                                        int64_t batch, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (!p || !u || !lam || !state || !adj || batch < 1) return fail(h, KANODE_ERR_INVALID_ARG, "null argument or batch < 1");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return vjp_stage_t<double>(h, (const double*)p, (const double*)u, state, (const double*)lam, adj, (double*)lamJ,
+                                   (double*)dp, batch, st, dp_assign);
+    return vjp_stage_t<float>(h, (const float*)p, (const float*)u, state, (const float*)lam, adj, (float*)lamJ,
+                              (float*)dp, batch, st, dp_assign);
+}

@@ -1,0 +1,24 @@
+// kanode_internal.hpp — handle accessors shared between the C-ABI translation units
+// (kanode_abi.cpp owns the handle; kanode_solve.cpp is the integrator around it).
+// C++ linkage, not part of the C-ABI.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+#include "kanode.h"
+
+kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
+kanode_status kanode_internal_check(kanode_handle* h);     // non-null, sets the handle's device
+int kanode_internal_dtype(const kanode_handle* h);
+int64_t kanode_internal_state_length(const kanode_handle* h);
+bool kanode_internal_square(const kanode_handle* h);       // N_in == N_out (an ODE right-hand side)
+// While held, each RHS / VJP table set is built by the first launch only (p must not change).
+void kanode_internal_hold_tables(kanode_handle* h, bool on);
+// handle scratch: kanode_internal_scratch_rows() doubles of per-block partials (stream-ordered use)
+double* kanode_internal_scratch(kanode_handle* h);
+int kanode_internal_scratch_rows(const kanode_handle* h);
+// kanode_vjp_stage with dp either accumulated (+=, the C-ABI semantics) or assigned (dp_assign)
+kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
+                                        const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
+                                        int64_t batch, void* stream);

@@ -1,0 +1,622 @@
+// kanode_solve.cpp — the Tsit5 integrator and the InterpolatingAdjoint around the HIP
+// RHS / VJP (include/kanode.h: kanode_solve_tsit5, kanode_adjoint_tsit5).
+//
+// A native host loop: every Runge-Kutta stage is one kanode_rhs_stage (the stage
+// combination u + dt·Σ a_sj k_j is formed inside the RHS kernel, the last stage also
+// writes u_new and the embedded-error sum of squares), every adjoint stage one
+// kanode_vjp_stage.  The only device->host traffic is the 8-byte error norm of an
+// adaptive step (the accept/reject decision); a fixed-step solve never synchronises.
+// The step sequence, controller and saveat handling restate OrdinaryDiffEqTsit5 1.1.0 /
+// OrdinaryDiffEq 6.89 and SciMLSensitivity 7.69 (third-party, pinned in
+// Lotka-Volterra/Manifest.toml; the Python driver kanode/ode.py + kanode/adjoint.py is
+// the same algorithm statement and the parity reference of the tests).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "kan_kernels.hpp"
+#include "kanode.h"
+#include "kanode_internal.hpp"
+
+namespace {
+
+// Tsitouras 5(4) (OrdinaryDiffEq tsit_tableaus.jl)
+constexpr double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
+constexpr double TA[6][6] = {
+    {0.161, 0, 0, 0, 0, 0},
+    {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
+    {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
+    {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
+    {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
+    {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
+};
+constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
+                          -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
+                          0.015151515151515152};
+// dense output b_i(θ) = Σ_m RI[i][m] θ^(m+1)  (Tsit5Interp)
+constexpr double RI[7][4] = {
+    {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
+    {0.0, 0.13169999999999998, -0.2234, 0.1017},
+    {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
+    {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
+    {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
+    {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
+    {0.0, 1.5, -4.0, 2.5},
+};
+
+void interp_weights(double theta, double w[7]) {
+    for (int i = 0; i < 7; ++i) {
+        double s = 0.0;
+        for (int m = 0; m < 4; ++m) s += RI[i][m] * std::pow(theta, (double)(m + 1));
+        w[i] = s;
+    }
+}
+
+kanode_solver_options resolved(const kanode_solver_options* o) {
+    kanode_solver_options d;
+    kanode_solver_options_default(&d);
+    return o ? *o : d;
+}
+
+}  // namespace
+
+extern "C" void kanode_solver_options_default(kanode_solver_options* o) {
+    if (!o) return;
+    o->abstol = 1e-6;
+    o->reltol = 1e-3;
+    o->dt = 0.0;
+    o->adaptive = 1;
+    o->maxiters = 100000;
+    o->dtmin = 0.0;
+    o->beta1 = 7.0 / 50.0;
+    o->beta2 = 2.0 / 25.0;
+    o->gamma = 0.9;
+    o->qmin = 0.2;
+    o->qmax = 10.0;
+    o->qoldinit = 1e-4;
+}
+
+// Dense output: step n keeps u_n and k_2..k_7 in slot n (7 states); k_1 of step n is
+// k_7 of step n-1 (FSAL), k_1 of step 0 has its own buffer.  Without recording only
+// two slots are used, alternately.
+struct kanode_solution {
+    kanode_handle* h = nullptr;
+    int dtype = 0;
+    size_t esize = 8;
+    int64_t n = 0;                   // elements of one state (N·B)
+    int64_t batch = 0;
+    double t0 = 0, tf = 0;
+    std::vector<double> saveat;
+    std::vector<double> ts, dts;     // accepted steps: start time, step
+    std::vector<void*> slots;
+    void* k1_0 = nullptr;
+    bool record = true;
+    double* dscal = nullptr;         // device scalars (norm totals)
+    double* hscal = nullptr;         // pinned host mirror
+    // adjoint scratch (sized on first use)
+    void* adj = nullptr;
+    size_t adj_bytes = 0;
+
+    ~kanode_solution() {
+        for (void* s : slots) (void)hipFree(s);
+        if (k1_0) (void)hipFree(k1_0);
+        if (dscal) (void)hipFree(dscal);
+        if (hscal) (void)hipHostFree(hscal);
+        if (adj) (void)hipFree(adj);
+    }
+    size_t state_bytes() const { return (size_t)n * esize; }
+    char* slot(int64_t i) const { return (char*)slots[record ? i : (i & 1)]; }
+    void* u(int64_t i) const { return slot(i); }
+    // stage vector k_j (j = 1..7) of step i
+    void* k(int64_t i, int j) const {
+        if (j == 1) return i == 0 ? k1_0 : k(i - 1, 7);
+        return slot(i) + (size_t)(j - 1) * state_bytes();
+    }
+};
+
+extern "C" void kanode_solution_free(kanode_solution* s) { delete s; }
+extern "C" int64_t kanode_solution_steps(const kanode_solution* s) { return s ? (int64_t)s->ts.size() : -1; }
+
+namespace {
+
+#define SOLVE_HIP(h, expr)                                                                                    \
+    do {                                                                                                      \
+        hipError_t e_ = (expr);                                                                               \
+        if (e_ != hipSuccess)                                                                                 \
+            return kanode_internal_fail((h), KANODE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define SOLVE_TRY(expr)                            \
+    do {                                           \
+        kanode_status s_ = (expr);                 \
+        if (s_ != KANODE_OK) return s_;            \
+    } while (0)
+
+bool capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+
+// slots [0, need) exist (allocating — not allowed during capture)
+kanode_status ensure_slots(kanode_handle* h, kanode_solution* s, int64_t need, hipStream_t st) {
+    if (!s->record) need = std::min<int64_t>(need, 2);
+    if ((int64_t)s->slots.size() >= need) return KANODE_OK;
+    if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "dense-output storage grows during capture");
+    while ((int64_t)s->slots.size() < need) {
+        void* p = nullptr;
+        if (hipMalloc(&p, 7 * s->state_bytes()) != hipSuccess) {
+            (void)hipGetLastError();
+            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "dense output: out of device memory at step " +
+                                                                 std::to_string(s->slots.size()));
+        }
+        s->slots.push_back(p);
+    }
+    return KANODE_OK;
+}
+
+// Σ over n entries of ((Σ_j ec_j k_j + ec_last·du) / (abstol + reltol·max(|u|,|y|)))² -> dst (device)
+template <typename T>
+kanode_status wsumsq(kanode_handle* h, const void* u, const void* y, int nk, const void* const* k, const double* ec,
+                     const void* du, double abstol, double reltol, int64_t n, double* dst, hipStream_t st) {
+    kan::StageArgs<T> sa{};
+    sa.nk = nk;
+    for (int j = 0; j < nk; ++j) sa.k[j] = (const T*)k[j];
+    for (int j = 0; j <= nk; ++j) sa.ec[j] = ec[j];
+    sa.abstol = abstol;
+    sa.reltol = reltol;
+    SOLVE_HIP(h, kan::launch_stage_error<T>((const T*)u, (const T*)y, (const T*)du, sa, kanode_internal_scratch(h),
+                                            kanode_internal_scratch_rows(h), dst, n, st));
+    return KANODE_OK;
+}
+
+// y = u + Σ_j c_j k_j over n entries (y may alias u)
+template <typename T>
+kanode_status lincomb(kanode_handle* h, const void* u, int nk, const void* const* k, const double* c, void* y,
+                      int64_t n, hipStream_t st) {
+    kan::StageArgs<T> sa{};
+    sa.nk = nk;
+    for (int j = 0; j < nk; ++j) {
+        sa.k[j] = (const T*)k[j];
+        sa.c[j] = c[j];
+    }
+    SOLVE_HIP(h, kan::launch_stage_lincomb<T>((const T*)u, sa, (T*)y, n, st));
+    return KANODE_OK;
+}
+
+kanode_status read_scalars(kanode_handle* h, kanode_solution* s, int cnt, hipStream_t st) {
+    if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
+    SOLVE_HIP(h, hipMemcpyAsync(s->hscal, s->dscal, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    return KANODE_OK;
+}
+
+kanode_stage make_stage(int nk, void* const* k, const double* c) {
+    kanode_stage sg{};
+    sg.n_prev = nk;
+    for (int j = 0; j < nk; ++j) {
+        sg.k[j] = k[j];
+        sg.c[j] = c[j];
+    }
+    return sg;
+}
+
+struct TableHold {   // p is constant for one solve: each table set is built once
+    kanode_handle* h;
+    explicit TableHold(kanode_handle* hh) : h(hh) { kanode_internal_hold_tables(h, true); }
+    ~TableHold() { kanode_internal_hold_tables(h, false); }
+};
+
+// Hairer & Wanner initial step (OrdinaryDiffEq ode_determine_initdt, order 5); kanode/ode.py _initdt
+template <typename T>
+kanode_status initdt(kanode_handle* h, kanode_solution* s, const void* p, const void* u0, const void* f0,
+                     double tdist, const kanode_solver_options& o, double& dt, hipStream_t st) {
+    const double one = 1.0;
+    double e1[2] = {1.0, 0.0};
+    void* tmp = s->k(0, 2);   // scratch: the k_2 buffer of step 0
+    SOLVE_TRY(wsumsq<T>(h, u0, u0, 0, nullptr, &one, u0, o.abstol, o.reltol, s->n, s->dscal + 0, st));
+    SOLVE_TRY(wsumsq<T>(h, u0, u0, 0, nullptr, &one, f0, o.abstol, o.reltol, s->n, s->dscal + 1, st));
+    SOLVE_TRY(read_scalars(h, s, 2, st));
+    const double d0 = std::sqrt(s->hscal[0] / (double)s->n), d1 = std::sqrt(s->hscal[1] / (double)s->n);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+    dt0 = std::min(dt0, tdist);
+    void* kk[1] = {(void*)f0};
+    kanode_stage sg = make_stage(1, kk, &dt0);
+    SOLVE_TRY(kanode_rhs_stage(h, p, u0, &sg, tmp, s->batch, st));
+    const void* kd[1] = {tmp};
+    e1[1] = -1.0;
+    SOLVE_TRY(wsumsq<T>(h, u0, u0, 1, kd, e1, f0, o.abstol, o.reltol, s->n, s->dscal + 2, st));
+    SOLVE_TRY(read_scalars(h, s, 3, st));
+    const double d2 = std::sqrt(s->hscal[2] / (double)s->n) / dt0;
+    const double mx = std::max(d1, d2);
+    const double dt1 = mx <= 1e-15 ? std::max(1e-6, dt0 * 1e-3) : std::pow(0.01 / mx, 1.0 / 5.0);
+    dt = std::min(std::min(100 * dt0, dt1), tdist);
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0, double tf, const double* saveat,
+                      int64_t n_save, void* u_save, const kanode_solver_options& o, kanode_solution* s,
+                      kanode_solve_stats* stats, hipStream_t st) {
+    const size_t sb = s->state_bytes();
+    int64_t si = 0;
+    while (si < n_save && saveat[si] <= t0 + 1e-14 * std::max(1.0, std::fabs(t0))) {
+        SOLVE_HIP(h, hipMemcpyAsync((char*)u_save + si * sb, u0, sb, hipMemcpyDeviceToDevice, st));
+        ++si;
+    }
+    // fixed step: the whole step sequence is known, allocate it up front
+    if (!o.adaptive) {
+        int64_t nst = 0;
+        for (double t = t0, dt = o.dt; nst < o.maxiters && !(t >= tf - 1e-14 * std::max(1.0, std::fabs(tf)));) {
+            dt = std::min(dt, tf - t);
+            t = t + dt;
+            ++nst;
+        }
+        SOLVE_TRY(ensure_slots(h, s, nst + 1, st));
+    } else {
+        SOLVE_TRY(ensure_slots(h, s, 2, st));
+    }
+    SOLVE_HIP(h, hipMemcpyAsync(s->u(0), u0, sb, hipMemcpyDeviceToDevice, st));
+    kanode_stage s0{};
+    SOLVE_TRY(kanode_rhs_stage(h, p, s->u(0), &s0, s->k1_0, s->batch, st));   // k1 = f(u0)
+    double dt = o.dt;
+    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st));
+    double qold = o.qoldinit;
+    double t = t0;
+    int64_t step = 0, naccept = 0, nreject = 0, nf = 0;
+    int64_t it = 0;
+    for (; it < o.maxiters; ++it) {
+        if (t >= tf - 1e-14 * std::max(1.0, std::fabs(tf))) break;
+        dt = std::min(dt, tf - t);
+        SOLVE_TRY(ensure_slots(h, s, step + 2, st));
+        void* ks[7];
+        for (int j = 0; j < 7; ++j) ks[j] = s->k(step, j + 1);
+        for (int i = 0; i < 6; ++i) {
+            double c[6];
+            for (int j = 0; j <= i; ++j) c[j] = dt * TA[i][j];
+            kanode_stage sg = make_stage(i + 1, ks, c);
+            if (i == 5) {
+                sg.y_out = s->u(step + 1);
+                if (o.adaptive) {
+                    sg.want_error = 1;
+                    for (int j = 0; j < 7; ++j) sg.ec[j] = dt * BT[j];
+                    sg.abstol = o.abstol;
+                    sg.reltol = o.reltol;
+                    sg.error_sumsq = s->dscal;
+                }
+            }
+            SOLVE_TRY(kanode_rhs_stage(h, p, s->u(step), &sg, ks[i + 1], s->batch, st));
+        }
+        nf += 6;
+        double dtnew = dt;
+        if (o.adaptive) {
+            SOLVE_TRY(read_scalars(h, s, 1, st));
+            const double EEst = std::sqrt(s->hscal[0] / (double)s->n);
+            const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
+            if (EEst > 1.0 && dt > o.dtmin) {
+                ++nreject;
+                dt = dt / std::min(1.0 / o.qmin, q11 / o.gamma);
+                continue;
+            }
+            double q = q11 / std::pow(qold, o.beta2);
+            q = std::max(1.0 / o.qmax, std::min(1.0 / o.qmin, q / o.gamma));
+            if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
+            dtnew = q > 0 ? dt / q : dt * o.qmax;
+            qold = std::max(EEst, o.qoldinit);
+        }
+        const double tn = t + dt;
+        while (si < n_save && saveat[si] <= tn + 1e-12 * std::max(1.0, std::fabs(tn))) {
+            const double tsv = saveat[si];
+            void* dst = (char*)u_save + si * sb;
+            if (std::fabs(tsv - tn) <= 1e-12 * std::max(1.0, std::fabs(tn))) {
+                SOLVE_HIP(h, hipMemcpyAsync(dst, s->u(step + 1), sb, hipMemcpyDeviceToDevice, st));
+            } else {
+                double w[7];
+                interp_weights((tsv - t) / dt, w);
+                for (int j = 0; j < 7; ++j) w[j] *= dt;
+                SOLVE_TRY(lincomb<T>(h, s->u(step), 7, ks, w, dst, s->n, st));
+            }
+            ++si;
+        }
+        s->ts.push_back(t);
+        s->dts.push_back(dt);
+        t = tn;
+        ++step;
+        ++naccept;
+        dt = dtnew;
+    }
+    if (it == o.maxiters && !(t >= tf - 1e-14 * std::max(1.0, std::fabs(tf))))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
+    if (stats) {
+        stats->naccept = naccept;
+        stats->nreject = nreject;
+        stats->nf = nf + 1;
+    }
+    return KANODE_OK;
+}
+
+// ---- InterpolatingAdjoint -----------------------------------------------------------
+template <typename T>
+kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0, void* dp,
+                        const kanode_solver_options& o, kanode_solve_stats* stats, hipStream_t st) {
+    const int64_t n = s->n, P = kanode_param_length(h);
+    const size_t sb = s->state_bytes(), pb = (size_t)P * s->esize;
+    const int64_t nsteps = (int64_t)s->ts.size();
+    if (nsteps < 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint: the forward solve took no steps");
+    // scratch: lam[2], kl[7] (states), mu[2], km[7] (parameter vectors)
+    const size_t need = 9 * sb + 9 * pb + 256;
+    if (s->adj_bytes < need) {
+        if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adjoint scratch grows during capture");
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        if (s->adj) SOLVE_HIP(h, hipFree(s->adj));
+        s->adj = nullptr;
+        s->adj_bytes = 0;
+        if (hipMalloc(&s->adj, need) != hipSuccess) {
+            (void)hipGetLastError();
+            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "adjoint scratch: out of device memory");
+        }
+        s->adj_bytes = need;
+    }
+    auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char* w = (char*)s->adj;
+    void *lam[2], *kl[7], *mu[2], *km[7];
+    for (auto& x : lam) { x = w; w += sb; }
+    for (auto& x : kl) { x = w; w += sb; }
+    w = (char*)s->adj + align(9 * sb);
+    for (auto& x : mu) { x = w; w += pb; }
+    for (auto& x : km) { x = w; w += pb; }
+
+    const double t0 = s->t0, tf = s->tf, TT = tf - t0;
+    const double eps = 1e-12 * std::max(1.0, std::fabs(tf));
+    // jumps: distinct saveat values, each with the rows of dl_du that land on it
+    struct Jump { double ts; std::vector<int64_t> rows; bool live; };
+    std::vector<Jump> jumps;
+    for (int64_t j = 0; j < (int64_t)s->saveat.size(); ++j) {
+        auto f = std::find_if(jumps.begin(), jumps.end(), [&](const Jump& x) { return x.ts == s->saveat[j]; });
+        if (f == jumps.end()) jumps.push_back({s->saveat[j], {j}, true});
+        else f->rows.push_back(j);
+    }
+    auto add_jump = [&](Jump& jm, void* l) -> kanode_status {
+        for (int64_t r : jm.rows) {
+            const void* g[1] = {(const char*)dl_du + r * sb};
+            const double one = 1.0;
+            SOLVE_TRY(lincomb<T>(h, l, 1, g, &one, l, n, st));
+        }
+        jm.live = false;
+        return KANODE_OK;
+    };
+    SOLVE_HIP(h, hipMemsetAsync(lam[0], 0, sb, st));
+    SOLVE_HIP(h, hipMemsetAsync(mu[0], 0, pb, st));
+    if (dl_du) {
+        for (auto& jm : jumps)
+            if (jm.live && jm.ts == tf) SOLVE_TRY(add_jump(jm, lam[0]));
+    } else {
+        for (auto& jm : jumps) jm.live = false;
+    }
+    std::vector<double> stops;
+    for (auto& jm : jumps)
+        if (jm.live && t0 + eps < jm.ts && jm.ts < tf - eps) stops.push_back(tf - jm.ts);
+    std::sort(stops.begin(), stops.end());
+    stops.push_back(TT);
+
+    // adjoint RHS at τ: u(tf - τ) from the dense output, λ stage input l + Σ lc_j lks_j
+    // (-> lam_out), lamJ = λsᵀ∂f/∂u, dpo = λsᵀ∂f/∂p; ec != NULL adds the λ error total -> err
+    auto adj_rhs = [&](double tau, const void* l, int nl, void* const* lks, const double* lc, void* lamJ, void* dpo,
+                       void* lam_out, const double* ec, double* err) -> kanode_status {
+        const double t = tf - tau;
+        int64_t i = (int64_t)(std::upper_bound(s->ts.begin(), s->ts.end(), t) - s->ts.begin()) - 1;
+        i = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, i));
+        const double dti = s->dts[i];
+        const double theta = std::min(1.0, std::max(0.0, (t - s->ts[i]) / dti));
+        double c[7];
+        interp_weights(theta, c);
+        for (double& x : c) x *= dti;
+        void* ks[7];
+        for (int j = 0; j < 7; ++j) ks[j] = s->k(i, j + 1);
+        kanode_stage su = make_stage(7, ks, c);
+        kanode_stage sl = make_stage(nl, lks, lc);
+        sl.y_out = lam_out;
+        if (ec) {
+            sl.want_error = 1;
+            for (int j = 0; j <= nl; ++j) sl.ec[j] = ec[j];
+            sl.abstol = o.abstol;
+            sl.reltol = o.reltol;
+            sl.error_sumsq = err;
+        }
+        return kanode_internal_vjp_stage(h, p, s->u(i), &su, l, &sl, lamJ, dpo, true, s->batch, st);
+    };
+    const int64_t ntot = n + P;
+    int cur = 0;   // lam[cur], mu[cur] hold λ, μ
+    SOLVE_TRY(adj_rhs(0.0, lam[cur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
+    int64_t nf = 1;
+    double hstep = o.dt;
+    if (o.adaptive && !(o.dt > 0)) {
+        // Hairer-Wanner on the augmented state [λ; μ] (kanode/adjoint.py)
+        const double one = 1.0;
+        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 0, nullptr, &one, lam[cur], o.abstol, o.reltol, n, s->dscal + 0, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 0, nullptr, &one, mu[cur], o.abstol, o.reltol, P, s->dscal + 1, st));
+        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 0, nullptr, &one, kl[0], o.abstol, o.reltol, n, s->dscal + 2, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 0, nullptr, &one, km[0], o.abstol, o.reltol, P, s->dscal + 3, st));
+        SOLVE_TRY(read_scalars(h, s, 4, st));
+        const double d0 = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot);
+        const double d1 = std::sqrt((s->hscal[2] + s->hscal[3]) / (double)ntot);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = std::min(h0, TT);
+        void* k1l[1] = {kl[0]};
+        SOLVE_TRY(adj_rhs(h0, lam[cur], 1, k1l, &h0, kl[1], km[1], nullptr, nullptr, nullptr));
+        ++nf;
+        const double e2[2] = {1.0, -1.0};
+        const void* a1[1] = {kl[1]};
+        const void* b1[1] = {km[1]};
+        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 1, a1, e2, kl[0], o.abstol, o.reltol, n, s->dscal + 0, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 1, b1, e2, km[0], o.abstol, o.reltol, P, s->dscal + 1, st));
+        SOLVE_TRY(read_scalars(h, s, 2, st));
+        const double d2 = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot) / h0;
+        const double mx = std::max(d1, d2);
+        const double h1 = mx <= 1e-15 ? std::max(1e-6, h0 * 1e-3) : std::pow(0.01 / mx, 1.0 / 5.0);
+        hstep = std::min(std::min(100 * h0, h1), TT);
+    } else if (!(hstep > 0)) {
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step adjoint needs opt->dt > 0");
+    }
+    double qold = o.qoldinit, tau = 0.0;
+    size_t si = 0;
+    int64_t naccept = 0, nreject = 0, it = 0;
+    for (; it < o.maxiters; ++it) {
+        if (tau >= TT - 1e-14 * std::max(1.0, TT)) break;
+        hstep = std::min(hstep, stops[si] - tau);
+        const int nxt = cur ^ 1;
+        for (int i = 0; i < 6; ++i) {
+            double lc[6];
+            for (int j = 0; j <= i; ++j) lc[j] = hstep * TA[i][j];
+            if (i == 5) {
+                double ec[7];
+                for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
+                SOLVE_TRY(adj_rhs(tau + hstep, lam[cur], 6, kl, lc, kl[6], km[6], lam[nxt], o.adaptive ? ec : nullptr,
+                                  s->dscal + 0));
+            } else {
+                SOLVE_TRY(adj_rhs(tau + TC[i] * hstep, lam[cur], i + 1, kl, lc, kl[i + 1], km[i + 1], nullptr,
+                                  nullptr, nullptr));
+            }
+        }
+        nf += 6;
+        double a6[6];
+        for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
+        SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
+        double hnew = hstep;
+        if (o.adaptive) {
+            double ec[7];
+            for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
+            SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[nxt], 6, km, ec, km[6], o.abstol, o.reltol, P, s->dscal + 1, st));
+            SOLVE_TRY(read_scalars(h, s, 2, st));
+            const double EEst = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot);
+            const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
+            if (EEst > 1.0 && hstep > o.dtmin) {
+                ++nreject;
+                hstep = hstep / std::min(1.0 / o.qmin, q11 / o.gamma);
+                continue;
+            }
+            double q = q11 / std::pow(qold, o.beta2);
+            q = std::max(1.0 / o.qmax, std::min(1.0 / o.qmin, q / o.gamma));
+            hnew = q > 0 ? hstep / q : hstep * o.qmax;
+            qold = std::max(EEst, o.qoldinit);
+        }
+        tau = tau + hstep;
+        cur = nxt;
+        std::swap(kl[0], kl[6]);   // FSAL
+        std::swap(km[0], km[6]);
+        ++naccept;
+        if (std::fabs(tau - stops[si]) <= 1e-12 * std::max(1.0, TT)) {
+            tau = stops[si];
+            const double tsv = tf - tau;
+            Jump* key = nullptr;
+            for (auto& jm : jumps)
+                if (jm.live && (!key || std::fabs(jm.ts - tsv) < std::fabs(key->ts - tsv))) key = &jm;
+            if (key && std::fabs(key->ts - tsv) <= eps && si + 1 < stops.size()) {
+                SOLVE_TRY(add_jump(*key, lam[cur]));                       // callback: λ += ∂L/∂u(t_j)
+                SOLVE_TRY(adj_rhs(tau, lam[cur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
+                ++nf;                                                      // u_modified!: FSAL re-evaluated
+            }
+            si = std::min(si + 1, stops.size() - 1);
+        }
+        hstep = hnew;
+    }
+    if (it == o.maxiters && !(tau >= TT - 1e-14 * std::max(1.0, TT)))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
+    for (auto& jm : jumps)   // a saveat at t0 adds to dL/du0 only
+        if (jm.live && std::fabs(jm.ts - t0) <= eps) SOLVE_TRY(add_jump(jm, lam[cur]));
+    if (du0) SOLVE_HIP(h, hipMemcpyAsync(du0, lam[cur], sb, hipMemcpyDeviceToDevice, st));
+    if (dp) SOLVE_HIP(h, hipMemcpyAsync(dp, mu[cur], pb, hipMemcpyDeviceToDevice, st));
+    if (stats) {
+        stats->naccept = naccept;
+        stats->nreject = nreject;
+        stats->nf = nf;
+    }
+    return KANODE_OK;
+}
+
+kanode_status check_opts(kanode_handle* h, const kanode_solver_options& o) {
+    if (!(o.abstol >= 0) || !(o.reltol >= 0) || o.maxiters < 1 || !(o.qmin > 0) || !(o.qmax > 0) || !(o.gamma > 0))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solver options out of range");
+    if (!o.adaptive && !(o.dt > 0)) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step Tsit5 needs dt > 0");
+    return KANODE_OK;
+}
+
+}  // namespace
+
+extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch, double t0,
+                                            double tf, const double* saveat, int64_t n_save, void* u_save,
+                                            const kanode_solver_options* opt, kanode_solution** dense,
+                                            kanode_solve_stats* stats, void* stream) {
+    SOLVE_TRY(kanode_internal_check(h));
+    const kanode_solver_options o = resolved(opt);
+    SOLVE_TRY(check_opts(h, o));
+    if (!p || !u0 || batch < 1 || !(tf > t0) || n_save < 0 || (n_save > 0 && (!saveat || !u_save)))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve: null pointer, batch < 1 or tf <= t0");
+    if (!kanode_internal_square(h))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve needs an RHS with N_in == N_out");
+    for (int64_t j = 1; j < n_save; ++j)
+        if (!(saveat[j] >= saveat[j - 1])) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must ascend");
+    hipStream_t st = (hipStream_t)stream;
+    const int dtype = kanode_internal_dtype(h);
+    const int64_t n = kanode_internal_state_length(h) * batch;
+    kanode_solution* s = dense ? *dense : nullptr;
+    if (s && (s->h != h || s->n != n || s->dtype != dtype || s->record != (dense != nullptr))) {
+        // storage of another shape: start over
+        if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "dense output of another shape");
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        delete s;
+        s = nullptr;
+    }
+    if (!s) {
+        if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "solve allocates its dense output");
+        s = new (std::nothrow) kanode_solution();
+        if (!s) return kanode_internal_fail(h, KANODE_ERR_ALLOC, "solution");
+        s->h = h;
+        s->dtype = dtype;
+        s->esize = dtype == KANODE_F64 ? 8 : 4;
+        s->n = n;
+        s->record = dense != nullptr;
+        if (hipMalloc(&s->k1_0, s->state_bytes()) != hipSuccess || hipMalloc(&s->dscal, 8 * sizeof(double)) != hipSuccess ||
+            hipHostMalloc((void**)&s->hscal, 8 * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            delete s;
+            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "solve: out of device memory");
+        }
+    }
+    s->batch = batch;
+    s->t0 = t0;
+    s->tf = tf;
+    s->saveat.assign(saveat, saveat + n_save);
+    s->ts.clear();
+    s->dts.clear();
+    kanode_status r;
+    {
+        TableHold hold(h);
+        r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
+                                : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
+    }
+    if (dense) {
+        *dense = s;
+    } else {
+        if (hipStreamSynchronize(st) != hipSuccess) (void)hipGetLastError();   // scratch freed below
+        delete s;
+    }
+    return r;
+}
+
+extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,
+                                              const void* dl_du, void* du0, void* dp, const kanode_solver_options* opt,
+                                              kanode_solve_stats* stats, void* stream) {
+    SOLVE_TRY(kanode_internal_check(h));
+    const kanode_solver_options o = resolved(opt);
+    SOLVE_TRY(check_opts(h, o));
+    if (!p || !dense) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint: null p or dense output");
+    kanode_solution* s = const_cast<kanode_solution*>(dense);   // scratch only; the dense output is not modified
+    if (s->h != h || !s->record)
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint: dense output of another handle or not recorded");
+    hipStream_t st = (hipStream_t)stream;
+    TableHold hold(h);
+    return s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
+                                  : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);
+}

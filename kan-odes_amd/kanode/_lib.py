@@ -63,6 +63,19 @@ class StageC(C.Structure):
     ]
 
 
+class SolverOptsC(C.Structure):
+    """kanode_solver_options (include/kanode.h)."""
+    _fields_ = [
+        ("abstol", C.c_double), ("reltol", C.c_double), ("dt", C.c_double), ("adaptive", C.c_int32),
+        ("maxiters", C.c_int64), ("dtmin", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
+        ("gamma", C.c_double), ("qmin", C.c_double), ("qmax", C.c_double), ("qoldinit", C.c_double),
+    ]
+
+
+class SolveStatsC(C.Structure):
+    _fields_ = [("naccept", C.c_int64), ("nreject", C.c_int64), ("nf", C.c_int64)]
+
+
 # (name, restype, argtypes) for every symbol include/kanode.h declares
 _P = C.c_void_p
 _H = C.c_void_p
@@ -85,6 +98,12 @@ SIGNATURES = [
     ("kanode_rhs_stage", C.c_int, [_H, _P, _P, C.POINTER(StageC), _P, C.c_int64, _P]),
     ("kanode_vjp_stage", C.c_int, [_H, _P, _P, C.POINTER(StageC), _P, C.POINTER(StageC), _P, _P, C.c_int64, _P]),
     ("kanode_vjp", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_solver_options_default", None, [C.POINTER(SolverOptsC)]),
+    ("kanode_solution_free", None, [_P]),
+    ("kanode_solution_steps", C.c_int64, [_P]),
+    ("kanode_solve_tsit5", C.c_int, [_H, _P, _P, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_double), C.c_int64,
+                                     _P, C.POINTER(SolverOptsC), C.POINTER(C.c_void_p), C.POINTER(SolveStatsC), _P]),
+    ("kanode_adjoint_tsit5", C.c_int, [_H, _P, _P, _P, _P, _P, C.POINTER(SolverOptsC), C.POINTER(SolveStatsC), _P]),
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
     ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),
     ("kanode_layer_forward", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),

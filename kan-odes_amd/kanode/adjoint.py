@@ -127,8 +127,8 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
         nf += 6
         mu_new = mu + sum((h * a) * k for a, k in zip(A[5], km))
         if opt.adaptive:
-            emu = sum((h * b) * k for b, k in zip(BTILDE, km))
-            skm = opt.abstol + torch.maximum(mu.abs(), mu_new.abs()) * opt.reltol
+            emu = sum((h * b) * k.double() for b, k in zip(BTILDE, km))        # norms in double
+            skm = opt.abstol + torch.maximum(mu.abs(), mu_new.abs()).double() * opt.reltol
             EEst = math.sqrt((sumsq.item() + _rms2(emu / skm)) / (n_lam + n_mu))
             q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
             if EEst > 1.0 and h > opt.dtmin:
@@ -193,3 +193,32 @@ def solve_interpolating_adjoint(f, u0, tspan, p, saveat, opt: Tsit5Options) -> S
     t0, tf = float(tspan[0]), float(tspan[1])
     ts = list(saveat) if saveat is not None else [t0, tf]
     return Solution(ts[:u.shape[0]], u, stats)
+
+
+class _NativeAdjointSolve(torch.autograd.Function):
+    """kanode_solve_tsit5 keeping its dense output; backward = kanode_adjoint_tsit5 (both native)."""
+
+    @staticmethod
+    def forward(ctx, hd, tspan, saveat, opt, stats, p, u0):
+        oc = opt.to_c()
+        u_save, st, dense = hd.solve_tsit5(p.detach().contiguous(), u0.detach().contiguous(), float(tspan[0]),
+                                           float(tspan[1]), saveat, oc, keep_dense=True)
+        ctx.hd, ctx.dense, ctx.oc, ctx.stats, ctx.u_shape = hd, dense, oc, stats, tuple(u0.shape)
+        ctx.save_for_backward(p)
+        stats.update(st)
+        return u_save
+
+    @staticmethod
+    def backward(ctx, g):
+        (p,) = ctx.saved_tensors
+        du0, dp, st = ctx.hd.adjoint_tsit5(p.detach().contiguous(), ctx.dense, g.contiguous(), ctx.oc, ctx.u_shape)
+        ctx.stats["adjoint"] = st
+        ctx.hd.release_dense(ctx.dense)
+        ctx.dense = None
+        return None, None, None, None, None, dp, du0
+
+
+def solve_native_interpolating_adjoint(f, u0, tspan, p, saveat, opt: Tsit5Options) -> Solution:
+    stats = {}
+    u = _NativeAdjointSolve.apply(f.hd, tspan, list(saveat), opt, stats, p, u0)
+    return Solution(list(saveat), u, stats)

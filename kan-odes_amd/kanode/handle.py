@@ -57,6 +57,26 @@ def _stream(device: torch.device):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+class DenseOutput:
+    """Owner of a kanode_solution* (the device-resident dense output of one solve)."""
+
+    def __init__(self, hd):
+        self.hd = hd
+        self.ptr = C.c_void_p()
+
+    @property
+    def steps(self) -> int:
+        return int(L.lib().kanode_solution_steps(self.ptr)) if self.ptr.value else 0
+
+    def __del__(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            try:
+                L.lib().kanode_solution_free(self.ptr)
+            except Exception:
+                pass
+            self.ptr = C.c_void_p()
+
+
 class KanodeHandle:
     """A configured RHS (chain or pointwise+periodic-Laplacian) bound to one device."""
 
@@ -246,6 +266,49 @@ class KanodeHandle:
         L.check(L.lib().kanode_vjp(self._h, _ptr(p), _ptr(u), _ptr(lam), _ptr(lamJ), _ptr(dp), B,
                                    _stream(self.device)), self._h, "kanode_vjp")
         return lamJ, dp
+
+    # -- integrator (kanode_solve_tsit5 / kanode_adjoint_tsit5) --------------------
+    def solve_tsit5(self, p: torch.Tensor, u0: torch.Tensor, t0: float, tf: float, saveat, opts: "L.SolverOptsC",
+                    keep_dense: bool = False):
+        """Native Tsit5 solve on the device: (u_save (len(saveat), *u0.shape), stats dict,
+        DenseOutput or None).  saveat: ascending floats within [t0, tf]."""
+        B = u0.shape[0] if u0.dim() == 2 else 1
+        self._check_t(p, (self.P,), "p")
+        self._check_t(u0, None, "u0")
+        if u0.numel() != B * self.N or self.N_out != self.N:
+            raise ValueError("solve needs u0 of B x N entries and an RHS with N_in == N_out")
+        sv = (C.c_double * max(1, len(saveat)))(*[float(x) for x in saveat])
+        u_save = torch.empty((len(saveat),) + tuple(u0.shape), dtype=self.dtype, device=self.device)
+        st = L.SolveStatsC()
+        dense = None
+        dptr = None
+        if keep_dense:
+            dense = self._dense_pool.pop() if getattr(self, "_dense_pool", None) else DenseOutput(self)
+            dptr = C.byref(dense.ptr)
+        L.check(L.lib().kanode_solve_tsit5(self._h, _ptr(p), _ptr(u0), B, float(t0), float(tf), sv, len(saveat),
+                                           _ptr(u_save), C.byref(opts), dptr, C.byref(st), _stream(self.device)),
+                self._h, "kanode_solve_tsit5")
+        return u_save, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf), dense
+
+    def adjoint_tsit5(self, p: torch.Tensor, dense: "DenseOutput", dl_du: torch.Tensor, opts: "L.SolverOptsC",
+                      u_shape):
+        """InterpolatingAdjoint over a kept forward solve: (dL/du0, dL/dp, stats)."""
+        self._check_t(p, (self.P,), "p")
+        self._check_t(dl_du, None, "dl_du")
+        du0 = torch.empty(tuple(u_shape), dtype=self.dtype, device=self.device)
+        dp = torch.empty_like(p)
+        st = L.SolveStatsC()
+        L.check(L.lib().kanode_adjoint_tsit5(self._h, _ptr(p), dense.ptr, _ptr(dl_du), _ptr(du0), _ptr(dp),
+                                             C.byref(opts), C.byref(st), _stream(self.device)),
+                self._h, "kanode_adjoint_tsit5")
+        return du0, dp, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf)
+
+    def release_dense(self, dense: "DenseOutput") -> None:
+        """Return a dense output's device storage for reuse by the next solve."""
+        if not hasattr(self, "_dense_pool"):
+            self._dense_pool = []
+        if dense is not None and dense.ptr.value and len(self._dense_pool) < 2:
+            self._dense_pool.append(dense)
 
     # -- single layer ----------------------------------------------------------
     def layer_forward(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor) -> torch.Tensor:

@@ -24,6 +24,7 @@ squares, so no stage broadcast or error pass runs as separate torch kernels.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass, field
 
@@ -76,6 +77,19 @@ class Tsit5Options:
     qmax: float = 10.0
     qoldinit: float = 1e-4
     fused: bool = True                 # use f.stage (kanode_rhs_stage) when the RHS has one
+    native: bool = True                # run the loop in libkanode (kanode_solve_tsit5) when f is a kanode RHS
+
+    def to_c(self):
+        from . import _lib as L
+        o = L.SolverOptsC()
+        L.lib().kanode_solver_options_default(ctypes.byref(o))
+        o.abstol, o.reltol = float(self.abstol), float(self.reltol)
+        o.dt = float(self.dt) if self.dt is not None else 0.0
+        o.adaptive = 1 if self.adaptive else 0
+        o.maxiters, o.dtmin = int(self.maxiters), float(self.dtmin)
+        o.beta1, o.beta2, o.gamma = float(self.beta1), float(self.beta2), float(self.gamma)
+        o.qmin, o.qmax, o.qoldinit = float(self.qmin), float(self.qmax), float(self.qoldinit)
+        return o
 
 
 @dataclass
@@ -153,9 +167,22 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
     saveat = [float(s) for s in saveat]
     if sensealg not in ("discrete", "interpolating_adjoint"):
         raise ValueError(f"unknown sensealg {sensealg!r}")
-    if sensealg == "interpolating_adjoint" and torch.is_grad_enabled() and (p.requires_grad or u0.requires_grad):
+    grad = torch.is_grad_enabled() and (getattr(p, "requires_grad", False) or u0.requires_grad)
+    native = (opt.native and hasattr(f, "hd") and isinstance(p, torch.Tensor) and u0.is_cuda and u0.dim() in (1, 2) and dense_record is None
+              and tf > t0 and all(a <= b for a, b in zip(saveat, saveat[1:])))
+    if native:
+        tol = 1e-12 * max(1.0, abs(tf))
+        saveat = [s for s in saveat if s <= tf + tol]
+    if sensealg == "interpolating_adjoint" and grad:
+        if native:
+            from .adjoint import solve_native_interpolating_adjoint
+            return solve_native_interpolating_adjoint(f, u0, tspan, p, saveat, opt)
         from .adjoint import solve_interpolating_adjoint
         return solve_interpolating_adjoint(f, u0, tspan, p, saveat, opt)
+    if native and not grad:
+        u_save, stats, _ = f.hd.solve_tsit5(p.detach().contiguous(), u0.detach().contiguous(), t0, tf, saveat,
+                                            opt.to_c())
+        return Solution(list(saveat), u_save, stats)
     out = []
     si = 0
     while si < len(saveat) and saveat[si] <= t0 + 1e-14 * max(1.0, abs(t0)):

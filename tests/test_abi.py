@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "kanode.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(kanode_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(kanode_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_the_boundary():
@@ -46,19 +46,30 @@ def test_library_loads_and_reports_version():
     assert lib.kanode_status_string(L.ERR_UNSUPPORTED) == b"unsupported configuration"
 
 
-def test_stage_struct_layout_matches_c_compiler(tmp_path):
-    """kanode_stage offsets as gcc lays them out from include/kanode.h vs the ctypes mirror."""
-    import subprocess
-    fields = [f[0] for f in L.StageC._fields_]
+@pytest.mark.parametrize("cname,cls", [("kanode_stage", L.StageC), ("kanode_solver_options", L.SolverOptsC),
+                                        ("kanode_solve_stats", L.SolveStatsC)])
+def test_struct_layout_matches_c_compiler(tmp_path, cname, cls):
+    """Struct offsets as gcc lays them out from include/kanode.h vs the ctypes mirror."""
+    fields = [f[0] for f in cls._fields_]
     src = tmp_path / "probe.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kanode.h"\nint main(void) {\n'
-                   + "".join(f'  printf("%zu\\n", offsetof(kanode_stage, {f}));\n' for f in fields)
-                   + '  printf("%zu\\n", sizeof(kanode_stage));\n  return 0;\n}\n')
+                   + "".join(f'  printf("%zu\\n", offsetof({cname}, {f}));\n' for f in fields)
+                   + f'  printf("%zu\\n", sizeof({cname}));\n  return 0;\n}}\n')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
-    assert got[:-1] == [getattr(L.StageC, f).offset for f in fields]
-    assert got[-1] == C.sizeof(L.StageC)
+    assert got[:-1] == [getattr(cls, f).offset for f in fields]
+    assert got[-1] == C.sizeof(cls)
+
+
+def test_solver_option_defaults():
+    """kanode_solver_options_default == kanode.Tsit5Options() (OrdinaryDiffEq defaults)."""
+    o = L.SolverOptsC()
+    kanode.lib().kanode_solver_options_default(C.byref(o))
+    d = kanode.Tsit5Options().to_c()
+    for f, _ in L.SolverOptsC._fields_:
+        assert getattr(o, f) == getattr(d, f), f
+    assert (o.abstol, o.reltol, o.adaptive, o.qmin, o.qmax) == (1e-6, 1e-3, 1, 0.2, 10.0)
 
 
 def test_struct_layout_matches_header():

@@ -1,0 +1,209 @@
+"""The native integrator (kanode_solve_tsit5 / kanode_adjoint_tsit5) vs the Python statement of
+the same algorithm (kanode/ode.py, kanode/adjoint.py with native=False) driving the same HIP
+RHS, and vs the CPU oracle: identical step sequences, saveat values and gradients.
+(solve(prob, Tsit5(); saveat) at LV_driver_KANODE.jl:180-184, Fisher-KPP_Source.jl:102-103;
+InterpolatingAdjoint = the NeuralODE default sensealg.)"""
+import ctypes as C
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import device, t
+from oracle import oracle as O
+from oracle_rhs import OracleFKRHS
+
+import kanode
+from kanode import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def fk(nx, table=None):
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
+    return kanode.FisherKPPRHS(kan1, nx=nx, dx=1.0 / (nx - 1), D=0.01, device=device(), table=table)
+
+
+def lv(dtype=torch.float64):
+    return kanode.ChainRHS(kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5)), dtype=dtype,
+                           device=device())
+
+
+def fk_u0(nx, B, seed=0):
+    rng = np.random.default_rng(seed)
+    x = np.arange(nx) / (nx - 1)
+    c, d, a = rng.uniform(0.3, 0.7, (B, 1)), rng.uniform(0.1, 0.3, (B, 1)), rng.uniform(0.5, 1, (B, 1))
+    return a * (np.tanh((x - (c - d / 2)) / (d / 10)) - np.tanh((x - (c + d / 2)) / (d / 10))) / 2
+
+
+CASES = {
+    "fk256": (lambda: fk(256), lambda: fk_u0(256, 4), 11, 1.0, (0.0, 2.0), [0.25 * i for i in range(9)]),
+    "fk256_rec": (lambda: fk(256, False), lambda: fk_u0(256, 3, 1), 11, 1.0, (0.0, 1.0), [0.0, 0.3, 0.3, 1.0]),
+    "fk26": (lambda: fk(26), lambda: fk_u0(26, 1, 2), 11, 1.0, (0.0, 2.0), [0.5 * i for i in range(5)]),
+    "lv64": (lv, lambda: np.array([[1.0, 1.0], [0.7, 1.3], [1.5, 0.6]]), 240, 0.3, (0.0, 3.5),
+             [0.1 * i for i in range(35)]),
+    "lv32": (lambda: lv(torch.float32), lambda: np.random.default_rng(3).uniform(0.5, 2.0, (64, 2)), 240, 0.3,
+             (0.0, 3.5), [0.1 * i for i in range(35)]),
+}
+
+
+def _setup(name):
+    make, mk_u0, P, scale, tspan, ts = CASES[name]
+    rhs = make()
+    dt = rhs.hd.dtype
+    p = t(np.random.default_rng(7).uniform(-scale, scale, P), dt)
+    return rhs, t(mk_u0(), dt), p, tspan, ts
+
+
+def _tol(dtype):
+    return 1e-11 if dtype == torch.float64 else 2e-5
+
+
+# fixed steps inside the explicit stability limit (FK256: D/dx² = 650)
+FIXED = {"fk256": ((0.0, 0.2), 5e-4), "fk256_rec": ((0.0, 0.2), 5e-4)}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_native_forward_matches_python_driver(name, adaptive):
+    rhs, u0, p, tspan, ts = _setup(name)
+    dt = 0.01
+    if not adaptive and name in FIXED:
+        tspan, dt = FIXED[name]
+        ts = [x for x in ts if x <= tspan[1]] + [tspan[1]]
+    opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else dt, abstol=1e-8, reltol=1e-7)
+    nat = kanode.solve(rhs, u0, tspan, p, ts, opt)
+    py = kanode.solve(rhs, u0, tspan, p, ts, dataclasses.replace(opt, native=False))
+    assert nat.stats["naccept"] == py.stats["naccept"] and nat.stats["nreject"] == py.stats["nreject"]
+    assert nat.stats["nf"] == py.stats["nf"]
+    assert nat.u.shape == py.u.shape
+    scale = max(1.0, py.u.abs().max().item())
+    assert (nat.u - py.u).abs().max().item() <= _tol(u0.dtype) * scale
+
+
+@pytest.mark.parametrize("name", ["fk256", "fk26", "lv64", "lv32"])
+def test_native_adjoint_matches_python_adjoint(name):
+    rhs, u0, p0, tspan, ts = _setup(name)
+    w = t(np.random.default_rng(11).normal(size=(len(ts),) + tuple(u0.shape)), u0.dtype)
+    # fp32: a reltol near the fp32 rounding level would make both controllers follow rounding noise
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7) if u0.dtype == torch.float64 else \
+        kanode.Tsit5Options(abstol=1e-6, reltol=1e-4)
+    out = []
+    for native in (True, False):
+        p = p0.clone().requires_grad_(True)
+        x0 = u0.clone().requires_grad_(True)
+        sol = kanode.solve(rhs, x0, tspan, p, ts, dataclasses.replace(opt, native=native),
+                           sensealg="interpolating_adjoint")
+        gp, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+        out.append((gp, gu, sol.stats))
+    (gp, gu, sn), (rp, ru, sp) = out
+    assert sn["naccept"] == sp["naccept"]
+    na, nb = sn["adjoint"]["naccept"], sp["adjoint"]["naccept"]
+    if na == nb and sn["adjoint"]["nreject"] == sp["adjoint"]["nreject"]:
+        tol = 1e-9 if u0.dtype == torch.float64 else 1e-3      # same step sequence: rounding only
+    else:
+        # A stability-limited adjoint (FK256: ~2000 steps hovering at EEst ~ 1) can flip one
+        # accept/reject on last-bit differences of the norm (fma vs separate rounding); the two
+        # then integrate the same ODE on different step sequences, so they agree to the tolerance.
+        # fp32: the initial-step norms differ at fp32 rounding (the native norms accumulate in
+        # double), so the step sequences may differ from the start.
+        assert abs(na - nb) <= (0.01 if u0.dtype == torch.float64 else 0.1) * nb
+        tol = 50 * opt.reltol if u0.dtype == torch.float64 else 5e-3
+    assert (gp - rp).abs().max().item() <= tol * rp.abs().max().item()
+    assert (gu - ru).abs().max().item() <= tol * ru.abs().max().item()
+
+
+def test_native_fk26_solve_and_gradient_match_cpu_oracle():
+    """End to end against the oracle: the native GPU solve + adjoint vs the Python driver on the
+    plain-C restatement of rc_kanode (dense Laplacian matvec, Fisher-KPP_Source.jl:55-59,95-98)."""
+    rhs, u0, p0, tspan, ts = _setup("fk26")
+    cpu = OracleFKRHS(O.LayerSpec(1, 1, 10, "softsign"), 0.01, 1.0 / 25, dense=True)
+    w = np.random.default_rng(2).normal(size=(len(ts),) + tuple(u0.shape))
+    opt = kanode.Tsit5Options(abstol=1e-9, reltol=1e-9)
+    res = []
+    for f, dev in ((rhs, device()), (cpu, "cpu")):
+        p = p0.detach().to(dev).clone().requires_grad_(True)
+        sol = kanode.solve(f, u0.to(dev), tspan, p, ts, opt, sensealg="interpolating_adjoint")
+        (g,) = torch.autograd.grad((sol.u * torch.as_tensor(w, device=dev)).sum(), [p])
+        res.append((sol.u.detach().cpu(), g.cpu(), sol.stats))
+    (ug, gg, sg), (uc, gc, sc) = res
+    assert sg["naccept"] == sc["naccept"] and sg["adjoint"]["naccept"] == sc["adjoint"]["naccept"]
+    assert (ug - uc).abs().max().item() <= 1e-11
+    assert (gg - gc).abs().max().item() <= 1e-9 * gc.abs().max().item()
+
+
+def test_native_saveat_edges():
+    """saveat at t0, duplicated, between steps, on the final time and past it (dropped, as the
+    Python driver never reaches it)."""
+    rhs, u0, p, tspan, _ = _setup("fk26")
+    ts = [0.0, 0.0, 0.123456, 1.0, 1.0, 2.0, 2.5]
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8)
+    nat = kanode.solve(rhs, u0, tspan, p, ts, opt)
+    py = kanode.solve(rhs, u0, tspan, p, ts, dataclasses.replace(opt, native=False))
+    assert nat.t == py.t == ts[:6]
+    assert torch.equal(nat.u[0], u0) and torch.equal(nat.u[1], u0)
+    assert (nat.u - py.u).abs().max().item() <= 1e-11
+
+
+def test_dense_output_reuse_is_stateless():
+    """Training reuses the dense-output storage between iterations: results equal a fresh solve."""
+    rhs, u0, p0, tspan, ts = _setup("fk256")
+    w = t(np.random.default_rng(1).normal(size=(len(ts),) + tuple(u0.shape)))
+    opt = kanode.Tsit5Options(abstol=1e-7, reltol=1e-6)
+    grads = []
+    for scale in (1.0, 0.5, 1.0):       # a different problem in between (other step count)
+        p = (p0 * scale).requires_grad_(True)
+        sol = kanode.solve(rhs, u0, tspan, p, ts, opt, sensealg="interpolating_adjoint")
+        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+        grads.append(g)
+    assert torch.equal(grads[0], grads[2])
+
+
+def test_native_solve_rejects_bad_arguments():
+    rhs, u0, p, tspan, ts = _setup("fk26")
+    lib = kanode.lib()
+    o = L.SolverOptsC()
+    lib.kanode_solver_options_default(C.byref(o))
+    out = torch.empty((2,) + tuple(u0.shape), dtype=u0.dtype, device=u0.device)
+    sv = (C.c_double * 2)(1.0, 0.5)          # descending
+    h = rhs.hd._h
+    st = lib.kanode_solve_tsit5(h, C.c_void_p(p.data_ptr()), C.c_void_p(u0.data_ptr()), 1, 0.0, 2.0, sv, 2,
+                                C.c_void_p(out.data_ptr()), C.byref(o), None, None, None)
+    assert st == L.ERR_INVALID_ARG and b"ascend" in lib.kanode_last_error(h)
+    o.adaptive, o.dt = 0, 0.0               # fixed step without dt
+    sv = (C.c_double * 2)(0.5, 1.0)
+    st = lib.kanode_solve_tsit5(h, C.c_void_p(p.data_ptr()), C.c_void_p(u0.data_ptr()), 1, 0.0, 2.0, sv, 2,
+                                C.c_void_p(out.data_ptr()), C.byref(o), None, None, None)
+    assert st == L.ERR_INVALID_ARG
+    lib.kanode_solver_options_default(C.byref(o))
+    o.maxiters = 3
+    st = lib.kanode_solve_tsit5(h, C.c_void_p(p.data_ptr()), C.c_void_p(u0.data_ptr()), 1, 0.0, 2.0, sv, 2,
+                                C.c_void_p(out.data_ptr()), C.byref(o), None, None, None)
+    assert st == L.ERR_INVALID_ARG and b"maxiters" in lib.kanode_last_error(h)
+    torch.cuda.synchronize()
+
+
+def test_fixed_step_solve_captures_into_a_hip_graph():
+    """adaptive = 0 never synchronises: the whole solve (with a reused dense output) replays from a
+    hipGraph and reproduces the eager result."""
+    rhs, u0, p, _, _ = _setup("fk256")
+    tspan, ts = (0.0, 0.05), [0.0, 0.025, 0.05]
+    opt = kanode.Tsit5Options(adaptive=False, dt=5e-4).to_c()
+    eager, _, dense = rhs.hd.solve_tsit5(p, u0, tspan[0], tspan[1], ts, opt, keep_dense=True)
+    rhs.hd.release_dense(dense)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        out, _, dense = rhs.hd.solve_tsit5(p, u0, tspan[0], tspan[1], ts, opt, keep_dense=True)   # warm (allocates)
+        rhs.hd.release_dense(dense)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            out, _, dense = rhs.hd.solve_tsit5(p, u0, tspan[0], tspan[1], ts, opt, keep_dense=True)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.isfinite(eager).all()
+    assert torch.equal(out, eager)
+    rhs.hd.release_dense(dense)
