@@ -116,7 +116,7 @@ def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: fl
     torch.cuda.synchronize()
     gpu_s = (time.perf_counter() - t0) / reps
     out = {"unit": "s/epoch", "gpu": gpu_s, "gpu_batch": B_gpu, "steps": steps, "dt": dt, "stages_per_step": 6,
-           "what": "fixed-step Tsit5 solve + InterpolatingAdjoint + Adam, FK256 fp64"}
+           "what": "fixed-step Tsit5 solve + InterpolatingAdjoint + Adam, FK256 fp64 (native kanode_solve_tsit5 + kanode_adjoint_tsit5)"}
     if B_cpu > 0:
         from oracle import oracle as O
         from oracle.oracle_rhs import OracleFKRHS
@@ -136,7 +136,10 @@ def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: fl
 
 def lv4096_bench(dev, steps: int = 200):
     """BASELINE configs[1]: Lotka-Volterra KAN [2,10,2] grid=5, 4096 batched ICs, fp32 — the
-    NeuralODE dudt (LV_driver_KANODE.jl:139-143,180) over the batch, as RHS evals/s."""
+    NeuralODE dudt (LV_driver_KANODE.jl:139-143,180) over the batch, as RHS evals/s.  One RHS is
+    one launch of the fused chain kernel (kd_chain_col_kernel); 32 KB of state makes a single
+    call launch-bound, so the device rate is measured on a hipGraph of `steps` back-to-back RHS
+    calls (captured through the C-ABI after kanode_reserve), next to the eager per-call time."""
     chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
     rhs = kanode.ChainRHS(chain, dtype=torch.float32, device=dev)
     p = torch.as_tensor(chain.setup(np.random.default_rng(0))[0] / 1e5, dtype=torch.float32, device=dev)
@@ -151,9 +154,28 @@ def lv4096_bench(dev, steps: int = 200):
     for _ in range(steps):
         rhs.rhs(u, p, du)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": 4096 / dt, "unit": "RHS-evals/s", "us_per_launch": dt * 1e6, "batch": 4096, "dtype": "f32",
-            "note": "one launch per layer; launch-bound at this size (32 KB of state)"}
+    eager = (time.perf_counter() - t0) / steps
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        rhs.rhs(u, p, du)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=s):
+            for _ in range(steps):
+                rhs.rhs(u, p, du)
+    graph.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        graph.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    dt = e0.elapsed_time(e1) * 1e-3 / (5 * steps)
+    return {"value": 4096 / dt, "unit": "RHS-evals/s", "us_per_rhs": dt * 1e6, "batch": 4096, "dtype": "f32",
+            "eager_us_per_call": eager * 1e6,
+            "note": f"device time per RHS from a hipGraph of {steps} launches (one fused-chain kernel each)"}
 
 
 def main() -> None:
@@ -233,6 +255,15 @@ def main() -> None:
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # this box's streaming reference: a device copy moving the same bytes (u -> du)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    du.copy_(u)
+    c0.record(stream)
+    for _ in range(5):
+        du.copy_(u)
+    c1.record(stream)
+    torch.cuda.synchronize()
+    copy_gbps = 16.0 * B * nx / (c0.elapsed_time(c1) / 5 * 1e-3) / 1e9
 
     total_evals = B * args.steps * world
     value = total_evals / elapsed
@@ -262,7 +293,8 @@ def main() -> None:
                      "kernel": ("fk_pp_build_kernel + fk_rhs_pp_wave_kernel<SOFTSIGN,RBF,2>" if table
                                 else "fk_rhs_kernel<double,SOFTSIGN,REC_CORR,10>"),
                      "kernel_ms": kern_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     "torch_copy_GBps": copy_gbps},
     }
 
     if not args.no_vjp:

@@ -108,6 +108,83 @@ kd_fwd_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, c
     }
 }
 
+// A whole small chain in one launch (every layer I, O <= 16; the NeuralODE dudt of
+// LV_driver_KANODE.jl:139-143, KAN [2,10,2]).  A group of 16 lanes owns one column and lane
+// j holds activation j, so a layer's inputs are spread over lanes: lane i evaluates the G
+// basis values and swish of its input and its partial sums for every output o, the group
+// sums them with butterfly shuffles, and lane o keeps output o as the next layer's input.
+// 16x the waves of a thread-per-column kernel, each with 1/I of the serial work: at 4096
+// columns the per-column latency chain, not launch count, bounds it.  The parameter vector
+// and the layers' constants are staged in LDS once per block (wave-uniform LDS reads).
+constexpr int kChainBlock = 256;
+constexpr int kChainDim = 16;    // lanes per column = max layer width
+template <typename T, int NORM, int PATH>
+__global__ void __launch_bounds__(kChainBlock)
+kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
+                    const T* __restrict__ x, T* __restrict__ y, int64_t K) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char chain_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(chain_raw);
+    T* ps = reinterpret_cast<T*>(chain_raw + nl * sizeof(LayerConst));
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(chain_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+    }
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps)
+    const Math<T> M{tab};
+    const int I0 = lcl[0].I, OL = lcl[nl - 1].O;
+    const int j = threadIdx.x & (kChainDim - 1);
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kChainDim;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kChainDim; k < K; k += stride) {
+        T a = j < I0 ? x[(int64_t)I0 * k + j] : T(0);
+        for (int l = 0; l < nl; ++l) {
+            const LayerConst& lc = lcl[l];
+            const int I = lc.I, O = lc.O, G = lc.G;
+            const T* __restrict__ C = ps + lc.p_off;
+            const T* __restrict__ W = ps + lc.w_off;
+            T acc[kChainDim], bas[kChainDim];
+#pragma unroll
+            for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
+            if (j < I) {
+                BasisStream<T, PATH> bs;
+                bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
+                for (int g = 0; g < G; ++g) {
+                    T z, aux;
+                    const T phi = bs.next(M, lc, g, z, aux);
+                    const T* Cc = C + O * (g + G * j);
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o)
+                        if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
+                }
+                if (lc.use_base) {
+                    const T sw = swish<T>(M, a);
+                    const T* Wj = W + O * j;
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o)
+                        if (o < O) bas[o] = Wj[o] * sw;
+                }
+            }
+            T out = T(0);
+#pragma unroll
+            for (int o = 0; o < kChainDim; ++o) {
+                if (o < O) {
+                    T s = acc[o], b = bas[o];
+#pragma unroll
+                    for (int m = 1; m < kChainDim; m <<= 1) {
+                        s += __shfl_xor(s, m, kChainDim);
+                        if (lc.use_base) b += __shfl_xor(b, m, kChainDim);
+                    }
+                    if (o == j) out = lc.use_base ? s + b : s;
+                }
+            }
+            a = out;
+        }
+        if (j < OL) y[(int64_t)OL * k + j] = a;
+    }
+}
+
 // Column VJP with LDS staging: per tile of TILE columns every thread stages its
 // basis values φ[c][t], ȳ[o][t], swish(x)[i][t] in LDS (rows padded to TILE+1),
 // then the block computes the tile's dC = ȳ·φᵀ, dW = ȳ·swish(x)ᵀ with each
@@ -329,7 +406,40 @@ hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const
     }
 }
 
+// One launch for the whole chain when every layer is small (I, O <= 16), shares the
+// normalizer/path specialisation, the parameters fit in LDS and the batch is small enough
+// to be latency-bound; else returns hipErrorNotSupported and the caller runs one launch
+// per layer.
+template <typename T>
+hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                               const T* x, T* y, int64_t K, hipStream_t st) {
+    // 16 lanes per column pays while the batch leaves the chip latency-bound (<= 32 columns
+    // per CU); beyond that the per-layer thread-per-column kernels keep every lane busy
+    if (nl < 1 || nl > 8 || K > 32768) return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T);
+    if (lds > 48 * 1024) return hipErrorNotSupported;
+    const int g = grid_for(K * kChainDim, kChainBlock, kGridCap);
+    const LayerConst& h = hlcs[0];
+#define KAN_CHAIN(NORM, PATH)                                                                                    \
+    hipLaunchKernelGGL((kd_chain_col_kernel<T, NORM, PATH>), dim3(g), dim3(kChainBlock), lds, st, lcs, nl, p,     \
+                       (int)P, x, y, K)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CHAIN(NORM_TANH_FAST, PATH_REC);
+    else if (h.path == PATH_REC_CORR) KAN_CHAIN(NORM_RUNTIME, PATH_REC_CORR);
+    else if (h.path == PATH_REC) KAN_CHAIN(NORM_RUNTIME, PATH_REC);
+    else KAN_CHAIN(NORM_RUNTIME, PATH_DIRECT);
+#undef KAN_CHAIN
+    return hipGetLastError();
+}
+
 #define KAN_COL_INST(T)                                                                                          \
+    template hipError_t launch_kd_chain_col<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,     \
+                                               const T*, T*, int64_t, hipStream_t);                               \
     template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
     template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
                                              int64_t, hipStream_t);                                               \

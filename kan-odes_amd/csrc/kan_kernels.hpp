@@ -66,6 +66,10 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                              hipStream_t st);
+// whole chain, one launch (all layers I, O <= 16); hipErrorNotSupported otherwise
+template <typename T>
+hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                               const T* x, T* y, int64_t K, hipStream_t st);
 template <typename T>
 hipError_t launch_kd_vjp_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb,
                              T* xb, T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st);

@@ -333,6 +333,13 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
         HIP_TRY(h, kan::launch_fk_rhs<T>(h->hlc[0], h->dlc, p, cd, co, (int)h->spec.nx, u, du, B, st));
         return KANODE_OK;
     }
+    bool all_col = h->n_layers > 1;
+    for (int l = 0; l < h->n_layers; ++l) all_col = all_col && h->kind[l] == KIND_COL;
+    if (all_col) {
+        const hipError_t e = kan::launch_kd_chain_col<T>(h->hlc, h->n_layers, h->dlc, p, h->P, u, du, B, st);
+        if (e == hipSuccess) return KANODE_OK;
+        if (e != hipErrorNotSupported) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_col: ") + hipGetErrorString(e));
+    }
     kanode_status s = ensure_ws(h, B, st);
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;

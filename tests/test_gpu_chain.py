@@ -118,3 +118,24 @@ def test_chain_empty_batch():
     hd = _handle([O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")], torch.float64)
     p = t(np.zeros(hd.P))
     assert hd.rhs(p, torch.empty((0, 2), dtype=torch.float64, device=device())).shape == (0, 2)
+
+
+@pytest.mark.parametrize("name", CHAIN_FIXTURES)
+def test_fused_chain_equals_layer_by_layer(golden, name):
+    """The one-launch chain kernel (kd_chain_col_kernel, small layers: the layer's input sums run as a
+    lane butterfly instead of a sequential loop) equals the composition of kanode_layer_forward calls
+    to rounding (the stated RTOL of the dtype against the |terms| scale)."""
+    d = golden(name)
+    specs = specs_from_meta(d["meta"])
+    dt = _dt(d["meta"])
+    hd = _handle(specs, dt)
+    p = t(d["p"], dt)
+    x = t(np.tile(d["u"], (97, 1)), dt)          # 97 x rows: several blocks and a ragged tail
+    y = hd.rhs(p, x)
+    cur, off = x, 0
+    for li, s in enumerate(specs):
+        n = s.param_length()
+        cur = hd.layer_forward(li, p[off:off + n].contiguous(), cur)
+        off += n
+    sc = chain_scale(specs, d["p"].astype(np.float64), np.tile(d["u"], (97, 1)).astype(np.float64))
+    assert_close(y, cur.cpu().numpy(), sc, RTOL[dt], name)
