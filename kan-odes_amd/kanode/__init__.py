@@ -12,11 +12,13 @@ from .rhs import ChainRHS, FisherKPPRHS, fisher_kpp_laplacian, layer_apply, rhs_
 from .ode import Solution, Tsit5Options, solve
 from .adjoint import DenseRecord, interpolating_adjoint
 from .train import Adam, Trainer, mse_loss, reg_loss
-from . import checkpoint
+from . import checkpoint, tp
+from .tp import GridShardedChainRHS
 
 __all__ = [
     "DenseRecord", "interpolating_adjoint",
     "KanodeError", "LIB_PATH", "lib", "KanodeHandle", "LayerCfg", "Chain", "KDense", "glorot_uniform",
     "linrange_f32", "ChainRHS", "FisherKPPRHS", "fisher_kpp_laplacian", "layer_apply", "rhs_apply",
-    "Solution", "Tsit5Options", "solve", "Adam", "Trainer", "mse_loss", "reg_loss", "checkpoint",
+    "Solution", "Tsit5Options", "solve", "Adam", "Trainer", "mse_loss", "reg_loss", "checkpoint", "tp",
+    "GridShardedChainRHS",
 ]

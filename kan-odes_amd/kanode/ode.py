@@ -62,6 +62,16 @@ def rms(x: torch.Tensor) -> torch.Tensor:
     return torch.sqrt(torch.mean(x * x))
 
 
+def _norm(f, x: torch.Tensor) -> float:
+    """ODE_DEFAULT_NORM of x: RMS over every state entry.  A state sharded over ranks
+    (kanode.tp) supplies f.reduce_sum, and the sum and count run over all shards."""
+    red = getattr(f, "reduce_sum", None)
+    if red is None:
+        return rms(x).item()
+    x = x.detach().double()
+    return math.sqrt(red(float((x * x).sum())) / red(float(x.numel())))
+
+
 @dataclass
 class Tsit5Options:
     abstol: float = 1e-6
@@ -102,13 +112,13 @@ class Solution:
 def _initdt(f, u0, p, t0, tdist, opt: Tsit5Options, f0):
     """Hairer & Wanner initial step (OrdinaryDiffEq ode_determine_initdt, order 5)."""
     sk = opt.abstol + torch.abs(u0) * opt.reltol
-    d0 = rms(u0 / sk).item()
-    d1 = rms(f0 / sk).item()
+    d0 = _norm(f, u0 / sk)
+    d1 = _norm(f, f0 / sk)
     dt0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
     dt0 = min(dt0, tdist)
     u1 = u0 + dt0 * f0
     f1 = f(u1, p, t0 + dt0)
-    d2 = rms((f1 - f0) / sk).item() / dt0
+    d2 = _norm(f, (f1 - f0) / sk) / dt0
     mx = max(d1, d2)
     dt1 = max(1e-6, dt0 * 1e-3) if mx <= 1e-15 else (0.01 / mx) ** (1.0 / 5.0)
     return min(100 * dt0, dt1, tdist)
@@ -212,7 +222,7 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
             if not fused:
                 utilde = dt * sum(b * k for b, k in zip(BTILDE, ks))
                 sk = opt.abstol + torch.maximum(torch.abs(u), torch.abs(unew)) * opt.reltol
-                EEst = rms(utilde.detach() / sk.detach()).item()
+                EEst = _norm(f, utilde.detach() / sk.detach())
             q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
             if EEst > 1.0 and dt > opt.dtmin:
                 nreject += 1

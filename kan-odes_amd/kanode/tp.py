@@ -1,0 +1,142 @@
+"""Grid-sharded (tensor-parallel) full-field KAN surrogate — BASELINE configs[3]
+("Burgers_Surrogate.jl full-field KAN surrogate, 512 spatial x 200 steps, grid sharded
+4xMI355X"), SURVEY §8e E1.
+
+The surrogate RHS is du = KDense(H -> N)(KDense(N -> H)(u)) over the N-point field
+(PDE examples/Burgers_Surrogate.jl:85-97: KAN [512, 10, 512]).  With the spatial grid
+split over the R ranks of a process group, rank r owns the grid points [a_r, b_r):
+  * its slice of the state u[a_r:b_r, B] (every Tsit5 stage combination is local);
+  * layer 1's input columns C1[:, :, a_r:b_r], W1[:, a_r:b_r] -> the PARTIAL pre-activation
+    h_r = Σ_{i in slice} (C1 φ(u_i) + W1 swish(u_i))  as a KDense(n_r -> H) launch;
+  * one all_reduce(SUM) of the [H, B] partials per RHS (RCCL over xGMI with backend
+    "nccl"; 10·B values — latency-bound, the only exchange of the forward);
+  * layer 2's output rows C2[a_r:b_r, :, :], W2[a_r:b_r, :] -> du[a_r:b_r] as a
+    KDense(H -> n_r) launch.
+The pullback mirrors it: layer-2 VJP (local dC2/dW2 rows) -> all_reduce(SUM) of the [H, B]
+hidden cotangent partials -> layer-1 VJP (local dC1/dW1 columns, local ū slice).  Every
+parameter gradient is therefore shard-local: d(Σ_r L_r)/dp_r lands on the rank owning p_r,
+and no gradient all-reduce is needed across the grid shards (a data-parallel group over
+trajectories, if any, still all-reduces its gradients in Trainer).  The adaptive step
+control's error norm is the one global reduction of the integrator (`reduce_sum`).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .handle import KanodeHandle, LayerCfg
+from .rhs import layer_apply
+
+
+def shard_bounds(n: int, world: int, rank: int):
+    """Contiguous, balanced split of n grid points: [a, b) of `rank`."""
+    q, r = divmod(n, world)
+    a = rank * q + min(rank, r)
+    return a, a + q + (1 if rank < r else 0)
+
+
+def shard_index(cfg1: LayerCfg, cfg2: LayerCfg, a: int, b: int) -> np.ndarray:
+    """Positions in the full flat parameter vector (ComponentArray order, column-major:
+    layer_1.C [H, G·N], layer_1.W [H, N], layer_2.C [N, G·H], layer_2.W [N, H];
+    LV_driver_KANODE.jl:173-175) of the local vector [C1 cols, W1 cols, C2 rows, W2 rows] of the
+    shard [a, b)."""
+    N, H, G1, G2 = cfg1.in_dims, cfg1.out_dims, cfg1.grid_len, cfg2.grid_len
+    if cfg2.in_dims != H or cfg2.out_dims != N:
+        raise ValueError("a grid-sharded surrogate is KDense(N -> H) then KDense(H -> N)")
+    parts = [np.arange(H * G1 * a, H * G1 * b)]                    # C1[o, g + G·i], i in [a, b): contiguous
+    off = H * G1 * N
+    if cfg1.use_base_act:
+        parts.append(off + np.arange(H * a, H * b))                # W1[o, i]
+        off += H * N
+    rows = np.arange(a, b)
+    parts.append(off + (rows[None, :] + N * np.arange(G2 * H)[:, None]).reshape(-1))   # C2[o, c], o in [a, b)
+    off += N * G2 * H
+    if cfg2.use_base_act:
+        parts.append(off + (rows[None, :] + N * np.arange(H)[:, None]).reshape(-1))    # W2[o, i]
+    return np.concatenate(parts)
+
+
+class _AllReduceSum(torch.autograd.Function):
+    """y = Σ_ranks x; backward: x̄ = Σ_ranks ȳ (the pullback of a sum over ranks)."""
+
+    @staticmethod
+    def forward(ctx, x, reduce):
+        ctx.reduce = reduce
+        return reduce(x.clone())
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.reduce(g.contiguous().clone()), None
+
+
+class GridShardedChainRHS:
+    """NeuralODE RHS of a KAN [N, H, N] surrogate with the grid sharded over `group`.
+
+    u: (B, n_r) local slice of the Julia [N, B] state; p: the local parameter vector
+    (`shard_params`).  `layer_fn(l, p_l, x)` overrides the HIP layer launches (tests run the
+    CPU oracle through it); the default binds one kanode handle [KDense(n_r, H), KDense(H, n_r)]."""
+
+    def __init__(self, cfg1: LayerCfg, cfg2: LayerCfg, group=None, dtype=torch.float64, device=None,
+                 layer_fn=None):
+        self.group = group if group is not None else (dist.group.WORLD if dist.is_initialized() else None)
+        self.world = dist.get_world_size(self.group) if self.group is not None else 1
+        self.rank = dist.get_rank(self.group) if self.group is not None else 0
+        self.cfg1, self.cfg2 = cfg1, cfg2
+        self.N, self.H = cfg1.in_dims, cfg1.out_dims
+        self.a, self.b = shard_bounds(self.N, self.world, self.rank)
+        self.n = self.b - self.a
+        rep = dict(normalizer=cfg1.normalizer, basis=cfg1.basis, use_base_act=cfg1.use_base_act,
+                   grid_lims=cfg1.grid_lims, denominator=cfg1.denominator, iqf_reference_quirk=cfg1.iqf_reference_quirk)
+        self.local1 = LayerCfg(self.n, self.H, cfg1.grid_len, **rep)
+        rep2 = dict(normalizer=cfg2.normalizer, basis=cfg2.basis, use_base_act=cfg2.use_base_act,
+                    grid_lims=cfg2.grid_lims, denominator=cfg2.denominator, iqf_reference_quirk=cfg2.iqf_reference_quirk)
+        self.local2 = LayerCfg(self.H, self.n, cfg2.grid_len, **rep2)
+        self.P1 = self.local1.param_length
+        self.P = self.P1 + self.local2.param_length
+        self.index = shard_index(cfg1, cfg2, self.a, self.b)
+        assert self.index.size == self.P
+        self.P_full = cfg1.param_length + cfg2.param_length
+        self.dtype = dtype
+        if layer_fn is None:
+            self._hd = KanodeHandle([self.local1, self.local2], dtype=dtype, rhs_kind="chain", device=device)
+            layer_fn = lambda l, pl, x: layer_apply(self._hd, l, pl, x)   # noqa: E731
+        self.layer_fn = layer_fn
+        self.backend = dist.get_backend(self.group) if self.group is not None else None
+
+    # -- collectives ---------------------------------------------------------------
+    def _allreduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return x
+        if self.backend == "gloo" and x.is_cuda:      # gloo rehearsal on one GPU: stage through host
+            h = x.cpu()
+            dist.all_reduce(h, group=self.group)
+            return h.to(x.device)
+        dist.all_reduce(x, group=self.group)
+        return x
+
+    def reduce_sum(self, v: float) -> float:
+        """Σ over the grid shards (the integrator's global error norm)."""
+        if self.world == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        if self.backend == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, group=self.group)
+        return float(t.item())
+
+    # -- parameters -------------------------------------------------------------------
+    def shard_params(self, p_full: torch.Tensor) -> torch.Tensor:
+        return p_full[torch.as_tensor(self.index, device=p_full.device)].contiguous()
+
+    def gather_params(self, p_local: torch.Tensor) -> torch.Tensor:
+        """The full ComponentArray vector (for .mat checkpoints), assembled on every rank."""
+        full = torch.zeros(self.P_full, dtype=p_local.dtype, device=p_local.device)
+        full[torch.as_tensor(self.index, device=p_local.device)] = p_local
+        return self._allreduce(full)
+
+    # -- the RHS --------------------------------------------------------------------------
+    def __call__(self, u: torch.Tensor, p: torch.Tensor, t=None) -> torch.Tensor:
+        hpart = self.layer_fn(0, p[:self.P1], u)                  # (B, H) partial pre-activation
+        h = _AllReduceSum.apply(hpart, self._allreduce)           # one [H, B] all-reduce per RHS
+        return self.layer_fn(1, p[self.P1:], h)                   # (B, n_r): own rows of du

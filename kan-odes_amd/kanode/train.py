@@ -64,8 +64,11 @@ class Trainer:
     (len(saveat), *u0.shape).  `group` is a torch.distributed process group (or None)."""
 
     def __init__(self, rhs, u0, tspan, saveat, target, p0, eta: float = 5e-4, solver: Tsit5Options | None = None,
-                 sparse_reg: float = 0.0, group=None, sensealg: str | None = None):
+                 sparse_reg: float = 0.0, group=None, sensealg: str | None = None, tp: bool = False):
+        """tp=True: `rhs` is grid-sharded (kanode.tp.GridShardedChainRHS); u0/target/p0 are this rank's
+        slices, the loss is this shard's part of the global mean, gradients are shard-local."""
         self.rhs, self.u0, self.tspan, self.saveat, self.target = rhs, u0, tspan, saveat, target
+        self.tp = tp
         self.p = p0.detach().clone()
         self.opt = Adam(eta)
         self.solver = solver or Tsit5Options()
@@ -82,7 +85,10 @@ class Trainer:
     def loss_and_grad(self):
         p = self.p.detach().requires_grad_(True)
         sol = self.predict(p)
-        loss = mse_loss(sol.u, self.target)
+        if self.tp:   # Σ over the grid shards of these partial sums = the global mean
+            loss = torch.sum((self.target - sol.u) ** 2) / self.rhs.reduce_sum(float(sol.u.numel()))
+        else:
+            loss = mse_loss(sol.u, self.target)
         if self.sparse_reg:
             loss = loss + reg_loss(p, self.sparse_reg, 0.0)
         (g,) = torch.autograd.grad(loss, p)
@@ -90,6 +96,8 @@ class Trainer:
 
     def step(self) -> float:
         loss, g, _ = self.loss_and_grad()
+        if self.tp:
+            loss = torch.as_tensor(self.rhs.reduce_sum(float(loss)), dtype=g.dtype)
         if self.group is not None:
             import torch.distributed as dist
             ws = dist.get_world_size(self.group)
