@@ -446,7 +446,10 @@ __device__ __forceinline__ void pp_direct_dphi_sw(const Math<double>& M, const L
     dphi = dnormalize<NORM, double>(lc.norm, n) * s + (lc.use_base ? p[G] * dsw : 0.0);
 }
 
-// Two tables sharing one interval index: φ'(u) from td, swish(u) from ts.
+// Two tables sharing one interval index: φ'(u) from td, swish(u) from ts.  The two Horner
+// chains run one after the other (a scheduling barrier between them) so only one table's
+// five 16-byte LDS reads are live at a time: register pressure, not latency, limits the
+// VJP kernels' occupancy.
 __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const double2* __restrict__ ts, int ni,
                                          double inv_w, double x0, double u, double& d, double& s) {
     const double x = ::fma(u, inv_w, x0);
@@ -457,25 +460,34 @@ __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const d
     const double t = ::fma(2.0, xc - fl, -1.0);
     const double2* __restrict__ a = td + k;
     const double2* __restrict__ b = ts + k;
-    const double2 a8 = a[4 * ni], a6 = a[3 * ni], a4 = a[2 * ni], a2 = a[ni], a0 = a[0];
-    const double2 b8 = b[4 * ni], b6 = b[3 * ni], b4 = b[2 * ni], b2 = b[ni], b0 = b[0];
-    double y = ::fma(a8.y, t, a8.x), z = ::fma(b8.y, t, b8.x);
-    y = ::fma(y, t, a6.y);
-    z = ::fma(z, t, b6.y);
-    y = ::fma(y, t, a6.x);
-    z = ::fma(z, t, b6.x);
-    y = ::fma(y, t, a4.y);
-    z = ::fma(z, t, b4.y);
-    y = ::fma(y, t, a4.x);
-    z = ::fma(z, t, b4.x);
-    y = ::fma(y, t, a2.y);
-    z = ::fma(z, t, b2.y);
-    y = ::fma(y, t, a2.x);
-    z = ::fma(z, t, b2.x);
-    y = ::fma(y, t, a0.y);
-    z = ::fma(z, t, b0.y);
-    y = ::fma(y, t, a0.x);
-    z = ::fma(z, t, b0.x);
+    double y, z;
+    {
+        const double2 a8 = a[4 * ni], a6 = a[3 * ni], a4 = a[2 * ni], a2 = a[ni], a0 = a[0];
+        y = ::fma(a8.y, t, a8.x);
+        y = ::fma(y, t, a6.y);
+        y = ::fma(y, t, a6.x);
+        y = ::fma(y, t, a4.y);
+        y = ::fma(y, t, a4.x);
+        y = ::fma(y, t, a2.y);
+        y = ::fma(y, t, a2.x);
+        y = ::fma(y, t, a0.y);
+        y = ::fma(y, t, a0.x);
+    }
+#if KAN_VJP_SPLIT_HORNER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    {
+        const double2 b8 = b[4 * ni], b6 = b[3 * ni], b4 = b[2 * ni], b2 = b[ni], b0 = b[0];
+        z = ::fma(b8.y, t, b8.x);
+        z = ::fma(z, t, b6.y);
+        z = ::fma(z, t, b6.x);
+        z = ::fma(z, t, b4.y);
+        z = ::fma(z, t, b4.x);
+        z = ::fma(z, t, b2.y);
+        z = ::fma(z, t, b2.x);
+        z = ::fma(z, t, b0.y);
+        z = ::fma(z, t, b0.x);
+    }
     d = y;
     s = z;
     return in && (y == y) && (z == z);
@@ -518,6 +530,20 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
     return l * dphi;
 }
 
+// Block size of the VJP kernels: LDS (two 20 KB tables + the exp table, 42 KB) allows 3 blocks
+// per CU and the registers (~140 VGPRs) 3 waves/SIMD, so 256-thread blocks fill both.  Measured
+// (tools/ab_rhs.py --op vjp, 1M trajectories): 256/3 waves 1639 us; 512-thread blocks at 3 or 4
+// waves/SIMD (the latter spilling) 1740-1746 us.
+#ifndef KAN_VJP_BLOCK
+#define KAN_VJP_BLOCK 256
+#endif
+#ifndef KAN_VJP_SPLIT_HORNER
+#define KAN_VJP_SPLIT_HORNER 1
+#endif
+#ifndef KAN_VJP_WPE
+#define KAN_VJP_WPE 3
+#endif
+constexpr int kVjpBlock = KAN_VJP_BLOCK;
 // Nx = 128·NP, one wave per trajectory row (as fk_rhs_pp_wave_kernel): u and λ by
 // nontemporal 16-B loads, λ's stencil neighbours by wave rotation, λᵀJ by
 // nontemporal stores; per-thread dC/dW registers, block-summed into the slab row
@@ -528,7 +554,7 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 // to lam_out when non-null); with err_slab the λ error Σ (e/sk)², e = Σ sl.ec_j sl.k_j +
 // sl.ec_nk λᵀJ, sk = abstol + reltol·max(|lam|,|λs|), is block-summed into err_slab[block].
 template <int NORM, int PATH, int GT, int NP, bool STG>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))   // LDS allows 3 blocks/CU
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VJP_WPE)))
 fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                       const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
@@ -536,7 +562,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                       double* __restrict__ lam_out, double* __restrict__ err_slab) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
-    __shared__ double red[(kBlock / kWave) * (GT + 1)];
+    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     const int tsz = (kPPCoef / 2) * ni;   // double2 per table
     for (int i = threadIdx.x; i < tsz; i += kBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
@@ -559,8 +585,8 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     const bool want_err = STG && err_slab != nullptr;
     double eacc = 0.0;
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
-    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+    const int64_t rstride = (int64_t)gridDim.x * (kVjpBlock / kWave);
+    for (int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
         const int64_t rb = b * Nx + 2 * lane;
         kd2 uv[NP], lv[NP], l0[NP], ev[NP];
 #pragma unroll
@@ -796,10 +822,10 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 // 98.7 us at 1024 blocks vs 101.4 us at the 6-block occupancy limit); the nontemporal
 // copy microbenchmark peaks at the same shape.  KANODE_PP_GRID overrides (tuning only).
 template <typename K>
-static int pp_grid_cap(K kernel, size_t lds) {
+static int pp_grid_cap(K kernel, size_t lds, int bs = kBlock) {
     int dev = 0, cus = 256, nb = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, lds) != hipSuccess || nb < 1) nb = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, bs, lds) != hipSuccess || nb < 1) nb = 4;
     return (nb < 4 ? nb : 4) * cus;
 }
 
@@ -917,9 +943,9 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
 #define KAN_VJP_WAVE(NP)                                                                                          \
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
-        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds);                       \
-        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
-        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kBlock), lds, st,  \
+        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds, kVjpBlock);            \
+        grid = grid_for(B, kVjpBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kVjpBlock), lds, st,  \
                            lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
                            su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr);               \
     } while (0)

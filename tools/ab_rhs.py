@@ -51,11 +51,14 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--op", default="rhs", choices=["rhs", "vjp"], help="kanode_rhs or kanode_vjp")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     nx, dx, D = 256, 1 / 255, 0.01
     u = fk_ics(a.batch, nx, dx, 1, dev)
     du = torch.empty_like(u)
+    lam = torch.randn_like(u) if a.op == "vjp" else None
+    dp = torch.zeros(11, dtype=torch.float64, device=dev)
     p = torch.as_tensor(np.random.default_rng(0).uniform(-1, 1, 11), device=dev)
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     libs = [(os.path.basename(x).replace(".so", ""), load(x)) for x in a.libs]
@@ -63,7 +66,7 @@ def main():
     grids = [int(g) for g in a.grids.split(",")]
     cells = {}
     ref = None
-    nbytes = 8.0 * (11 + 2 * a.batch * nx)
+    nbytes = 8.0 * (11 + 2 * a.batch * nx) if a.op == "rhs" else 8.0 * (22 + 3 * a.batch * nx)
     for r in range(a.rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(2):
@@ -77,8 +80,13 @@ def main():
         for n, lib in libs:
             for g in grids:
                 os.environ["KANODE_PP_GRID"] = str(g)
-                call = lambda: lib.kanode_rhs(hs[n], C.c_void_p(p.data_ptr()), C.c_void_p(u.data_ptr()),
-                                              C.c_void_p(du.data_ptr()), a.batch, st)
+                if a.op == "rhs":
+                    call = lambda: lib.kanode_rhs(hs[n], C.c_void_p(p.data_ptr()), C.c_void_p(u.data_ptr()),  # noqa: E731
+                                                  C.c_void_p(du.data_ptr()), a.batch, st)
+                else:
+                    call = lambda: lib.kanode_vjp(hs[n], C.c_void_p(p.data_ptr()), C.c_void_p(u.data_ptr()),  # noqa: E731
+                                                  C.c_void_p(lam.data_ptr()), C.c_void_p(du.data_ptr()),
+                                                  C.c_void_p(dp.data_ptr()), a.batch, st)
                 for _ in range(2):
                     assert call() == 0
                 e0.record()
