@@ -194,10 +194,14 @@ kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const v
  *     Tsitouras 5(4) with FSAL, error norm = RMS over ALL N*B state entries (a batched
  *     state is one ODE), PI controller, Hairer-Wanner initial step, saveat from the
  *     free 4th-order interpolant.
- *   adaptive = 1: one 8-byte device->host read of the error norm per step (the
- *     accept/reject decision); adaptive = 0 (fixed dt): no host synchronisation at
- *     all, so the whole solve can be captured into a hipGraph (reserve + a reused
- *     kanode_solution first).
+ *   control = host: adaptive = 1 reads the 8-byte error norm once per step (the
+ *     accept/reject decision on the host); adaptive = 0 (fixed dt) never synchronises,
+ *     so the whole solve can be captured into a hipGraph by the caller.
+ *   control = device: the controller runs on the GPU (tsit5_post_kernel: accept/reject,
+ *     step size, saveat, dense-output record, u <- u_new commit) and the solve is a
+ *     hipGraph of graph_steps step slots (stage launches read the step size from device
+ *     memory) replayed until done: one host read per replay instead of per step.  The
+ *     graph is cached in the kanode_solution.  auto = device for states up to 64 MB.
  * kanode_adjoint_tsit5 is SciMLSensitivity 7.69's InterpolatingAdjoint (the NeuralODE
  * default; the reference's gradients): the adjoint ODE [λ; μ] integrated backward
  * with Tsit5 at the same tolerances, u(t) from the forward dense output, λ += ∂L/∂u
@@ -211,6 +215,9 @@ typedef struct {
     double dtmin;                   /* 0 */
     double beta1, beta2, gamma;     /* 7/50, 2/25, 9/10 */
     double qmin, qmax, qoldinit;    /* 1/5, 10, 1e-4 */
+    int32_t control;                /* step control: 0 = auto, 1 = host (one 8-byte norm read per step),
+                                       2 = device (hipGraph of graph_steps step slots, replayed until done) */
+    int32_t graph_steps;            /* step slots per graph replay (device control; even, 0 = 16) */
 } kanode_solver_options;
 void kanode_solver_options_default(kanode_solver_options* opt);
 

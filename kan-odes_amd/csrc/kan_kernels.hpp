@@ -19,6 +19,8 @@ hipError_t launch_fk_vjp(const LayerConst& hlc, const LayerConst* lc, const T* p
 // Runge-Kutta stage arguments (kanode_rhs_stage): y = u + Σ_{j<nk} c_j k_j; optional
 // embedded error e = Σ_{j<nk} ec_j k_j + ec_nk du, Σ (e / (abstol + reltol·max(|u|,|y|)))².
 constexpr int kMaxStages = 8;
+// cscale (nullable, device): c_j and ec_j are multiplied by *cscale inside the kernel — the
+// step size of a device-controlled solve (kanode_solve.cpp graph mode) lives in device memory.
 template <typename T>
 struct StageArgs {
     const T* k[kMaxStages];
@@ -26,7 +28,11 @@ struct StageArgs {
     double ec[kMaxStages + 1];
     double abstol, reltol;
     int nk;
+    const double* cscale;
+    const int32_t* skip;    // nullable, device: the launch does nothing while *skip != 0 (a finished solve)
 };
+__device__ __forceinline__ double stage_scale(const double* cscale) { return cscale ? *cscale : 1.0; }
+__device__ __forceinline__ bool stage_skip(const int32_t* skip) { return skip && *skip; }
 template <typename T>
 hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st);
 // per-block partials into `slab` (<= slab_blocks rows), then out[0] = ordered total
@@ -76,6 +82,32 @@ hipError_t launch_kd_vjp_col(const LayerConst& hlc, const LayerConst* lc, const 
 template <typename T>
 hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* act, int64_t K,
                               hipStream_t st);
+
+// device-side Tsit5 step control (kan_solve.hip; kanode_solve.cpp graph mode)
+struct SolveCtl {
+    double t, dt, qold, eest;
+    int64_t naccept, nreject, attempts, si;
+    int32_t done, status, accepted, pad;   // status: 0 ok, 1 maxiters, 2 dense-output storage full
+};
+template <typename T>
+struct Tsit5Bufs {
+    T* U;               // u_n (committed on accept)
+    T* K[7];            // k_1 .. k_7 (k_1 <- k_7 on accept)
+    const T* UNEW;      // stage-7 output u_{n+1}
+    T* save;            // [n_save][n] saveat values
+    void* const* slots; // dense-output slot n: [u_n, k_2..k_7] (record)
+};
+struct Tsit5PostArgs {
+    double tf, dtmin, beta1, beta2, gamma, qmin, qmax, qoldinit;
+    int32_t adaptive, record;
+    int64_t maxiters, n_save, slot_cap;
+    const double* saveat;
+    double* ts_rec;
+    double* dts_rec;
+};
+template <typename T>
+hipError_t launch_tsit5_post(const SolveCtl* cin, SolveCtl* cout, const double* sumsq, const Tsit5Bufs<T>& bf,
+                             const Tsit5PostArgs& pa, int64_t n, hipStream_t st);
 
 // surrogate shapes (kan_wide.hip)
 constexpr int kWideKT = 8;       // column tile of the wide-out kernels

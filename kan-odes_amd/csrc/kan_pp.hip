@@ -563,6 +563,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
+    if (STG && stage_skip(sl.skip)) return;
     const int tsz = (kPPCoef / 2) * ni;   // double2 per table
     for (int i = threadIdx.x; i < tsz; i += kBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
@@ -583,6 +584,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     }
     double dW = 0.0;
     const bool want_err = STG && err_slab != nullptr;
+    const double suc = STG ? stage_scale(su.cscale) : 1.0, slc = STG ? stage_scale(sl.cscale) : 1.0;
     double eacc = 0.0;
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t rstride = (int64_t)gridDim.x * (kVjpBlock / kWave);
@@ -603,7 +605,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
 #pragma unroll
             for (int j = 0; j < kMaxStages; ++j) {
                 if (j < su.nk) {
-                    const double cj = su.c[j];
+                    const double cj = su.c[j] * suc;
 #pragma unroll
                     for (int k = 0; k < NP; ++k) {
                         const kd2 kj = ld_stream(su.k[j] + rb + 128 * k);
@@ -615,7 +617,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
 #pragma unroll
             for (int j = 0; j < kMaxStages; ++j) {
                 if (j < sl.nk) {
-                    const double cj = sl.c[j], ej = sl.ec[j];
+                    const double cj = sl.c[j] * slc, ej = sl.ec[j] * slc;
 #pragma unroll
                     for (int k = 0; k < NP; ++k) {
                         const kd2 kj = ld_stream(sl.k[j] + rb + 128 * k);
@@ -675,7 +677,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             o.y = a1 + x1b;
             st_stream(lamJ + rb + 128 * k, o);
             if (want_err) {
-                const double en = sl.ec[sl.nk];
+                const double en = sl.ec[sl.nk] * slc;
                 const double ex = ::fma(en, o.x, ek.x), ey = ::fma(en, o.y, ek.y);
                 const double sx = ::fma(sl.reltol, fmax(kabs(l0k.x), kabs(lk.x)), sl.abstol);
                 const double sy = ::fma(sl.reltol, fmax(kabs(l0k.y), kabs(lk.y)), sl.abstol);
@@ -741,12 +743,14 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[kBlock / kWave];
+    if (stage_skip(sa.skip)) return;
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
     const int lane = threadIdx.x & (kWave - 1);
     const bool want_err = err_slab != nullptr;
+    const double sac = stage_scale(sa.cscale);
     const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
     double eacc = 0.0;
     for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
@@ -761,7 +765,7 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j) {
             if (j < sa.nk) {
-                const double cj = sa.c[j], ej = sa.ec[j];
+                const double cj = sa.c[j] * sac, ej = sa.ec[j] * sac;
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
                     const kd2 kj = ld_stream(sa.k[j] + rb + 128 * k);
@@ -801,7 +805,7 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             st_stream(du + b * Nx + i, o);
             if (y_out) st_stream(y_out + b * Nx + i, y[k]);
             if (want_err) {
-                const double en = sa.ec[sa.nk];
+                const double en = sa.ec[sa.nk] * sac;
                 const double ex = ::fma(en, o.x, e[k].x), ey = ::fma(en, o.y, e[k].y);
                 const double sx = ::fma(sa.reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), sa.abstol);
                 const double sy = ::fma(sa.reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), sa.abstol);

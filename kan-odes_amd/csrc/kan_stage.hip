@@ -16,11 +16,13 @@ namespace kan {
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
 stage_lincomb_kernel(const T* __restrict__ u, StageArgs<T> sa, T* __restrict__ y, int64_t n) {
+    if (stage_skip(sa.skip)) return;
+    const double sc = stage_scale(sa.cscale);
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         T v = u[i];
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j)
-            if (j < sa.nk) v = kfma<T>((T)sa.c[j], sa.k[j][i], v);
+            if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), sa.k[j][i], v);
         y[i] = v;
     }
 }
@@ -31,13 +33,15 @@ __global__ void __launch_bounds__(kBlock)
 stage_error_kernel(const T* __restrict__ u, const T* __restrict__ y, const T* __restrict__ du, StageArgs<T> sa,
                    double* __restrict__ slab, int64_t n) {
     __shared__ double red[kBlock / kWave];
+    if (stage_skip(sa.skip)) return;
+    const double sc = stage_scale(sa.cscale);
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
         double e = 0.0;
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j)
-            if (j < sa.nk) e = ::fma(sa.ec[j], (double)sa.k[j][i], e);
-        e = ::fma(sa.ec[sa.nk], (double)du[i], e);
+            if (j < sa.nk) e = ::fma(sa.ec[j] * sc, (double)sa.k[j][i], e);
+        e = ::fma(sa.ec[sa.nk] * sc, (double)du[i], e);
         const double sk = ::fma(sa.reltol, fmax(kabs((double)u[i]), kabs((double)y[i])), sa.abstol);
         const double r = e / sk;
         acc = ::fma(r, r, acc);

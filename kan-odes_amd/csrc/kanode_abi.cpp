@@ -55,6 +55,8 @@ struct kanode_handle {
     kan::PPConst* dpc = nullptr;
     double* dtable = nullptr;
     bool pp_on = false;
+    // the integrator's storage for solves without a dense output (kanode_solve.cpp)
+    kanode_solution* solve_cache = nullptr;
     // table reuse inside one integrator solve (p constant): build each table set once
     bool hold_tables = false;
     bool built_phi = false, built_vjp = false;
@@ -418,7 +420,7 @@ kanode_status ensure_stage_ws(kanode_handle* h, size_t need, hipStream_t st);
 
 template <typename T>
 kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* sg, T* du, int64_t B,
-                      hipStream_t st) {
+                      hipStream_t st, const double* cscale = nullptr, const int32_t* skip = nullptr) {
     if (sg->n_prev < 0 || sg->n_prev > KANODE_MAX_STAGES)
         return fail(h, KANODE_ERR_INVALID_ARG, "n_prev must be in [0, KANODE_MAX_STAGES]");
     if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "stage needs an RHS with N_in == N_out");
@@ -433,6 +435,8 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
     for (int j = 0; j <= sg->n_prev; ++j) sa.ec[j] = sg->want_error ? sg->ec[j] : 0.0;
     sa.abstol = sg->abstol;
     sa.reltol = sg->reltol;
+    sa.cscale = cscale;
+    sa.skip = skip;
     double* err_out = sg->want_error ? (double*)sg->error_sumsq : nullptr;
     if constexpr (std::is_same<T, double>::value) {
         if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on &&
@@ -492,7 +496,8 @@ kanode_status stage_args(kanode_handle* h, const kanode_stage* sg, kan::StageArg
 
 template <typename T>
 kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* state, const T* lam,
-                          const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st, bool dp_assign = false) {
+                          const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st, bool dp_assign = false,
+                          const double* su_scale = nullptr, const double* sl_scale = nullptr) {
     if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "adjoint stage needs an RHS with N_in == N_out");
     if (adj->want_error && !adj->error_sumsq) return fail(h, KANODE_ERR_INVALID_ARG, "want_error needs error_sumsq");
     kan::StageArgs<T> su, sl;
@@ -500,6 +505,8 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
     if (s != KANODE_OK) return s;
     s = stage_args<T>(h, adj, sl);
     if (s != KANODE_OK) return s;
+    su.cscale = su_scale;
+    sl.cscale = sl_scale;
     const int64_t n = h->n_in * B;
     if constexpr (std::is_same<T, double>::value) {
         // Fisher-KPP table path: the whole adjoint stage in one streaming kernel + one reduction
@@ -643,6 +650,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->dpc) (void)hipFree(h->dpc);
     if (h->stage_ws) (void)hipFree(h->stage_ws);
     if (h->dtable) (void)hipFree(h->dtable);
+    if (h->solve_cache) kanode_solution_free(h->solve_cache);
     delete h;
 }
 
@@ -873,18 +881,46 @@ void kanode_internal_hold_tables(kanode_handle* h, bool on) {
     h->built_phi = h->built_vjp = false;
 }
 double* kanode_internal_scratch(kanode_handle* h) { return (double*)h->slab; }
+void* kanode_internal_solution_cache(kanode_handle* h) { return &h->solve_cache; }
 int kanode_internal_scratch_rows(const kanode_handle*) { return kSlabBlocks; }
 kanode_status kanode_internal_check(kanode_handle* h) { return check_handle(h); }
 kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
                                         const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
-                                        int64_t batch, void* stream) {
+                                        int64_t batch, void* stream, const double* su_scale, const double* sl_scale) {
     kanode_status s = check_handle(h);
     if (s != KANODE_OK) return s;
     if (!p || !u || !lam || !state || !adj || batch < 1) return fail(h, KANODE_ERR_INVALID_ARG, "null argument or batch < 1");
     hipStream_t st = (hipStream_t)stream;
     if (h->spec.dtype == KANODE_F64)
         return vjp_stage_t<double>(h, (const double*)p, (const double*)u, state, (const double*)lam, adj, (double*)lamJ,
-                                   (double*)dp, batch, st, dp_assign);
+                                   (double*)dp, batch, st, dp_assign, su_scale, sl_scale);
     return vjp_stage_t<float>(h, (const float*)p, (const float*)u, state, (const float*)lam, adj, (float*)lamJ,
-                              (float*)dp, batch, st, dp_assign);
+                              (float*)dp, batch, st, dp_assign, su_scale, sl_scale);
+}
+
+kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,
+                                        void* du, int64_t batch, void* stream, const double* cscale,
+                                        const int32_t* skip) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (!p || !u || !du || !sg || batch < 1) return fail(h, KANODE_ERR_INVALID_ARG, "null argument or batch < 1");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->spec.dtype == KANODE_F64)
+        return stage_t<double>(h, (const double*)p, (const double*)u, sg, (double*)du, batch, st, cscale, skip);
+    return stage_t<float>(h, (const float*)p, (const float*)u, sg, (float*)du, batch, st, cscale, skip);
+}
+
+// every workspace a stage / adjoint-stage call of this batch may need, allocated now
+// (so the calls can be captured into a hipGraph)
+kanode_status kanode_internal_prepare(kanode_handle* h, int64_t batch, hipStream_t st) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if ((s = ensure_ws(h, batch, st)) != KANODE_OK) return s;
+    if (h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->ws_bytes < (size_t)(h->spec.nx * batch) * h->esize) {
+        HIP_TRY(h, hipStreamSynchronize(st));
+        if (h->ws) HIP_TRY(h, hipFree(h->ws));
+        HIP_TRY(h, hipMalloc(&h->ws, (size_t)(h->spec.nx * batch) * h->esize));
+        h->ws_bytes = (size_t)(h->spec.nx * batch) * h->esize;
+    }
+    return ensure_stage_ws(h, 2 * (size_t)(h->n_in * batch) * h->esize, st);
 }

@@ -6,6 +6,8 @@
 
 #include <string>
 
+#include <hip/hip_runtime.h>
+
 #include "kanode.h"
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -19,6 +21,18 @@ void kanode_internal_hold_tables(kanode_handle* h, bool on);
 double* kanode_internal_scratch(kanode_handle* h);
 int kanode_internal_scratch_rows(const kanode_handle* h);
 // kanode_vjp_stage with dp either accumulated (+=, the C-ABI semantics) or assigned (dp_assign)
+// su_scale / sl_scale (nullable, device): the state / adjoint stage coefficients are multiplied
+// by *scale in the kernels (device-resident step sizes)
 kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
                                         const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
-                                        int64_t batch, void* stream);
+                                        int64_t batch, void* stream, const double* su_scale = nullptr,
+                                        const double* sl_scale = nullptr);
+// kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;
+// while *skip != 0 (device, nullable) the stage kernels return at once (a finished graph-mode solve)
+kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,
+                                        void* du, int64_t batch, void* stream, const double* cscale,
+                                        const int32_t* skip = nullptr);
+// allocate every workspace the stage calls of this batch use (before hipGraph capture)
+kanode_status kanode_internal_prepare(kanode_handle* h, int64_t batch, hipStream_t st);
+// address of the handle's kanode_solution* slot for solves without a dense output (freed by kanode_destroy)
+void* kanode_internal_solution_cache(kanode_handle* h);

@@ -77,6 +77,8 @@ extern "C" void kanode_solver_options_default(kanode_solver_options* o) {
     o->qmin = 0.2;
     o->qmax = 10.0;
     o->qoldinit = 1e-4;
+    o->control = 0;
+    o->graph_steps = 16;
 }
 
 // Dense output: step n keeps u_n and k_2..k_7 in slot n (7 states); k_1 of step n is
@@ -99,6 +101,31 @@ struct kanode_solution {
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
+    // device step control (graph mode): U, K_1..K_7, U_new; control blocks; saveat staging;
+    // the dense-output slot table and step times as the device writes them; the cached graph
+    struct Graph {
+        void* bufs = nullptr;
+        size_t bufs_bytes = 0;
+        kan::SolveCtl* ctl = nullptr;      // [2], parity-buffered
+        kan::SolveCtl* hctl = nullptr;     // pinned mirror
+        double* saveat = nullptr;
+        int64_t saveat_cap = 0;
+        void* save = nullptr;
+        size_t save_bytes = 0;
+        void** slots = nullptr;            // device copy of the slot pointers
+        double* ts = nullptr;
+        double* dts = nullptr;
+        int64_t cap = 0;                   // capacity of slots / ts / dts
+        int64_t slots_synced = 0;
+        hipStream_t cap_stream = nullptr;
+        hipGraphExec_t exec = nullptr;
+        // what the graph baked in
+        const void* key_p = nullptr;
+        int64_t key_nsave = -1, key_cap = -1;
+        int key_record = -1, key_steps = -1;
+        double key_tf = 0;
+        kanode_solver_options key_opt{};
+    } g;
 
     ~kanode_solution() {
         for (void* s : slots) (void)hipFree(s);
@@ -106,6 +133,11 @@ struct kanode_solution {
         if (dscal) (void)hipFree(dscal);
         if (hscal) (void)hipHostFree(hscal);
         if (adj) (void)hipFree(adj);
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        if (g.cap_stream) (void)hipStreamDestroy(g.cap_stream);
+        for (void* p : {(void*)g.bufs, (void*)g.ctl, (void*)g.saveat, g.save, (void*)g.slots, (void*)g.ts, (void*)g.dts})
+            if (p) (void)hipFree(p);
+        if (g.hctl) (void)hipHostFree(g.hctl);
     }
     size_t state_bytes() const { return (size_t)n * esize; }
     char* slot(int64_t i) const { return (char*)slots[record ? i : (i & 1)]; }
@@ -211,10 +243,9 @@ struct TableHold {   // p is constant for one solve: each table set is built onc
 // Hairer & Wanner initial step (OrdinaryDiffEq ode_determine_initdt, order 5); kanode/ode.py _initdt
 template <typename T>
 kanode_status initdt(kanode_handle* h, kanode_solution* s, const void* p, const void* u0, const void* f0,
-                     double tdist, const kanode_solver_options& o, double& dt, hipStream_t st) {
+                     double tdist, const kanode_solver_options& o, double& dt, hipStream_t st, void* tmp) {
     const double one = 1.0;
     double e1[2] = {1.0, 0.0};
-    void* tmp = s->k(0, 2);   // scratch: the k_2 buffer of step 0
     SOLVE_TRY(wsumsq<T>(h, u0, u0, 0, nullptr, &one, u0, o.abstol, o.reltol, s->n, s->dscal + 0, st));
     SOLVE_TRY(wsumsq<T>(h, u0, u0, 0, nullptr, &one, f0, o.abstol, o.reltol, s->n, s->dscal + 1, st));
     SOLVE_TRY(read_scalars(h, s, 2, st));
@@ -261,7 +292,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
     kanode_stage s0{};
     SOLVE_TRY(kanode_rhs_stage(h, p, s->u(0), &s0, s->k1_0, s->batch, st));   // k1 = f(u0)
     double dt = o.dt;
-    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st));
+    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st, s->k(0, 2)));
     double qold = o.qoldinit;
     double t = t0;
     int64_t step = 0, naccept = 0, nreject = 0, nf = 0;
@@ -332,6 +363,240 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         stats->naccept = naccept;
         stats->nreject = nreject;
         stats->nf = nf + 1;
+    }
+    return KANODE_OK;
+}
+
+// ---- device step control: the solve as a replayed hipGraph ------------------------------
+kanode_status dev_alloc(kanode_handle* h, void** p, size_t bytes, const char* what) {
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return kanode_internal_fail(h, KANODE_ERR_ALLOC, std::string("device control: out of device memory (") + what + ")");
+    }
+    return KANODE_OK;
+}
+
+bool same_opts(const kanode_solver_options& a, const kanode_solver_options& b) {
+    return a.abstol == b.abstol && a.reltol == b.reltol && a.adaptive == b.adaptive && a.maxiters == b.maxiters &&
+           a.dtmin == b.dtmin && a.beta1 == b.beta1 && a.beta2 == b.beta2 && a.gamma == b.gamma && a.qmin == b.qmin &&
+           a.qmax == b.qmax && a.qoldinit == b.qoldinit;
+}
+
+template <typename T>
+kan::Tsit5Bufs<T> graph_bufs(kanode_solution* s) {
+    kan::Tsit5Bufs<T> bf{};
+    char* b = (char*)s->g.bufs;
+    const size_t sb = s->state_bytes();
+    bf.U = (T*)b;
+    for (int j = 0; j < 7; ++j) bf.K[j] = (T*)(b + (1 + j) * sb);
+    bf.UNEW = (const T*)(b + 8 * sb);
+    bf.save = (T*)s->g.save;
+    bf.slots = s->g.slots;
+    return bf;
+}
+
+// Capture `steps` step slots (six stage launches + tsit5_post_kernel each) into a graph.
+template <typename T>
+kanode_status build_graph(kanode_handle* h, kanode_solution* s, const void* p, double tf, int64_t n_save,
+                          const kanode_solver_options& o, int steps) {
+    auto& g = s->g;
+    if (g.exec) {
+        (void)hipGraphExecDestroy(g.exec);
+        g.exec = nullptr;
+    }
+    if (!g.cap_stream) SOLVE_HIP(h, hipStreamCreateWithFlags(&g.cap_stream, hipStreamNonBlocking));
+    const kan::Tsit5Bufs<T> bf = graph_bufs<T>(s);
+    kan::Tsit5PostArgs pa{};
+    pa.tf = tf;
+    pa.dtmin = o.dtmin;
+    pa.beta1 = o.beta1;
+    pa.beta2 = o.beta2;
+    pa.gamma = o.gamma;
+    pa.qmin = o.qmin;
+    pa.qmax = o.qmax;
+    pa.qoldinit = o.qoldinit;
+    pa.adaptive = o.adaptive;
+    pa.record = s->record;
+    pa.maxiters = o.maxiters;
+    pa.n_save = n_save;
+    pa.slot_cap = g.cap;
+    pa.saveat = g.saveat;
+    pa.ts_rec = g.ts;
+    pa.dts_rec = g.dts;
+    kanode_internal_hold_tables(h, true);   // the first captured stage rebuilds the tables on every replay
+    SOLVE_HIP(h, hipStreamBeginCapture(g.cap_stream, hipStreamCaptureModeRelaxed));
+    kanode_status r = KANODE_OK;
+    for (int sl = 0; sl < steps && r == KANODE_OK; ++sl) {
+        kan::SolveCtl* cin = g.ctl + (sl & 1);
+        kan::SolveCtl* cout = g.ctl + ((sl + 1) & 1);
+        void* ks[7];
+        for (int j = 0; j < 7; ++j) ks[j] = bf.K[j];
+        for (int i = 0; i < 6 && r == KANODE_OK; ++i) {
+            kanode_stage sg = make_stage(i + 1, ks, TA[i]);
+            if (i == 5) {
+                sg.y_out = (void*)bf.UNEW;
+                if (o.adaptive) {
+                    sg.want_error = 1;
+                    for (int j = 0; j < 7; ++j) sg.ec[j] = BT[j];
+                    sg.abstol = o.abstol;
+                    sg.reltol = o.reltol;
+                    sg.error_sumsq = s->dscal;
+                }
+            }
+            r = kanode_internal_rhs_stage(h, p, bf.U, &sg, ks[i + 1], s->batch, g.cap_stream, &cin->dt, &cin->done);
+        }
+        if (r == KANODE_OK) {
+            const hipError_t e = kan::launch_tsit5_post<T>(cin, cout, s->dscal, bf, pa, s->n, g.cap_stream);
+            if (e != hipSuccess) r = kanode_internal_fail(h, KANODE_ERR_HIP, std::string("tsit5_post: ") + hipGetErrorString(e));
+        }
+    }
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(g.cap_stream, &graph);
+    if (r != KANODE_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return r;
+    }
+    if (ec != hipSuccess) return kanode_internal_fail(h, KANODE_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+        g.exec = nullptr;
+        return kanode_internal_fail(h, KANODE_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    }
+    g.key_p = p;
+    g.key_nsave = n_save;
+    g.key_cap = g.cap;
+    g.key_record = s->record;
+    g.key_steps = steps;
+    g.key_tf = tf;
+    g.key_opt = o;
+    return KANODE_OK;
+}
+
+// dense-output capacity for `need` accepted steps: slots (host + device pointer table) and the
+// device step-time records; growing the tables invalidates the graph
+kanode_status graph_capacity(kanode_handle* h, kanode_solution* s, int64_t need, hipStream_t st) {
+    auto& g = s->g;
+    if (s->record) SOLVE_TRY(ensure_slots(h, s, need, st));
+    if (need > g.cap) {
+        int64_t cap = std::max<int64_t>(64, g.cap);
+        while (cap < need) cap *= 2;
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        void *nslots = nullptr, *nts = nullptr, *ndts = nullptr;
+        SOLVE_TRY(dev_alloc(h, &nslots, cap * sizeof(void*), "slot table"));
+        SOLVE_TRY(dev_alloc(h, &nts, cap * sizeof(double), "step times"));
+        SOLVE_TRY(dev_alloc(h, &ndts, cap * sizeof(double), "step sizes"));
+        if (g.cap > 0) {
+            SOLVE_HIP(h, hipMemcpy(nts, g.ts, g.cap * sizeof(double), hipMemcpyDeviceToDevice));
+            SOLVE_HIP(h, hipMemcpy(ndts, g.dts, g.cap * sizeof(double), hipMemcpyDeviceToDevice));
+        }
+        for (void* q : {(void*)g.slots, (void*)g.ts, (void*)g.dts})
+            if (q) (void)hipFree(q);
+        g.slots = (void**)nslots;
+        g.ts = (double*)nts;
+        g.dts = (double*)ndts;
+        g.cap = cap;
+        g.slots_synced = 0;
+    }
+    if (s->record && g.slots_synced < (int64_t)s->slots.size()) {
+        const int64_t a = g.slots_synced, b = std::min<int64_t>((int64_t)s->slots.size(), g.cap);
+        SOLVE_HIP(h, hipMemcpy(g.slots + a, s->slots.data() + a, (b - a) * sizeof(void*), hipMemcpyHostToDevice));
+        g.slots_synced = b;
+    }
+    return KANODE_OK;
+}
+
+template <typename T>
+kanode_status solve_graph_t(kanode_handle* h, const void* p, const void* u0, double t0, double tf,
+                            const double* saveat, int64_t n_save, void* u_save, const kanode_solver_options& o,
+                            kanode_solution* s, kanode_solve_stats* stats, hipStream_t st) {
+    auto& g = s->g;
+    const size_t sb = s->state_bytes();
+    const int steps = o.graph_steps > 0 ? (o.graph_steps + 1) / 2 * 2 : 16;
+    if (g.bufs_bytes < 9 * sb) {
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        if (g.bufs) (void)hipFree(g.bufs);
+        g.bufs = nullptr;
+        g.bufs_bytes = 0;
+        SOLVE_TRY(dev_alloc(h, &g.bufs, 9 * sb, "stage vectors"));
+        g.bufs_bytes = 9 * sb;
+        if (g.exec) {
+            (void)hipGraphExecDestroy(g.exec);
+            g.exec = nullptr;
+        }
+    }
+    if (!g.ctl) {
+        SOLVE_TRY(dev_alloc(h, (void**)&g.ctl, 2 * sizeof(kan::SolveCtl), "control"));
+        SOLVE_HIP(h, hipHostMalloc((void**)&g.hctl, sizeof(kan::SolveCtl)));
+    }
+    if (g.saveat_cap < std::max<int64_t>(n_save, 1) || g.save_bytes < (size_t)n_save * sb) {
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        if (g.saveat) (void)hipFree(g.saveat);
+        if (g.save) (void)hipFree(g.save);
+        g.saveat = nullptr;
+        g.save = nullptr;
+        SOLVE_TRY(dev_alloc(h, (void**)&g.saveat, std::max<int64_t>(n_save, 1) * sizeof(double), "saveat"));
+        SOLVE_TRY(dev_alloc(h, &g.save, std::max<size_t>((size_t)n_save * sb, 1), "saveat values"));
+        g.saveat_cap = std::max<int64_t>(n_save, 1);
+        g.save_bytes = (size_t)n_save * sb;
+        if (g.exec) {
+            (void)hipGraphExecDestroy(g.exec);
+            g.exec = nullptr;
+        }
+    }
+    SOLVE_TRY(kanode_internal_prepare(h, s->batch, st));
+    const kan::Tsit5Bufs<T> bf = graph_bufs<T>(s);
+    int64_t si = 0;
+    while (si < n_save && saveat[si] <= t0 + 1e-14 * std::max(1.0, std::fabs(t0))) {
+        SOLVE_HIP(h, hipMemcpyAsync((char*)g.save + si * sb, u0, sb, hipMemcpyDeviceToDevice, st));
+        ++si;
+    }
+    if (n_save > 0) SOLVE_HIP(h, hipMemcpyAsync(g.saveat, saveat, n_save * sizeof(double), hipMemcpyHostToDevice, st));
+    SOLVE_HIP(h, hipMemcpyAsync(bf.U, u0, sb, hipMemcpyDeviceToDevice, st));
+    kanode_stage s0{};
+    SOLVE_TRY(kanode_rhs_stage(h, p, bf.U, &s0, bf.K[0], s->batch, st));   // k1 = f(u0)
+    if (s->record) {
+        SOLVE_TRY(ensure_slots(h, s, 1, st));
+        SOLVE_HIP(h, hipMemcpyAsync(s->k1_0, bf.K[0], sb, hipMemcpyDeviceToDevice, st));
+    }
+    double dt = o.dt;
+    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, bf.U, bf.K[0], tf - t0, o, dt, st, bf.K[1]));
+    kan::SolveCtl c0{};
+    c0.t = t0;
+    c0.dt = std::min(dt, tf - t0);
+    c0.qold = o.qoldinit;
+    c0.si = si;
+    c0.done = t0 >= tf - 1e-14 * std::max(1.0, std::fabs(tf)) ? 1 : 0;
+    SOLVE_HIP(h, hipStreamSynchronize(st));   // the pinned control block is rewritten below
+    *g.hctl = c0;
+    SOLVE_HIP(h, hipMemcpyAsync(g.ctl, g.hctl, sizeof(c0), hipMemcpyHostToDevice, st));
+    int64_t naccept = 0;
+    for (;;) {
+        SOLVE_TRY(graph_capacity(h, s, naccept + steps + 1, st));
+        if (!g.exec || g.key_p != p || g.key_nsave != n_save || g.key_cap != g.cap || g.key_record != (int)s->record ||
+            g.key_steps != steps || g.key_tf != tf || !same_opts(g.key_opt, o))
+            SOLVE_TRY(build_graph<T>(h, s, p, tf, n_save, o, steps));
+        SOLVE_HIP(h, hipGraphLaunch(g.exec, st));
+        SOLVE_HIP(h, hipMemcpyAsync(g.hctl, g.ctl, sizeof(kan::SolveCtl), hipMemcpyDeviceToHost, st));
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        naccept = g.hctl->naccept;
+        if (g.hctl->done) break;
+    }
+    const kan::SolveCtl c = *g.hctl;
+    if (c.status == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
+    if (c.status != 0) return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device control): dense-output storage full");
+    if (s->record && c.naccept > 0) {
+        s->ts.resize(c.naccept);
+        s->dts.resize(c.naccept);
+        SOLVE_HIP(h, hipMemcpy(s->ts.data(), g.ts, c.naccept * sizeof(double), hipMemcpyDeviceToHost));
+        SOLVE_HIP(h, hipMemcpy(s->dts.data(), g.dts, c.naccept * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (n_save > 0) SOLVE_HIP(h, hipMemcpyAsync(u_save, g.save, n_save * sb, hipMemcpyDeviceToDevice, st));
+    if (stats) {
+        stats->naccept = c.naccept;
+        stats->nreject = c.nreject;
+        stats->nf = 6 * c.attempts + 1;
     }
     return KANODE_OK;
 }
@@ -539,6 +804,8 @@ kanode_status check_opts(kanode_handle* h, const kanode_solver_options& o) {
     if (!(o.abstol >= 0) || !(o.reltol >= 0) || o.maxiters < 1 || !(o.qmin > 0) || !(o.qmax > 0) || !(o.gamma > 0))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solver options out of range");
     if (!o.adaptive && !(o.dt > 0)) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step Tsit5 needs dt > 0");
+    if (o.control < 0 || o.control > 2 || o.graph_steps < 0)
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "control must be 0 (auto), 1 (host) or 2 (device)");
     return KANODE_OK;
 }
 
@@ -560,13 +827,17 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
     hipStream_t st = (hipStream_t)stream;
     const int dtype = kanode_internal_dtype(h);
     const int64_t n = kanode_internal_state_length(h) * batch;
-    kanode_solution* s = dense ? *dense : nullptr;
-    if (s && (s->h != h || s->n != n || s->dtype != dtype || s->record != (dense != nullptr))) {
+    // without a dense output the handle keeps the solve's storage (and any cached graph) for the next call
+    const bool record = dense != nullptr;
+    kanode_solution** slot = record ? dense : (kanode_solution**)kanode_internal_solution_cache(h);
+    kanode_solution* s = *slot;
+    if (s && (s->h != h || s->n != n || s->dtype != dtype || s->record != record)) {
         // storage of another shape: start over
         if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "dense output of another shape");
         SOLVE_HIP(h, hipStreamSynchronize(st));
         delete s;
         s = nullptr;
+        *slot = nullptr;
     }
     if (!s) {
         if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "solve allocates its dense output");
@@ -576,7 +847,7 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         s->dtype = dtype;
         s->esize = dtype == KANODE_F64 ? 8 : 4;
         s->n = n;
-        s->record = dense != nullptr;
+        s->record = record;
         if (hipMalloc(&s->k1_0, s->state_bytes()) != hipSuccess || hipMalloc(&s->dscal, 8 * sizeof(double)) != hipSuccess ||
             hipHostMalloc((void**)&s->hscal, 8 * sizeof(double)) != hipSuccess) {
             (void)hipGetLastError();
@@ -593,14 +864,26 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
     kanode_status r;
     {
         TableHold hold(h);
-        r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
-                                : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
+        // auto = host: a replayed graph node costs the GPU what an eager launch does (ROCm 7.2,
+        // tools/solve_modes.py), so device control only wins where the per-step norm read is a
+        // large part of a step (adaptive, small states); it is opt-in
+        const bool dev = o.control == 2;
+        if (dev && capturing(st)) {
+            r = kanode_internal_fail(h, KANODE_ERR_CAPTURE, "device step control cannot run inside a capture");
+        } else if (dev) {
+            r = dtype == KANODE_F64 ? solve_graph_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
+                                    : solve_graph_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
+        } else {
+            r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
+                                    : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
+        }
     }
-    if (dense) {
-        *dense = s;
+    if (record || s->state_bytes() <= (size_t)64 << 20) {
+        *slot = s;   // kept for the next solve (a large scratch solve gives its memory back)
     } else {
-        if (hipStreamSynchronize(st) != hipSuccess) (void)hipGetLastError();   // scratch freed below
+        if (hipStreamSynchronize(st) != hipSuccess) (void)hipGetLastError();
         delete s;
+        *slot = nullptr;
     }
     return r;
 }

@@ -69,6 +69,7 @@ class SolverOptsC(C.Structure):
         ("abstol", C.c_double), ("reltol", C.c_double), ("dt", C.c_double), ("adaptive", C.c_int32),
         ("maxiters", C.c_int64), ("dtmin", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double),
         ("gamma", C.c_double), ("qmin", C.c_double), ("qmax", C.c_double), ("qoldinit", C.c_double),
+        ("control", C.c_int32), ("graph_steps", C.c_int32),
     ]
 
 

@@ -88,6 +88,8 @@ class Tsit5Options:
     qoldinit: float = 1e-4
     fused: bool = True                 # use f.stage (kanode_rhs_stage) when the RHS has one
     native: bool = True                # run the loop in libkanode (kanode_solve_tsit5) when f is a kanode RHS
+    control: str = "auto"              # native step control: "host", "device" (hipGraph replay) or "auto"
+    graph_steps: int = 16              # step slots per graph replay (device control)
 
     def to_c(self):
         from . import _lib as L
@@ -99,6 +101,8 @@ class Tsit5Options:
         o.maxiters, o.dtmin = int(self.maxiters), float(self.dtmin)
         o.beta1, o.beta2, o.gamma = float(self.beta1), float(self.beta2), float(self.gamma)
         o.qmin, o.qmax, o.qoldinit = float(self.qmin), float(self.qmax), float(self.qoldinit)
+        o.control = {"auto": 0, "host": 1, "device": 2}[self.control]
+        o.graph_steps = int(self.graph_steps)
         return o
 
 
