@@ -28,9 +28,9 @@ for w in fk_rhs fk_rhs_rec fk_vjp; do
   for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_LDS"; do
     n=$(echo $c | cut -d' ' -f1)
     timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d $OUT/pmc_${w}_$n -o run --output-format csv -- \
-      python3 tools/prof_kernel.py --what $w --reps 5 > $OUT/pmc_${w}_$n.log 2>&1 || { echo "pmc $w $n failed"; tail -5 $OUT/pmc_${w}_$n.log; exit 3; }
+      python3 tools/prof_kernel.py --what $w --reps 5 --batch ${BATCH:-1048576} > $OUT/pmc_${w}_$n.log 2>&1 || { echo "pmc $w $n failed"; tail -5 $OUT/pmc_${w}_$n.log; exit 3; }
   done
 done
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
-python3 tools/traffic.py $OUT > $OUT/traffic.json
+BATCH=${BATCH:-1048576} python3 tools/traffic.py $OUT > $OUT/traffic.json
 cat $OUT/pmc_summary.txt $OUT/traffic.json

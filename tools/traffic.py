@@ -34,7 +34,7 @@ for w, kern, key, words in PASSES:
     write = mean_counter(wr[0], kern, "WRITE_SIZE")
     if fetch is None or write is None:
         continue
-    batch = 131072
+    batch = int(os.environ.get("BATCH", "131072"))
     alg = 8.0 * (11 + batch * words)
     hbm = (2.0 * fetch + write) * 1024.0
     out[key] = {
