@@ -121,7 +121,8 @@ constexpr int kChainDim = 16;    // lanes per column = max layer width
 template <typename T, int NORM, int PATH>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
-                    const T* __restrict__ x, T* __restrict__ y, int64_t K) {
+                    const T* __restrict__ x, T* __restrict__ y, int64_t K, StageArgs<T> sa, T* __restrict__ y_out,
+                    double* __restrict__ err_slab, double* __restrict__ err_direct) {
     extern __shared__ __attribute__((aligned(16))) unsigned char chain_raw[];
     LayerConst* lcl = reinterpret_cast<LayerConst*>(chain_raw);
     T* ps = reinterpret_cast<T*>(chain_raw + nl * sizeof(LayerConst));
@@ -136,9 +137,29 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
     const Math<T> M{tab};
     const int I0 = lcl[0].I, OL = lcl[nl - 1].O;
     const int j = threadIdx.x & (kChainDim - 1);
+    // Runge-Kutta stage (kanode_rhs_stage): input y = x + Σ sa.c k formed here, optional y_out and
+    // the embedded-error partial Σ (e/sk)² (block total -> err_slab[block], or err_direct with one block)
+    const double sc = stage_scale(sa.cscale);
+    const bool want_err = err_slab != nullptr || err_direct != nullptr;
+    double eacc = 0.0;
     const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kChainDim;
     for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kChainDim; k < K; k += stride) {
-        T a = j < I0 ? x[(int64_t)I0 * k + j] : T(0);
+        const int64_t idx = (int64_t)I0 * k + j;
+        T a = T(0), x0 = T(0);
+        double ev = 0.0;
+        if (j < I0) {
+            a = x0 = x[idx];
+#pragma unroll
+            for (int m = 0; m < kMaxStages; ++m) {
+                if (m < sa.nk) {
+                    const T km = sa.k[m][idx];
+                    a = kfma<T>((T)(sa.c[m] * sc), km, a);
+                    if (want_err) ev = ::fma(sa.ec[m] * sc, (double)km, ev);
+                }
+            }
+            if (y_out) y_out[idx] = a;
+        }
+        const T yin = a;
         for (int l = 0; l < nl; ++l) {
             const LayerConst& lc = lcl[l];
             const int I = lc.I, O = lc.O, G = lc.G;
@@ -181,7 +202,236 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
             }
             a = out;
         }
-        if (j < OL) y[(int64_t)OL * k + j] = a;
+        if (j < OL) {
+            y[(int64_t)OL * k + j] = a;
+            if (want_err) {
+                const double e = ::fma(sa.ec[sa.nk] * sc, (double)a, ev);
+                const double sk = ::fma(sa.reltol, fmax(kabs((double)x0), kabs((double)yin)), sa.abstol);
+                const double r = e / sk;
+                eacc = ::fma(r, r, eacc);
+            }
+        }
+    }
+    if (want_err) {
+        __shared__ double red[kChainBlock / kWave];
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_direct ? err_direct : err_slab + blockIdx.x);
+    }
+}
+
+// The adjoint stage of a small chain in one launch (kanode_vjp_stage for the LV [2,10,2]
+// shape): 16 lanes per column as in kd_chain_col_kernel.  Lane j forms the forward dense output
+// y_j = u_j + Σ su.c k_j and the adjoint stage input λs_j = λ_j + Σ sl.c lk_j, the forward pass
+// keeps each layer's input activation in registers, and the backward pass walks the layers in
+// reverse: the group broadcasts ȳ_o, lane i (input i) forms x̄_i exactly as kd_vjp_col_kernel
+// does and adds ȳ_o φ_g(x_i), ȳ_o swish(x_i) into its own entries of the group's LDS gradient
+// row (disjoint per lane, so no atomics).  The block sums its group rows in a fixed order into
+// its slab row; chain_vjp_finish_kernel reduces the slab rows (dp) and the λ error partials.
+constexpr int kChainVjpBlock = 64;               // 4 columns per block
+constexpr int kChainMaxLayers = 4;
+template <typename T, int NORM, int PATH>
+__global__ void __launch_bounds__(kChainVjpBlock)
+kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
+                          const T* __restrict__ u, StageArgs<T> su, const T* __restrict__ lam, StageArgs<T> sl,
+                          T* __restrict__ lam_out, T* __restrict__ lamJ, T* __restrict__ slab,
+                          double* __restrict__ err_slab, int64_t K, T* __restrict__ dp_direct, int assign,
+                          double* __restrict__ err_direct) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cv_raw[];
+    constexpr int NG = kChainVjpBlock / kChainDim;
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cv_raw);
+    T* ps = reinterpret_cast<T*>(cv_raw + nl * sizeof(LayerConst));
+    T* rows = ps + P;                                 // [NG][P] gradient rows
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int i = threadIdx.x; i < NG * P; i += blockDim.x) rows[i] = T(0);
+    }
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps, rows)
+    const Math<T> M{tab};
+    const int N0 = lcl[0].I;
+    const int j = threadIdx.x & (kChainDim - 1);
+    T* __restrict__ row = rows + (threadIdx.x / kChainDim) * P;
+    const double suc = stage_scale(su.cscale), slc = stage_scale(sl.cscale);
+    const bool want_err = err_slab != nullptr || err_direct != nullptr;
+    double eacc = 0.0;
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kChainDim;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kChainDim; k < K; k += stride) {
+        const int64_t idx = (int64_t)N0 * k + j;
+        T yj = T(0), lj = T(0), l0 = T(0);
+        double ev = 0.0;
+        if (j < N0) {
+            yj = u[idx];
+#pragma unroll
+            for (int m = 0; m < kMaxStages; ++m)
+                if (m < su.nk) yj = kfma<T>((T)(su.c[m] * suc), su.k[m][idx], yj);
+            lj = lam[idx];
+            l0 = lj;
+#pragma unroll
+            for (int m = 0; m < kMaxStages; ++m) {
+                if (m < sl.nk) {
+                    const T km = sl.k[m][idx];
+                    lj = kfma<T>((T)(sl.c[m] * slc), km, lj);
+                    if (want_err) ev = ::fma(sl.ec[m] * slc, (double)km, ev);
+                }
+            }
+            if (lam_out) lam_out[idx] = lj;
+        }
+        // forward: the input activation of every layer (lane j holds entry j)
+        T act[kChainMaxLayers];
+        act[0] = yj;
+#pragma unroll
+        for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
+            act[l + 1] = T(0);
+            if (l + 1 < nl) {
+                const LayerConst& lc = lcl[l];
+                const int I = lc.I, O = lc.O, G = lc.G;
+                const T* __restrict__ C = ps + lc.p_off;
+                const T* __restrict__ W = ps + lc.w_off;
+                T acc[kChainDim], bas[kChainDim];
+#pragma unroll
+                for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
+                if (j < I) {
+                    const T a = act[l];
+                    BasisStream<T, PATH> bs;
+                    bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
+                    for (int g = 0; g < G; ++g) {
+                        T z, aux;
+                        const T phi = bs.next(M, lc, g, z, aux);
+                        const T* Cc = C + O * (g + G * j);
+#pragma unroll
+                        for (int o = 0; o < kChainDim; ++o)
+                            if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
+                    }
+                    if (lc.use_base) {
+                        const T sw = swish<T>(M, a);
+#pragma unroll
+                        for (int o = 0; o < kChainDim; ++o)
+                            if (o < O) bas[o] = W[O * j + o] * sw;
+                    }
+                }
+                T out = T(0);
+#pragma unroll
+                for (int o = 0; o < kChainDim; ++o) {
+                    if (o < O) {
+                        T s = acc[o], b = bas[o];
+#pragma unroll
+                        for (int m = 1; m < kChainDim; m <<= 1) {
+                            s += __shfl_xor(s, m, kChainDim);
+                            if (lc.use_base) b += __shfl_xor(b, m, kChainDim);
+                        }
+                        if (o == j) out = lc.use_base ? s + b : s;
+                    }
+                }
+                act[l + 1] = out;
+            }
+        }
+        // backward: ȳ of the last layer is λs; lane i of layer l turns it into x̄_i
+        T ybar = lj;
+#pragma unroll
+        for (int l = kChainMaxLayers - 1; l >= 0; --l) {
+            if (l < nl) {
+                const LayerConst& lc = lcl[l];
+                const int I = lc.I, O = lc.O, G = lc.G;
+                const T* __restrict__ C = ps + lc.p_off;
+                const T* __restrict__ W = ps + lc.w_off;
+                T yb[kChainDim];
+#pragma unroll
+                for (int o = 0; o < kChainDim; ++o) yb[o] = o < O ? __shfl(ybar, o, kChainDim) : T(0);
+                T xb = T(0);
+                if (j < I) {
+                    const T a = act[l];
+                    const T n = normalize<NORM, T>(M, lc.norm, a);
+                    BasisStream<T, PATH> bs;
+                    bs.init(M, lc, n);
+                    const T invh = T(lc.invh);
+                    T nbar = T(0);
+                    for (int g = 0; g < G; ++g) {
+                        T z, aux;
+                        const T phi = bs.next(M, lc, g, z, aux);
+                        const int c = g + G * j;
+                        const T* Cc = C + O * c;
+                        T* __restrict__ rc = row + lc.p_off + O * c;
+                        T bb = T(0);
+#pragma unroll
+                        for (int o = 0; o < kChainDim; ++o) {
+                            if (o < O) {
+                                bb = kfma<T>(Cc[o], yb[o], bb);
+                                rc[o] = kfma<T>(yb[o], phi, rc[o]);
+                            }
+                        }
+                        const T zb = basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb);
+                        nbar = nbar + zb * invh;
+                    }
+                    xb = nbar * dnormalize<NORM, T>(lc.norm, n);
+                    if (lc.use_base) {
+                        T sw, dsw;
+                        swish_and_grad<T>(M, a, sw, dsw);
+                        const T* Wj = W + O * j;
+                        T* __restrict__ rw = row + lc.w_off + O * j;
+                        T sb = T(0);
+#pragma unroll
+                        for (int o = 0; o < kChainDim; ++o) {
+                            if (o < O) {
+                                sb = kfma<T>(Wj[o], yb[o], sb);
+                                rw[o] = kfma<T>(yb[o], sw, rw[o]);
+                            }
+                        }
+                        xb = xb + sb * dsw;
+                    }
+                }
+                ybar = xb;
+            }
+        }
+        if (j < N0) {
+            lamJ[idx] = ybar;
+            if (want_err) {
+                const double e = ::fma(sl.ec[sl.nk] * slc, (double)ybar, ev);
+                const double sk = ::fma(sl.reltol, fmax(kabs((double)l0), kabs((double)lj)), sl.abstol);
+                const double r = e / sk;
+                eacc = ::fma(r, r, eacc);
+            }
+        }
+    }
+    __syncthreads();
+    // one block (a few columns, e.g. the single LV trajectory): the block's sums are the totals
+    for (int q = threadIdx.x; q < P; q += blockDim.x) {
+        T s = rows[q];
+#pragma unroll
+        for (int g = 1; g < NG; ++g) s = s + rows[g * P + q];
+        if (dp_direct) dp_direct[q] = assign ? s : dp_direct[q] + s;
+        else if (slab) slab[(int64_t)blockIdx.x * P + q] = s;
+    }
+    if (want_err) {
+        __shared__ double red[kChainVjpBlock / kWave];
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_direct ? err_direct : err_slab + blockIdx.x);
+    }
+}
+
+// dp[q] (= or +=) Σ_b slab[b·P + q] (block q < P) and err_out[0] = Σ_b err_slab[b] (block P)
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+chain_vjp_finish_kernel(const T* __restrict__ slab, int64_t nblk, int64_t P, T* __restrict__ dp, int assign,
+                        const double* __restrict__ err_slab, double* __restrict__ err_out) {
+    __shared__ double red[kBlock / kWave];
+    const int64_t q = blockIdx.x;
+    double s = 0.0;
+    if (q < P) {
+        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += (double)slab[b * P + q];
+    } else {
+        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += err_slab[b];
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        if (q < P) dp[q] = assign ? (T)t : dp[q] + (T)t;
+        else err_out[0] = t;
     }
 }
 
@@ -406,13 +656,16 @@ hipError_t launch_kd_edge_act(const LayerConst& hlc, const LayerConst* lc, const
     }
 }
 
+static bool I_ne_O(const LayerConst* hlcs, int nl) { return hlcs[0].I != hlcs[nl - 1].O; }
+
 // One launch for the whole chain when every layer is small (I, O <= 16), shares the
 // normalizer/path specialisation, the parameters fit in LDS and the batch is small enough
 // to be latency-bound; else returns hipErrorNotSupported and the caller runs one launch
 // per layer.
 template <typename T>
 hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
-                               const T* x, T* y, int64_t K, hipStream_t st) {
+                               const T* x, T* y, int64_t K, hipStream_t st, const StageArgs<T>* sa, T* y_out,
+                               double* err_slab, int slab_rows, double* err_out) {
     // 16 lanes per column pays while the batch leaves the chip latency-bound (<= 32 columns
     // per CU); beyond that the per-layer thread-per-column kernels keep every lane busy
     if (nl < 1 || nl > 8 || K > 32768) return hipErrorNotSupported;
@@ -424,22 +677,79 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
     }
     const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T);
     if (lds > 48 * 1024) return hipErrorNotSupported;
-    const int g = grid_for(K * kChainDim, kChainBlock, kGridCap);
+    if (sa && I_ne_O(hlcs, nl)) return hipErrorNotSupported;
+    const StageArgs<T> none{};
+    const StageArgs<T>& s = sa ? *sa : none;
+    const int g = grid_for(K * kChainDim, kChainBlock, err_out ? (slab_rows < kGridCap ? slab_rows : kGridCap) : kGridCap);
+    const bool one = g == 1;
+    double* es = err_out && !one ? err_slab : nullptr;
+    double* ed = err_out && one ? err_out : nullptr;
     const LayerConst& h = hlcs[0];
 #define KAN_CHAIN(NORM, PATH)                                                                                    \
     hipLaunchKernelGGL((kd_chain_col_kernel<T, NORM, PATH>), dim3(g), dim3(kChainBlock), lds, st, lcs, nl, p,     \
-                       (int)P, x, y, K)
+                       (int)P, x, y, K, s, y_out, es, ed)
     if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CHAIN(NORM_TANH_FAST, PATH_REC);
     else if (h.path == PATH_REC_CORR) KAN_CHAIN(NORM_RUNTIME, PATH_REC_CORR);
     else if (h.path == PATH_REC) KAN_CHAIN(NORM_RUNTIME, PATH_REC);
     else KAN_CHAIN(NORM_RUNTIME, PATH_DIRECT);
 #undef KAN_CHAIN
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !es) return e;
+    return launch_stage_error_final(err_slab, g, err_out, st);
+}
+
+// The fused adjoint stage of a small chain (kd_chain_vjp_stage_kernel) when every layer is
+// small (I, O <= 16), the layers share the normalizer/path specialisation, nl <= 4 and the
+// parameter vector plus the gradient rows fit in LDS; hipErrorNotSupported otherwise.
+template <typename T>
+hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                     const T* u, const StageArgs<T>& su, const T* lam, const StageArgs<T>& sl,
+                                     T* lam_out, T* lamJ, T* dp, bool dp_assign, double* err_out, void* slab,
+                                     size_t slab_bytes, int64_t K, hipStream_t st) {
+    if (nl < 1 || nl > kChainMaxLayers || K < 1) return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    if (hlcs[nl - 1].O != hlcs[0].I) return hipErrorNotSupported;
+    const int ng = kChainVjpBlock / kChainDim;
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + ng);
+    if (lds > 60 * 1024) return hipErrorNotSupported;
+    // slab: [grid][P] T rows, then [grid] double error partials
+    int64_t cap = (int64_t)(slab_bytes / (P * sizeof(T) + sizeof(double))) - 1;
+    if (cap > 1024) cap = 1024;
+    if (cap < 1) return hipErrorNotSupported;
+    const int grid = grid_for(K, ng, (int)cap);
+    T* tslab = (T*)slab;
+    double* eslab = err_out ? (double*)((char*)slab + (((size_t)grid * P * sizeof(T) + 255) & ~(size_t)255)) : nullptr;
+    const LayerConst& h = hlcs[0];
+    const bool one = grid == 1;   // a single block writes dp and the error total itself
+#define KAN_CVJP(NORM, PATH)                                                                                     \
+    hipLaunchKernelGGL((kd_chain_vjp_stage_kernel<T, NORM, PATH>), dim3(grid), dim3(kChainVjpBlock), lds, st,    \
+                       lcs, nl, p, (int)P, u, su, lam, sl, lam_out, lamJ, one ? nullptr : tslab,                  \
+                       one ? nullptr : eslab, K, one ? dp : nullptr, dp_assign ? 1 : 0, one ? err_out : nullptr)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CVJP(NORM_TANH_FAST, PATH_REC);
+    else if (h.path == PATH_REC_CORR) KAN_CVJP(NORM_RUNTIME, PATH_REC_CORR);
+    else if (h.path == PATH_REC) KAN_CVJP(NORM_RUNTIME, PATH_REC);
+    else KAN_CVJP(NORM_RUNTIME, PATH_DIRECT);
+#undef KAN_CVJP
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || one || (!dp && !err_out)) return e;
+    hipLaunchKernelGGL((chain_vjp_finish_kernel<T>), dim3((unsigned)(dp ? P : 0) + (err_out ? 1 : 0)), dim3(kBlock), 0,
+                       st, tslab, (int64_t)grid, (int64_t)P, dp, dp_assign ? 1 : 0, eslab, err_out);
     return hipGetLastError();
 }
 
 #define KAN_COL_INST(T)                                                                                          \
+    template hipError_t launch_kd_chain_vjp_stage<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t, \
+                                                     const T*, const StageArgs<T>&, const T*, const StageArgs<T>&, \
+                                                     T*, T*, T*, bool, double*, void*, size_t, int64_t,          \
+                                                     hipStream_t);                                                \
     template hipError_t launch_kd_chain_col<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,     \
-                                               const T*, T*, int64_t, hipStream_t);                               \
+                                               const T*, T*, int64_t, hipStream_t, const StageArgs<T>*, T*,       \
+                                               double*, int, double*);                                            \
     template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
     template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
                                              int64_t, hipStream_t);                                               \

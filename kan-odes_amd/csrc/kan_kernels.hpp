@@ -72,10 +72,21 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                              hipStream_t st);
-// whole chain, one launch (all layers I, O <= 16); hipErrorNotSupported otherwise
+// whole chain, one launch (all layers I, O <= 16); hipErrorNotSupported otherwise.  With `sa` it is
+// a Runge-Kutta stage (kanode_rhs_stage): input x + Σ c_j k_j, optional y_out, and with err_out the
+// embedded-error total (per-block partials in err_slab, <= slab_rows blocks)
 template <typename T>
 hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
-                               const T* x, T* y, int64_t K, hipStream_t st);
+                               const T* x, T* y, int64_t K, hipStream_t st, const StageArgs<T>* sa = nullptr,
+                               T* y_out = nullptr, double* err_slab = nullptr, int slab_rows = 0,
+                               double* err_out = nullptr);
+// adjoint stage of a whole small chain in one launch + one reduction launch (dp = or +=; the λ
+// error total into err_out when non-null); hipErrorNotSupported outside its shapes
+template <typename T>
+hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                     const T* u, const StageArgs<T>& su, const T* lam, const StageArgs<T>& sl,
+                                     T* lam_out, T* lamJ, T* dp, bool dp_assign, double* err_out, void* slab,
+                                     size_t slab_bytes, int64_t K, hipStream_t st);
 template <typename T>
 hipError_t launch_kd_vjp_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, const T* yb,
                              T* xb, T* pbar, T* slab, int slab_blocks, int64_t K, hipStream_t st);

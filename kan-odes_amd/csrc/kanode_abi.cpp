@@ -388,6 +388,19 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
                                          kSlabBlocks, B, st));
         return KANODE_OK;
     }
+    if (lamJ && h->n_in == h->n_out) {
+        bool all_col = true;
+        for (int l = 0; l < h->n_layers; ++l) all_col = all_col && h->kind[l] == KIND_COL;
+        if (all_col) {
+            const kan::StageArgs<T> none{};
+            const hipError_t e = kan::launch_kd_chain_vjp_stage<T>(h->hlc, h->n_layers, h->dlc, p, h->P, u, none, lam,
+                                                                   none, nullptr, lamJ, dp, false, nullptr, h->slab,
+                                                                   h->slab_bytes, B, st);
+            if (e == hipSuccess) return KANODE_OK;
+            if (e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_vjp_stage: ") + hipGetErrorString(e));
+        }
+    }
     kanode_status s = ensure_ws(h, B, st);
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;
@@ -447,6 +460,18 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
                                                (int)h->spec.nx, u, sa, (double*)sg->y_out, (double*)h->slab,
                                                kSlabBlocks, err_out, du, B, st, table_build(h, h->built_phi)));
             return KANODE_OK;
+        }
+    }
+    if (h->spec.rhs_kind == KANODE_RHS_CHAIN) {
+        // a small chain: stage input, RHS and error partials in one kernel (kd_chain_col_kernel)
+        bool all_col = true;
+        for (int l = 0; l < h->n_layers; ++l) all_col = all_col && h->kind[l] == KIND_COL;
+        if (all_col) {
+            const hipError_t e = kan::launch_kd_chain_col<T>(h->hlc, h->n_layers, h->dlc, p, h->P, u, du, B, st, &sa,
+                                                             (T*)sg->y_out, (double*)h->slab, kSlabBlocks, err_out);
+            if (e == hipSuccess) return KANODE_OK;
+            if (e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_col: ") + hipGetErrorString(e));
         }
     }
     // unfused: y materialised (into y_out or the handle's stage workspace), RHS, error pass
@@ -519,6 +544,19 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
                                                    dp_assign, adj->want_error ? (double*)adj->error_sumsq : nullptr,
                                                    (double*)h->slab, kSlabBlocks, B, st, table_build(h, h->built_vjp)));
             return KANODE_OK;
+        }
+    }
+    if (h->spec.rhs_kind == KANODE_RHS_CHAIN && lamJ) {
+        // a small chain: the whole adjoint stage in one kernel (kd_chain_vjp_stage_kernel) + one reduction
+        bool all_col = true;
+        for (int l = 0; l < h->n_layers; ++l) all_col = all_col && h->kind[l] == KIND_COL;
+        if (all_col) {
+            const hipError_t e = kan::launch_kd_chain_vjp_stage<T>(
+                h->hlc, h->n_layers, h->dlc, p, h->P, u, su, lam, sl, (T*)adj->y_out, lamJ, dp, dp_assign,
+                adj->want_error ? (double*)adj->error_sumsq : nullptr, h->slab, h->slab_bytes, B, st);
+            if (e == hipSuccess) return KANODE_OK;
+            if (e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_vjp_stage: ") + hipGetErrorString(e));
         }
     }
     if (dp && dp_assign) HIP_TRY(h, hipMemsetAsync(dp, 0, (size_t)h->P * sizeof(T), st));
