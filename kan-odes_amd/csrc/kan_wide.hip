@@ -5,14 +5,18 @@
 // KDense forward kdense.jl:109-130).  With B <= 8 columns the contraction is a
 // parameter-streaming GEMV, not a GEMM: VALU + reductions, no MFMA.
 //
-//   wide-in  (I·G large, O <= 16): one thread per input i computes its basis and
-//            its partial y[o] for every column; partials are reduced in the block
-//            (fixed order) into a per-block slab, then an ordered slab reduction.
-//   wide-out (O large): one thread per output row o; the block stages the (small)
-//            basis of its column tile in LDS once; C[o + O*c] reads are coalesced
-//            over o (C is column-major [O, G*I]).
-// Pullbacks mirror them: wide-out owns its dC/dW rows (no reduction) and emits
-// partial basis cotangents per row block; wide-in owns dC/dW of its inputs.
+// The batch is a handful of trajectories, so the kernels spread each column over many
+// workgroups instead of looping over the columns in a few:
+//   wide-in  (I·G large, O <= 16): grid (input chunk of 64, column); lane i evaluates the
+//            basis of its input and its partial y[o]; a wave sum per o gives the chunk's
+//            partial (slab), then an ordered reduction over the chunks.
+//   wide-out (O large): grid (row chunk of 256, column tile of 8); the block stages the
+//            small basis of its tile in LDS; C[o + O*c] reads are coalesced over o.
+// Pullbacks: wide-out parameters -- thread o owns dC[o, :], dW[o, :] (no reduction);
+// wide-out input cotangent -- one workgroup per (input i, column tile) forms the G + 1
+// dot products Σ_o C[o, g + G i] ȳ[o, k] (coalesced over o, wave sums) and then x̄[i, k];
+// wide-in -- lane i owns dC[:, g + G i], dW[:, i] (accumulated in its own LDS slots over
+// the columns) and x̄[i, :].  Every reduction runs in a fixed order (bitwise reproducible).
 #include "kan_common.hpp"
 #include "kan_kernels.hpp"
 
@@ -51,21 +55,21 @@ struct Basis1 {
 };
 
 // ---------------------------------------------------------------------------
-// wide-in forward: grid.x = ceil(I/256); slab[(blk*K + k)*O + o] = Σ_{i in blk} (C φ + W sw)
+// wide-in forward: grid (ceil(I/64), columns); slab[(chunk*K + k)*O + o] = Σ_{i in chunk} (C φ + W sw)
+constexpr int kWIB = 64;   // inputs per wide-in workgroup (one wave)
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kWIB)
 kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                      T* __restrict__ slab, int64_t K) {
-    __shared__ T red[(kBlock / kWave) * kOWide];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.x * kWIB + threadIdx.x;
     const bool valid = i < I;
-    for (int64_t k = 0; k < K; ++k) {
+    for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
         T acc[kOWide];
 #pragma unroll
         for (int o = 0; o < kOWide; ++o) acc[o] = T(0);
@@ -89,7 +93,13 @@ kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p
                     if (o < O) acc[o] = kfma<T>(Wi[o], sw, acc[o]);
             }
         }
-        block_sum_to<T, kOWide>(acc, O, red, slab + ((int64_t)blockIdx.x * K + k) * O);
+#pragma unroll
+        for (int o = 0; o < kOWide; ++o) {
+            if (o < O) {
+                const T sum = wave_sum(acc[o]);
+                if (threadIdx.x == 0) slab[((int64_t)blockIdx.x * K + k) * O + o] = sum;
+            }
+        }
     }
 }
 
@@ -106,11 +116,37 @@ kd_widein_reduce_kernel(const T* __restrict__ slab, int nblk, int O, int64_t K, 
     y[(int64_t)O * k + o] = s;
 }
 
-// ---------------------------------------------------------------------------
-// wide-out forward: grid.x = ceil(O/256); each block stages the basis of a column
-// tile (GI x KT values + I x KT swish values) in LDS, then thread o contracts.
+// Basis values of a column tile of the (short) input, staged in LDS:
+// phiL[(g + G i)*kKT + kk], swL[i*kKT + kk] (zero outside the tile).
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kBlock)
+__device__ __forceinline__ void stage_tile_basis(const Math<T>& M, const LayerConst& lc, const T* __restrict__ x,
+                                                 int64_t k0, int kt, T* phiL, T* swL) {
+    const int I = lc.I, G = lc.G;
+    for (int t = threadIdx.x; t < I * kKT; t += blockDim.x) {
+        const int i = t / kKT, kk = t - i * kKT;
+        if (kk < kt) {
+            const T xi = x[(int64_t)I * (k0 + kk) + i];
+            Basis1<T, PATH> bs;
+            bs.init(M, lc, xi);
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                phiL[(g + G * i) * kKT + kk] = bs.next(M, lc, g, z, aux);
+            }
+            swL[i * kKT + kk] = lc.use_base ? swish<T>(M, xi) : T(0);
+        } else {
+            for (int g = 0; g < G; ++g) phiL[(g + G * i) * kKT + kk] = T(0);
+            swL[i * kKT + kk] = T(0);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// wide-out forward: grid (ceil(O/64), column tiles); thread o contracts its row of C
+// against the tile's basis (one-wave workgroups: at a few columns the launch is latency
+// bound, so more workgroups and more loads in flight per lane beat bigger blocks).
+constexpr int kWOB = 64;
+template <typename T, int PATH>
+__global__ void __launch_bounds__(kWOB)
 kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                       T* __restrict__ y, int64_t K) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -124,41 +160,29 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t k0 = 0; k0 < K; k0 += kKT) {
+    for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
         const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
         __syncthreads();
-        for (int t = threadIdx.x; t < I * kKT; t += blockDim.x) {
-            const int i = t / kKT, kk = t - i * kKT;
-            if (kk < kt) {
-                const T xi = x[(int64_t)I * (k0 + kk) + i];
-                Basis1<T, PATH> bs;
-                bs.init(M, lc, xi);
-                for (int g = 0; g < G; ++g) {
-                    T z, aux;
-                    phiL[(g + G * i) * kKT + kk] = bs.next(M, lc, g, z, aux);
-                }
-                swL[i * kKT + kk] = lc.use_base ? swish<T>(M, xi) : T(0);
-            } else {
-                for (int g = 0; g < G; ++g) phiL[(g + G * i) * kKT + kk] = T(0);
-                swL[i * kKT + kk] = T(0);
-            }
-        }
+        stage_tile_basis<T, PATH>(M, lc, x, k0, kt, phiL, swL);
         __syncthreads();
         if (o < O) {
             T acc[kKT], bas[kKT];
 #pragma unroll
             for (int kk = 0; kk < kKT; ++kk) { acc[kk] = T(0); bas[kk] = T(0); }
+#pragma unroll 4
             for (int c = 0; c < GI; ++c) {
                 const T cv = C[o + (int64_t)O * c];
 #pragma unroll
                 for (int kk = 0; kk < kKT; ++kk) acc[kk] = kfma<T>(cv, phiL[c * kKT + kk], acc[kk]);
             }
-            if (lc.use_base)
+            if (lc.use_base) {
+#pragma unroll 4
                 for (int i = 0; i < I; ++i) {
                     const T wv = W[o + (int64_t)O * i];
 #pragma unroll
                     for (int kk = 0; kk < kKT; ++kk) bas[kk] = kfma<T>(wv, swL[i * kKT + kk], bas[kk]);
                 }
+            }
 #pragma unroll
             for (int kk = 0; kk < kKT; ++kk)
                 if (kk < kt) y[(int64_t)O * (k0 + kk) + o] = lc.use_base ? acc[kk] + bas[kk] : acc[kk];
@@ -167,138 +191,172 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// wide-out pullback, pass 1: thread o owns dC[o, :], dW[o, :] (accumulated into
-// pbar); the block's partial cotangents of the basis (Σ_o C[o,c] ȳ[o,k]) and of
-// the base branch (Σ_o W[o,i] ȳ[o,k]) go to slab[(blk*K + k)*(GI+I) + c].
+// wide-out pullback, parameters: workgroup (row chunk, input i); thread o owns
+// dC[o, g + G i] (g < G) and dW[o, i] in registers over all columns, then adds them to pbar
+// once (coalesced over o).  The basis of input i is staged in LDS kWOPK columns at a time.
+constexpr int kWOPK = 128;
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kBlock)
-kd_vjp_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                      const T* __restrict__ ybar, T* __restrict__ pbar, T* __restrict__ slab, int64_t K) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+__global__ void __launch_bounds__(kWOB)
+kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ ybar,
+                            T* __restrict__ pbar, int64_t K) {
+    __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
-    const int GI = G * I;
-    const int R = GI + I;                            // cotangent rows per column
-    T* phiL = reinterpret_cast<T*>(smem_raw);       // [GI][kKT]
-    T* swL = phiL + (int64_t)GI * kKT;              // [I][kKT]
-    T* redw = swL + (int64_t)I * kKT;               // [wave][R][kKT] wave partials
-    const T* __restrict__ C = p + lc.p_off;
-    const T* __restrict__ W = p + lc.w_off;
-    T* __restrict__ dC = pbar ? pbar + lc.p_off : nullptr;
-    T* __restrict__ dW = pbar ? pbar + lc.w_off : nullptr;
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = o < O;
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave, nw = blockDim.x / kWave;
-    for (int64_t k0 = 0; k0 < K; k0 += kKT) {
-        const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
+    const int i = blockIdx.y;
+    const int o = blockIdx.x * kWOB + threadIdx.x;
+    const bool base = lc.use_base != 0;
+    T acc[kMaxGrid + 1];
+#pragma unroll
+    for (int r = 0; r <= kMaxGrid; ++r) acc[r] = T(0);
+    for (int64_t k0 = 0; k0 < K; k0 += kWOPK) {
+        const int kt = (int)((K - k0) < kWOPK ? (K - k0) : kWOPK);
         __syncthreads();
-        for (int t = threadIdx.x; t < I * kKT; t += blockDim.x) {
-            const int i = t / kKT, kk = t - i * kKT;
-            const bool on = kk < kt;
-            const T xi = on ? x[(int64_t)I * (k0 + kk) + i] : T(0);
+        for (int kk = threadIdx.x; kk < kt; kk += kWOB) {
+            const T xi = x[(int64_t)I * (k0 + kk) + i];
             Basis1<T, PATH> bs;
             bs.init(M, lc, xi);
             for (int g = 0; g < G; ++g) {
                 T z, aux;
-                const T v = bs.next(M, lc, g, z, aux);
-                phiL[(g + G * i) * kKT + kk] = on ? v : T(0);
+                Ph[g * kWOPK + kk] = bs.next(M, lc, g, z, aux);
             }
-            swL[i * kKT + kk] = (on && lc.use_base) ? swish<T>(M, xi) : T(0);
+            Ph[kMaxGrid * kWOPK + kk] = base ? swish<T>(M, xi) : T(0);
         }
         __syncthreads();
-        T yb[kKT];
+        if (o < O) {
+            for (int kk = 0; kk < kt; ++kk) {
+                const T yb = ybar[(int64_t)O * (k0 + kk) + o];
 #pragma unroll
-        for (int kk = 0; kk < kKT; ++kk) yb[kk] = (valid && kk < kt) ? ybar[(int64_t)O * (k0 + kk) + o] : T(0);
-        for (int c = 0; c < R; ++c) {
-            const bool isC = c < GI;
-            const T coef = valid ? (isC ? C[o + (int64_t)O * c] : (lc.use_base ? W[o + (int64_t)O * (c - GI)] : T(0)))
-                                 : T(0);
-            const T* row = isC ? phiL + c * kKT : swL + (c - GI) * kKT;
-            // owned parameter gradient: Σ_k ȳ[o,k] basis[c,k]
-            T g = T(0);
-#pragma unroll
-            for (int kk = 0; kk < kKT; ++kk) g = kfma<T>(yb[kk], row[kk], g);
-            if (valid && pbar && (isC || lc.use_base)) {
-                if (isC) dC[o + (int64_t)O * c] += g;
-                else dW[o + (int64_t)O * (c - GI)] += g;
+                for (int r = 0; r < kMaxGrid; ++r)
+                    if (r < G) acc[r] = kfma<T>(yb, Ph[r * kWOPK + kk], acc[r]);
+                acc[kMaxGrid] = kfma<T>(yb, Ph[kMaxGrid * kWOPK + kk], acc[kMaxGrid]);
             }
-            // partial cotangent of basis row c for every column of the tile (wave sums)
-#pragma unroll
-            for (int kk = 0; kk < kKT; ++kk) {
-                const T s = wave_sum(coef * yb[kk]);
-                if (lane == 0) redw[((int64_t)wid * R + c) * kKT + kk] = s;
-            }
-        }
-        __syncthreads();
-        // block partial = Σ over waves in wave order -> slab
-        for (int t = threadIdx.x; t < R * kt; t += blockDim.x) {
-            const int c = t / kt, kk = t - c * kt;
-            T s = redw[(int64_t)c * kKT + kk];
-            for (int w = 1; w < nw; ++w) s += redw[((int64_t)w * R + c) * kKT + kk];
-            slab[((int64_t)blockIdx.x * K + (k0 + kk)) * R + c] = s;
         }
     }
+    if (o >= O) return;
+    T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
+#pragma unroll
+    for (int r = 0; r < kMaxGrid; ++r)
+        if (r < G) dC[(int64_t)O * r] += acc[r];
+    if (base) pbar[lc.w_off + o + (int64_t)O * i] += acc[kMaxGrid];
 }
 
-// wide-out pullback, pass 2: x̄[i,k] from the summed basis cotangents
-// (rrule(_rbf) + normalizer + swish rrules; utils.jl:15-21, NNlib).
+// wide-out pullback, input cotangent: workgroup (i, column tile).  Waves take the rows
+// r < G (C[:, g + G i]) and r = G (W[:, i]) and form Σ_o row[o] ȳ[o, k] (lanes stride over
+// o, coalesced; one wave sum per column); then lane kk turns them into x̄[i, k0 + kk]
+// through the basis / normalizer / swish rrules (utils.jl:15-21, NNlib).
+constexpr int kWOX = 256;
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kBlock)
-kd_vjp_wideout_finalize_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x,
-                               const T* __restrict__ slab, int nblk, T* __restrict__ xbar, int64_t K) {
+__global__ void __launch_bounds__(kWOX)
+kd_vjp_wideout_xbar_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                           const T* __restrict__ ybar, T* __restrict__ xbar, int64_t K) {
+    __shared__ T S[(kMaxGrid + 1) * kKT];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
-    const int I = lc.I, G = lc.G;
-    const int GI = G * I, R = GI + I;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)I * K) return;
-    const int64_t k = idx / I;
-    const int i = (int)(idx - k * I);
-    const T xi = x[(int64_t)I * k + i];
-    Basis1<T, PATH> bs;
-    bs.init(M, lc, xi);
-    const T invh = T(lc.invh);
-    T nbar = T(0);
-    for (int g = 0; g < G; ++g) {
-        T z, aux;
-        const T phi = bs.next(M, lc, g, z, aux);
-        T bb = T(0);
-        for (int b = 0; b < nblk; ++b) bb += slab[((int64_t)b * K + k) * R + g + G * i];
-        nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb) * invh;
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const int i = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave, nw = blockDim.x / kWave;
+    const int rows = G + (lc.use_base ? 1 : 0);
+    for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
+        const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
+        for (int r = wid; r < rows; r += nw) {
+            const T* __restrict__ row = r < G ? p + lc.p_off + (int64_t)O * (r + (int64_t)G * i)
+                                              : p + lc.w_off + (int64_t)O * i;
+            T acc[kKT];
+#pragma unroll
+            for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
+#pragma unroll 2
+            for (int o = lane; o < O; o += kWave) {
+                const T cv = row[o];
+#pragma unroll
+                for (int kk = 0; kk < kKT; ++kk)
+                    if (kk < kt) acc[kk] = kfma<T>(cv, ybar[(int64_t)O * (k0 + kk) + o], acc[kk]);
+            }
+#pragma unroll
+            for (int kk = 0; kk < kKT; ++kk) {
+                if (kk < kt) {
+                    const T s = wave_sum(acc[kk]);
+                    if (lane == 0) S[r * kKT + kk] = s;
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < kt) {
+            const int kk = threadIdx.x;
+            const T xi = x[(int64_t)I * (k0 + kk) + i];
+            Basis1<T, PATH> bs;
+            bs.init(M, lc, xi);
+            const T invh = T(lc.invh);
+            T nbar = T(0);
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                const T phi = bs.next(M, lc, g, z, aux);
+                nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, S[g * kKT + kk]) * invh;
+            }
+            T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
+            if (lc.use_base) {
+                T sw, dsw;
+                swish_and_grad<T>(M, xi, sw, dsw);
+                xb = xb + S[G * kKT + kk] * dsw;
+            }
+            xbar[(int64_t)I * (k0 + kk) + i] = xb;
+        }
+        __syncthreads();
     }
-    T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
-    if (lc.use_base) {
-        T sb = T(0);
-        for (int b = 0; b < nblk; ++b) sb += slab[((int64_t)b * K + k) * R + GI + i];
-        T sw, dsw;
-        swish_and_grad<T>(M, xi, sw, dsw);
-        xb = xb + sb * dsw;
-    }
-    xbar[(int64_t)I * k + i] = xb;
 }
 
 // ---------------------------------------------------------------------------
-// wide-in pullback: thread i owns dC[:, g+G i], dW[:, i] and x̄[i, :].
+// wide-in pullback, grid (ceil(I/64), np + nx):
+//   blockIdx.y <  np (= O when pbar): lane i, row o = blockIdx.y owns dC[o, g + G i] (g < G)
+//                  and dW[o, i] in registers over all columns, added to pbar once;
+//   blockIdx.y >= np: lane i forms x̄[i, k] for the columns k = y - np (+ nx, ...): the G + 1
+//                  dot products Σ_o C[o, g + G i] ȳ[o, k] (O <= 16, registers) then the
+//                  basis / normalizer / swish rrules.
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kWIB)
 kd_vjp_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                     const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K) {
+                     const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
+                     int nx) {
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.x * kWIB + threadIdx.x;
     if (i >= I) return;
-    const T invh = T(lc.invh);
-    T dWacc[kOWide];
+    const bool base = lc.use_base != 0;
+    if ((int)blockIdx.y < np) {
+        const int o = blockIdx.y;
+        T acc[kMaxGrid];
 #pragma unroll
-    for (int o = 0; o < kOWide; ++o) dWacc[o] = T(0);
-    for (int64_t k = 0; k < K; ++k) {
+        for (int g = 0; g < kMaxGrid; ++g) acc[g] = T(0);
+        T accw = T(0);
+        for (int64_t k = 0; k < K; ++k) {
+            const T xi = x[(int64_t)I * k + i];
+            const T yb = ybar[(int64_t)O * k + o];
+            Basis1<T, PATH> bs;
+            bs.init(M, lc, xi);
+#pragma unroll
+            for (int g = 0; g < kMaxGrid; ++g) {
+                if (g < G) {
+                    T z, aux;
+                    acc[g] = kfma<T>(yb, bs.next(M, lc, g, z, aux), acc[g]);
+                }
+            }
+            if (base) accw = kfma<T>(yb, swish<T>(M, xi), accw);
+        }
+        T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
+#pragma unroll
+        for (int g = 0; g < kMaxGrid; ++g)
+            if (g < G) dC[(int64_t)O * g] += acc[g];
+        if (base) pbar[lc.w_off + o + (int64_t)O * i] += accw;
+        return;
+    }
+    const T invh = T(lc.invh);
+    for (int64_t k = (int)blockIdx.y - np; k < K; k += nx) {
         T yb[kOWide];
 #pragma unroll
         for (int o = 0; o < kOWide; ++o) yb[o] = o < O ? ybar[(int64_t)O * k + o] : T(0);
@@ -309,58 +367,47 @@ kd_vjp_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p
         for (int g = 0; g < G; ++g) {
             T z, aux;
             const T phi = bs.next(M, lc, g, z, aux);
-            const int64_t col = (int64_t)O * (g + (int64_t)G * i);
+            const T* __restrict__ Cc = C + (int64_t)O * (g + (int64_t)G * i);
             T bb = T(0);
 #pragma unroll
             for (int o = 0; o < kOWide; ++o)
-                if (o < O) bb = kfma<T>(C[col + o], yb[o], bb);
+                if (o < O) bb = kfma<T>(Cc[o], yb[o], bb);
             nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb) * invh;
-            if (pbar) {
-#pragma unroll
-                for (int o = 0; o < kOWide; ++o)
-                    if (o < O) pbar[lc.p_off + col + o] += yb[o] * phi;
-            }
         }
         T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
-        if (lc.use_base) {
+        if (base) {
             T sw, dsw;
             swish_and_grad<T>(M, xi, sw, dsw);
             T sb = T(0);
 #pragma unroll
             for (int o = 0; o < kOWide; ++o)
-                if (o < O) {
-                    sb = kfma<T>(W[(int64_t)O * i + o], yb[o], sb);
-                    dWacc[o] = kfma<T>(yb[o], sw, dWacc[o]);
-                }
+                if (o < O) sb = kfma<T>(W[(int64_t)O * i + o], yb[o], sb);
             xb = xb + sb * dsw;
         }
         xbar[(int64_t)I * k + i] = xb;
-    }
-    if (pbar && lc.use_base) {
-#pragma unroll
-        for (int o = 0; o < kOWide; ++o)
-            if (o < O) pbar[lc.w_off + (int64_t)O * i + o] += dWacc[o];
     }
 }
 
 // ---------------------------------------------------------------------------
 // launchers
 static inline size_t wideout_lds(const LayerConst& h, size_t es) { return es * (size_t)(h.G * h.I + h.I) * kKT; }
+static inline unsigned col_tiles(int64_t K) {
+    const int64_t t = (K + kKT - 1) / kKT;
+    return (unsigned)(t < 65535 ? t : 65535);
+}
 
 template <typename T>
 hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
                                 int64_t K, hipStream_t st) {
-    const int nblk = (h.I + kBlock - 1) / kBlock;
+    const int nblk = (h.I + kWIB - 1) / kWIB;
+    const dim3 grid(nblk, (unsigned)(K < 65535 ? K : 65535));
+#define KAN_WI(PATH) hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH>), grid, dim3(kWIB), 0, st, lc, p, x, slab, K)
     switch (h.path) {
-    case PATH_REC_CORR:
-        hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH_REC_CORR>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, slab, K);
-        break;
-    case PATH_REC:
-        hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH_REC>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, slab, K);
-        break;
-    default:
-        hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH_DIRECT>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, slab, K);
+    case PATH_REC_CORR: KAN_WI(PATH_REC_CORR); break;
+    case PATH_REC: KAN_WI(PATH_REC); break;
+    default: KAN_WI(PATH_DIRECT);
     }
+#undef KAN_WI
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t n = (int64_t)h.O * K;
@@ -372,65 +419,55 @@ hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const
 template <typename T>
 hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                                  hipStream_t st) {
-    const int nblk = (h.O + kBlock - 1) / kBlock;
+    const dim3 grid((h.O + kWOB - 1) / kWOB, col_tiles(K));
     const size_t lds = wideout_lds(h, sizeof(T));
+#define KAN_WO(PATH) hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH>), grid, dim3(kWOB), lds, st, lc, p, x, y, K)
     switch (h.path) {
-    case PATH_REC_CORR:
-        hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH_REC_CORR>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, y, K);
-        break;
-    case PATH_REC:
-        hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH_REC>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, y, K);
-        break;
-    default:
-        hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH_DIRECT>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, y, K);
+    case PATH_REC_CORR: KAN_WO(PATH_REC_CORR); break;
+    case PATH_REC: KAN_WO(PATH_REC); break;
+    default: KAN_WO(PATH_DIRECT);
     }
+#undef KAN_WO
     return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
                                  T* xb, T* pbar, T* slab, int64_t K, hipStream_t st) {
-    const int nblk = (h.O + kBlock - 1) / kBlock;
-    const size_t lds = wideout_lds(h, sizeof(T)) + sizeof(T) * (size_t)(kBlock / kWave) * (h.G * h.I + h.I) * kKT;
-    const int64_t nfin = (int64_t)h.I * K;
+    (void)slab;
+    const dim3 gp((h.O + kWOB - 1) / kWOB, h.I), gx(h.I, col_tiles(K));
+#define KAN_WOV(PATH)                                                                                              \
+    do {                                                                                                           \
+        if (pbar) hipLaunchKernelGGL((kd_vjp_wideout_param_kernel<T, PATH>), gp, dim3(kWOB), 0, st, lc, x, yb, pbar, \
+                                     K);                                                                          \
+        if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xbar_kernel<T, PATH>), gx, dim3(kWOX), 0, st, lc, p, x, yb, xb,   \
+                                   K);                                                                            \
+    } while (0)
     switch (h.path) {
-    case PATH_REC_CORR:
-        hipLaunchKernelGGL((kd_vjp_wideout_kernel<T, PATH_REC_CORR>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, yb,
-                           pbar, slab, K);
-        hipLaunchKernelGGL((kd_vjp_wideout_finalize_kernel<T, PATH_REC_CORR>), dim3(grid_for(nfin, kBlock, 1 << 30)),
-                           dim3(kBlock), 0, st, lc, x, slab, nblk, xb, K);
-        break;
-    case PATH_REC:
-        hipLaunchKernelGGL((kd_vjp_wideout_kernel<T, PATH_REC>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, yb, pbar,
-                           slab, K);
-        hipLaunchKernelGGL((kd_vjp_wideout_finalize_kernel<T, PATH_REC>), dim3(grid_for(nfin, kBlock, 1 << 30)),
-                           dim3(kBlock), 0, st, lc, x, slab, nblk, xb, K);
-        break;
-    default:
-        hipLaunchKernelGGL((kd_vjp_wideout_kernel<T, PATH_DIRECT>), dim3(nblk), dim3(kBlock), lds, st, lc, p, x, yb,
-                           pbar, slab, K);
-        hipLaunchKernelGGL((kd_vjp_wideout_finalize_kernel<T, PATH_DIRECT>), dim3(grid_for(nfin, kBlock, 1 << 30)),
-                           dim3(kBlock), 0, st, lc, x, slab, nblk, xb, K);
+    case PATH_REC_CORR: KAN_WOV(PATH_REC_CORR); break;
+    case PATH_REC: KAN_WOV(PATH_REC); break;
+    default: KAN_WOV(PATH_DIRECT);
     }
+#undef KAN_WOV
     return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
                                 T* pbar, int64_t K, hipStream_t st) {
-    const int nblk = (h.I + kBlock - 1) / kBlock;
+    const int nblk = (h.I + kWIB - 1) / kWIB;
+    const int np = pbar ? h.O : 0;
+    const int nx = xb ? (int)(K < 4096 ? K : 4096) : 0;
+    if (np + nx == 0) return hipSuccess;
+    const dim3 grid(nblk, np + nx);
+#define KAN_WIV(PATH)                                                                                              \
+    hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH>), grid, dim3(kWIB), 0, st, lc, p, x, yb, xb, pbar, K, np, nx)
     switch (h.path) {
-    case PATH_REC_CORR:
-        hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH_REC_CORR>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, yb, xb,
-                           pbar, K);
-        break;
-    case PATH_REC:
-        hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH_REC>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, yb, xb, pbar, K);
-        break;
-    default:
-        hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH_DIRECT>), dim3(nblk), dim3(kBlock), 0, st, lc, p, x, yb, xb,
-                           pbar, K);
+    case PATH_REC_CORR: KAN_WIV(PATH_REC_CORR); break;
+    case PATH_REC: KAN_WIV(PATH_REC); break;
+    default: KAN_WIV(PATH_DIRECT);
     }
+#undef KAN_WIV
     return hipGetLastError();
 }
 

@@ -234,9 +234,7 @@ int64_t wide_slab_elems(const kanode_handle* h, int64_t B) {
     int64_t m = 0;
     for (int l = 0; l < h->n_layers; ++l) {
         const LayerConst& c = h->hlc[l];
-        if (h->kind[l] == KIND_WIDE_IN) m = std::max<int64_t>(m, (int64_t)((c.I + 255) / 256) * B * c.O);
-        if (h->kind[l] == KIND_WIDE_OUT)
-            m = std::max<int64_t>(m, (int64_t)((c.O + 255) / 256) * B * (c.G * c.I + c.I));
+        if (h->kind[l] == KIND_WIDE_IN) m = std::max<int64_t>(m, (int64_t)((c.I + 63) / 64) * B * c.O);
     }
     return m;
 }
@@ -634,7 +632,7 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
             h->kind[l] = KIND_COL;
         } else if (lc.O <= kan::kWideOMax) {
             h->kind[l] = KIND_WIDE_IN;
-        } else if (rows * kan::kWideKT * h->esize * (1 + 4) <= 150 * 1024) {
+        } else if (rows * kan::kWideKT * h->esize <= 150 * 1024) {
             h->kind[l] = KIND_WIDE_OUT;
         } else {
             return bail(fail(h, KANODE_ERR_UNSUPPORTED,
