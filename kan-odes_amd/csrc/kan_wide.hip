@@ -13,8 +13,9 @@
 //   wide-out (O large): grid (row chunk of 256, column tile of 8); the block stages the
 //            small basis of its tile in LDS; C[o + O*c] reads are coalesced over o.
 // Pullbacks: wide-out parameters -- thread o owns dC[o, :], dW[o, :] (no reduction);
-// wide-out input cotangent -- one workgroup per (input i, column tile) forms the G + 1
-// dot products Σ_o C[o, g + G i] ȳ[o, k] (coalesced over o, wave sums) and then x̄[i, k];
+// wide-out input cotangent -- one workgroup per (input i, basis row r, column tile) forms
+// Σ_o C[o, r + G i] ȳ[o, k] (coalesced over o, ordered block sum) into a slab, then one
+// thread per (i, k) turns the G + 1 sums into x̄[i, k];
 // wide-in -- lane i owns dC[:, g + G i], dW[:, i] (accumulated in its own LDS slots over
 // the columns) and x̄[i, :].  Every reduction runs in a fixed order (bitwise reproducible).
 #include "kan_common.hpp"
@@ -56,20 +57,24 @@ struct Basis1 {
 
 // ---------------------------------------------------------------------------
 // wide-in forward: grid (ceil(I/64), columns); slab[(chunk*K + k)*O + o] = Σ_{i in chunk} (C φ + W sw)
-constexpr int kWIB = 64;   // inputs per wide-in workgroup (one wave)
+constexpr int kWIB = 64;   // inputs per wide-in workgroup (one per lane)
+constexpr int kSW = 4;     // waves per workgroup splitting the inner loop (latency: more loads in flight)
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kWIB)
+__global__ void __launch_bounds__(kWIB * kSW)
 kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                      T* __restrict__ slab, int64_t K) {
+    __shared__ T red[kSW][kOWide];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
-    const int i = blockIdx.x * kWIB + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int i = blockIdx.x * kWIB + lane;
     const bool valid = i < I;
     for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+        // wave w takes the knots g ≡ w (mod kSW); the base term goes to wave G mod kSW
         T acc[kOWide];
 #pragma unroll
         for (int o = 0; o < kOWide; ++o) acc[o] = T(0);
@@ -80,12 +85,13 @@ kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p
             for (int g = 0; g < G; ++g) {
                 T z, aux;
                 const T phi = bs.next(M, lc, g, z, aux);
+                if ((g % kSW) != w) continue;
                 const T* Cc = C + (int64_t)O * (g + (int64_t)G * i);
 #pragma unroll
                 for (int o = 0; o < kOWide; ++o)
                     if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
             }
-            if (lc.use_base) {
+            if (lc.use_base && w == G % kSW) {
                 const T sw = swish<T>(M, xi);
                 const T* Wi = W + (int64_t)O * i;
 #pragma unroll
@@ -97,9 +103,17 @@ kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p
         for (int o = 0; o < kOWide; ++o) {
             if (o < O) {
                 const T sum = wave_sum(acc[o]);
-                if (threadIdx.x == 0) slab[((int64_t)blockIdx.x * K + k) * O + o] = sum;
+                if (lane == 0) red[w][o] = sum;
             }
         }
+        __syncthreads();
+        if (threadIdx.x < O) {
+            T sum = red[0][threadIdx.x];
+#pragma unroll
+            for (int v = 1; v < kSW; ++v) sum += red[v][threadIdx.x];
+            slab[((int64_t)blockIdx.x * K + k) * O + threadIdx.x] = sum;
+        }
+        __syncthreads();
     }
 }
 
@@ -141,15 +155,17 @@ __device__ __forceinline__ void stage_tile_basis(const Math<T>& M, const LayerCo
 }
 
 // ---------------------------------------------------------------------------
-// wide-out forward: grid (ceil(O/64), column tiles); thread o contracts its row of C
-// against the tile's basis (one-wave workgroups: at a few columns the launch is latency
-// bound, so more workgroups and more loads in flight per lane beat bigger blocks).
+// wide-out forward: grid (ceil(O/64), column tiles); lane o contracts its row of C against
+// the tile's basis, the kSW waves of the workgroup splitting the G·I columns of C (the
+// launch is latency bound at a few trajectories: more workgroups and more loads in flight
+// beat longer per-lane loops); partials are summed in wave order through LDS.
 constexpr int kWOB = 64;
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kWOB)
+__global__ void __launch_bounds__(kWOB * kSW)
 kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                       T* __restrict__ y, int64_t K) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    __shared__ T red[kSW][kKT][kWOB];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
@@ -159,53 +175,68 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
     T* swL = phiL + (int64_t)GI * kKT;              // [I][kKT]
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int o = blockIdx.x * kWOB + lane;
     for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
         const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
         __syncthreads();
         stage_tile_basis<T, PATH>(M, lc, x, k0, kt, phiL, swL);
         __syncthreads();
-        if (o < O) {
-            T acc[kKT], bas[kKT];
+        T acc[kKT];
 #pragma unroll
-            for (int kk = 0; kk < kKT; ++kk) { acc[kk] = T(0); bas[kk] = T(0); }
+        for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
+        if (o < O) {
 #pragma unroll 4
-            for (int c = 0; c < GI; ++c) {
+            for (int c = w; c < GI; c += kSW) {
                 const T cv = C[o + (int64_t)O * c];
 #pragma unroll
                 for (int kk = 0; kk < kKT; ++kk) acc[kk] = kfma<T>(cv, phiL[c * kKT + kk], acc[kk]);
             }
             if (lc.use_base) {
-#pragma unroll 4
-                for (int i = 0; i < I; ++i) {
+#pragma unroll 2
+                for (int i = w; i < I; i += kSW) {
                     const T wv = W[o + (int64_t)O * i];
 #pragma unroll
-                    for (int kk = 0; kk < kKT; ++kk) bas[kk] = kfma<T>(wv, swL[i * kKT + kk], bas[kk]);
+                    for (int kk = 0; kk < kKT; ++kk) acc[kk] = kfma<T>(wv, swL[i * kKT + kk], acc[kk]);
                 }
             }
+        }
 #pragma unroll
-            for (int kk = 0; kk < kKT; ++kk)
-                if (kk < kt) y[(int64_t)O * (k0 + kk) + o] = lc.use_base ? acc[kk] + bas[kk] : acc[kk];
+        for (int kk = 0; kk < kKT; ++kk) red[w][kk][lane] = acc[kk];
+        __syncthreads();
+        if (w == 0 && o < O) {
+#pragma unroll
+            for (int kk = 0; kk < kKT; ++kk) {
+                if (kk < kt) {
+                    T sum = red[0][kk][lane];
+#pragma unroll
+                    for (int v = 1; v < kSW; ++v) sum += red[v][kk][lane];
+                    y[(int64_t)O * (k0 + kk) + o] = sum;
+                }
+            }
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// wide-out pullback, parameters: workgroup (row chunk, input i); thread o owns
-// dC[o, g + G i] (g < G) and dW[o, i] in registers over all columns, then adds them to pbar
-// once (coalesced over o).  The basis of input i is staged in LDS kWOPK columns at a time.
+// wide-out pullback, parameters: workgroup (row chunk, input i); lane o owns
+// dC[o, g + G i] (g < G) and dW[o, i] in registers, the kSW waves taking every kSW-th
+// column; the wave partials are summed in order through LDS and added to pbar once
+// (coalesced over o).  The basis of input i is staged in LDS kWOPK columns at a time.
 constexpr int kWOPK = 128;
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kWOB)
+__global__ void __launch_bounds__(kWOB * kSW)
 kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ ybar,
                             T* __restrict__ pbar, int64_t K) {
     __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
+    __shared__ T red[kSW][kWOB];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const int i = blockIdx.y;
-    const int o = blockIdx.x * kWOB + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int o = blockIdx.x * kWOB + lane;
     const bool base = lc.use_base != 0;
     T acc[kMaxGrid + 1];
 #pragma unroll
@@ -213,7 +244,7 @@ kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restr
     for (int64_t k0 = 0; k0 < K; k0 += kWOPK) {
         const int kt = (int)((K - k0) < kWOPK ? (K - k0) : kWOPK);
         __syncthreads();
-        for (int kk = threadIdx.x; kk < kt; kk += kWOB) {
+        for (int kk = threadIdx.x; kk < kt; kk += blockDim.x) {
             const T xi = x[(int64_t)I * (k0 + kk) + i];
             Basis1<T, PATH> bs;
             bs.init(M, lc, xi);
@@ -225,7 +256,8 @@ kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restr
         }
         __syncthreads();
         if (o < O) {
-            for (int kk = 0; kk < kt; ++kk) {
+#pragma unroll 2
+            for (int kk = w; kk < kt; kk += kSW) {
                 const T yb = ybar[(int64_t)O * (k0 + kk) + o];
 #pragma unroll
                 for (int r = 0; r < kMaxGrid; ++r)
@@ -234,129 +266,170 @@ kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restr
             }
         }
     }
-    if (o >= O) return;
     T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
 #pragma unroll
-    for (int r = 0; r < kMaxGrid; ++r)
-        if (r < G) dC[(int64_t)O * r] += acc[r];
-    if (base) pbar[lc.w_off + o + (int64_t)O * i] += acc[kMaxGrid];
+    for (int r = 0; r <= kMaxGrid; ++r) {
+        if (r < G || (r == kMaxGrid && base)) {
+            __syncthreads();
+            red[w][lane] = acc[r];
+            __syncthreads();
+            if (w == 0 && o < O) {
+                T sum = red[0][lane];
+#pragma unroll
+                for (int v = 1; v < kSW; ++v) sum += red[v][lane];
+                if (r < G) dC[(int64_t)O * r] += sum;
+                else pbar[lc.w_off + o + (int64_t)O * i] += sum;
+            }
+        }
+    }
 }
 
-// wide-out pullback, input cotangent: workgroup (i, column tile).  Waves take the rows
-// r < G (C[:, g + G i]) and r = G (W[:, i]) and form Σ_o row[o] ȳ[o, k] (lanes stride over
-// o, coalesced; one wave sum per column); then lane kk turns them into x̄[i, k0 + kk]
-// through the basis / normalizer / swish rrules (utils.jl:15-21, NNlib).
+// wide-out pullback, input cotangent, in two passes:
+//   dot:  workgroup (i·R + r, column tile), R = G + use_base: S[i, r, k] = Σ_o row[o] ȳ[o, k]
+//         with row = C[:, r + G i] (r < G) or W[:, i] (r = G); threads stride over o
+//         (coalesced), then an ordered block reduction per column;
+//   fin:  thread (i, k): x̄[i, k] from S through the basis / normalizer / swish rrules
+//         (utils.jl:15-21, NNlib).
 constexpr int kWOX = 256;
-template <typename T, int PATH>
+template <typename T>
 __global__ void __launch_bounds__(kWOX)
-kd_vjp_wideout_xbar_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                           const T* __restrict__ ybar, T* __restrict__ xbar, int64_t K) {
-    __shared__ T S[(kMaxGrid + 1) * kKT];
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
+kd_vjp_wideout_dot_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ ybar,
+                          T* __restrict__ S, int64_t K) {
+    __shared__ T red[kWOX / kWave][kKT];
     const LayerConst& lc = *lcp;
-    const int I = lc.I, O = lc.O, G = lc.G;
-    const int i = blockIdx.x;
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave, nw = blockDim.x / kWave;
-    const int rows = G + (lc.use_base ? 1 : 0);
+    const int O = lc.O, G = lc.G;
+    const int R = G + (lc.use_base ? 1 : 0);
+    const int i = blockIdx.x / R, r = blockIdx.x - i * R;
+    const T* __restrict__ row = r < G ? p + lc.p_off + (int64_t)O * (r + (int64_t)G * i) : p + lc.w_off + (int64_t)O * i;
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
         const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
-        for (int r = wid; r < rows; r += nw) {
-            const T* __restrict__ row = r < G ? p + lc.p_off + (int64_t)O * (r + (int64_t)G * i)
-                                              : p + lc.w_off + (int64_t)O * i;
-            T acc[kKT];
+        T acc[kKT];
 #pragma unroll
-            for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
-#pragma unroll 2
-            for (int o = lane; o < O; o += kWave) {
-                const T cv = row[o];
+        for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
+#pragma unroll 4
+        for (int o = threadIdx.x; o < O; o += kWOX) {
+            const T cv = row[o];
 #pragma unroll
-                for (int kk = 0; kk < kKT; ++kk)
-                    if (kk < kt) acc[kk] = kfma<T>(cv, ybar[(int64_t)O * (k0 + kk) + o], acc[kk]);
-            }
+            for (int kk = 0; kk < kKT; ++kk)
+                if (kk < kt) acc[kk] = kfma<T>(cv, ybar[(int64_t)O * (k0 + kk) + o], acc[kk]);
+        }
 #pragma unroll
-            for (int kk = 0; kk < kKT; ++kk) {
-                if (kk < kt) {
-                    const T s = wave_sum(acc[kk]);
-                    if (lane == 0) S[r * kKT + kk] = s;
-                }
-            }
+        for (int kk = 0; kk < kKT; ++kk) {
+            const T s = wave_sum(acc[kk]);
+            if (lane == 0) red[wid][kk] = s;
         }
         __syncthreads();
         if (threadIdx.x < kt) {
-            const int kk = threadIdx.x;
-            const T xi = x[(int64_t)I * (k0 + kk) + i];
-            Basis1<T, PATH> bs;
-            bs.init(M, lc, xi);
-            const T invh = T(lc.invh);
-            T nbar = T(0);
-            for (int g = 0; g < G; ++g) {
-                T z, aux;
-                const T phi = bs.next(M, lc, g, z, aux);
-                nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, S[g * kKT + kk]) * invh;
-            }
-            T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
-            if (lc.use_base) {
-                T sw, dsw;
-                swish_and_grad<T>(M, xi, sw, dsw);
-                xb = xb + S[G * kKT + kk] * dsw;
-            }
-            xbar[(int64_t)I * (k0 + kk) + i] = xb;
+            T s = red[0][threadIdx.x];
+#pragma unroll
+            for (int w = 1; w < kWOX / kWave; ++w) s += red[w][threadIdx.x];
+            S[((int64_t)blockIdx.x * K) + k0 + threadIdx.x] = s;
         }
         __syncthreads();
     }
 }
 
-// ---------------------------------------------------------------------------
-// wide-in pullback, grid (ceil(I/64), np + nx):
-//   blockIdx.y <  np (= O when pbar): lane i, row o = blockIdx.y owns dC[o, g + G i] (g < G)
-//                  and dW[o, i] in registers over all columns, added to pbar once;
-//   blockIdx.y >= np: lane i forms x̄[i, k] for the columns k = y - np (+ nx, ...): the G + 1
-//                  dot products Σ_o C[o, g + G i] ȳ[o, k] (O <= 16, registers) then the
-//                  basis / normalizer / swish rrules.
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kWIB)
+__global__ void __launch_bounds__(kBlock)
+kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ S,
+                           T* __restrict__ xbar, int64_t K) {
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const LayerConst& lc = *lcp;
+    const int I = lc.I, G = lc.G;
+    const int R = G + (lc.use_base ? 1 : 0);
+    const T invh = T(lc.invh);
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < (int64_t)I * K;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = idx / I;
+        const int i = (int)(idx - k * I);
+        const T* __restrict__ Si = S + (int64_t)i * R * K + k;
+        const T xi = x[idx];
+        Basis1<T, PATH> bs;
+        bs.init(M, lc, xi);
+        T nbar = T(0);
+        for (int g = 0; g < G; ++g) {
+            T z, aux;
+            const T phi = bs.next(M, lc, g, z, aux);
+            nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, Si[(int64_t)g * K]) * invh;
+        }
+        T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
+        if (lc.use_base) {
+            T sw, dsw;
+            swish_and_grad<T>(M, xi, sw, dsw);
+            xb = xb + Si[(int64_t)G * K] * dsw;
+        }
+        xbar[idx] = xb;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// wide-in pullback, grid (ceil(I/64), np + nx), lane = input i:
+//   blockIdx.y <  np (= O when pbar): row o = blockIdx.y; lane i owns dC[o, g + G i] (g < G)
+//                  and dW[o, i] in registers, the kSW waves taking every kSW-th column; the
+//                  wave partials are summed in order through LDS and added to pbar once;
+//   blockIdx.y >= np: wave w forms x̄[i, k] for the columns k = (y - np)·kSW + w (stride
+//                  nx·kSW): the G + 1 dot products Σ_o C[o, g + G i] ȳ[o, k] (O <= 16,
+//                  registers) then the basis / normalizer / swish rrules.
+template <typename T, int PATH>
+__global__ void __launch_bounds__(kWIB * kSW)
 kd_vjp_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                      const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
                      int nx) {
+    __shared__ T red[kSW][kWIB];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const T* __restrict__ C = p + lc.p_off;
     const T* __restrict__ W = p + lc.w_off;
-    const int i = blockIdx.x * kWIB + threadIdx.x;
-    if (i >= I) return;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int i = blockIdx.x * kWIB + lane;
+    const bool valid = i < I;
     const bool base = lc.use_base != 0;
     if ((int)blockIdx.y < np) {
         const int o = blockIdx.y;
-        T acc[kMaxGrid];
+        T acc[kMaxGrid + 1];
 #pragma unroll
-        for (int g = 0; g < kMaxGrid; ++g) acc[g] = T(0);
-        T accw = T(0);
-        for (int64_t k = 0; k < K; ++k) {
-            const T xi = x[(int64_t)I * k + i];
-            const T yb = ybar[(int64_t)O * k + o];
-            Basis1<T, PATH> bs;
-            bs.init(M, lc, xi);
+        for (int g = 0; g <= kMaxGrid; ++g) acc[g] = T(0);
+        if (valid) {
+            for (int64_t k = w; k < K; k += kSW) {
+                const T xi = x[(int64_t)I * k + i];
+                const T yb = ybar[(int64_t)O * k + o];
+                Basis1<T, PATH> bs;
+                bs.init(M, lc, xi);
 #pragma unroll
-            for (int g = 0; g < kMaxGrid; ++g) {
-                if (g < G) {
-                    T z, aux;
-                    acc[g] = kfma<T>(yb, bs.next(M, lc, g, z, aux), acc[g]);
+                for (int g = 0; g < kMaxGrid; ++g) {
+                    if (g < G) {
+                        T z, aux;
+                        acc[g] = kfma<T>(yb, bs.next(M, lc, g, z, aux), acc[g]);
+                    }
                 }
+                if (base) acc[kMaxGrid] = kfma<T>(yb, swish<T>(M, xi), acc[kMaxGrid]);
             }
-            if (base) accw = kfma<T>(yb, swish<T>(M, xi), accw);
         }
         T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
 #pragma unroll
-        for (int g = 0; g < kMaxGrid; ++g)
-            if (g < G) dC[(int64_t)O * g] += acc[g];
-        if (base) pbar[lc.w_off + o + (int64_t)O * i] += accw;
+        for (int g = 0; g <= kMaxGrid; ++g) {
+            if (g < G || (g == kMaxGrid && base)) {
+                __syncthreads();
+                red[w][lane] = acc[g];
+                __syncthreads();
+                if (w == 0 && valid) {
+                    T sum = red[0][lane];
+#pragma unroll
+                    for (int v = 1; v < kSW; ++v) sum += red[v][lane];
+                    if (g < G) dC[(int64_t)O * g] += sum;
+                    else pbar[lc.w_off + o + (int64_t)O * i] += sum;
+                }
+            }
+        }
         return;
     }
+    if (!valid) return;
     const T invh = T(lc.invh);
-    for (int64_t k = (int)blockIdx.y - np; k < K; k += nx) {
+    for (int64_t k = (int64_t)((int)blockIdx.y - np) * kSW + w; k < K; k += (int64_t)nx * kSW) {
         T yb[kOWide];
 #pragma unroll
         for (int o = 0; o < kOWide; ++o) yb[o] = o < O ? ybar[(int64_t)O * k + o] : T(0);
@@ -401,7 +474,7 @@ hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const
                                 int64_t K, hipStream_t st) {
     const int nblk = (h.I + kWIB - 1) / kWIB;
     const dim3 grid(nblk, (unsigned)(K < 65535 ? K : 65535));
-#define KAN_WI(PATH) hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH>), grid, dim3(kWIB), 0, st, lc, p, x, slab, K)
+#define KAN_WI(PATH) hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH>), grid, dim3(kWIB * kSW), 0, st, lc, p, x, slab, K)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WI(PATH_REC_CORR); break;
     case PATH_REC: KAN_WI(PATH_REC); break;
@@ -421,7 +494,7 @@ hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, cons
                                  hipStream_t st) {
     const dim3 grid((h.O + kWOB - 1) / kWOB, col_tiles(K));
     const size_t lds = wideout_lds(h, sizeof(T));
-#define KAN_WO(PATH) hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH>), grid, dim3(kWOB), lds, st, lc, p, x, y, K)
+#define KAN_WO(PATH) hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH>), grid, dim3(kWOB * kSW), lds, st, lc, p, x, y, K)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WO(PATH_REC_CORR); break;
     case PATH_REC: KAN_WO(PATH_REC); break;
@@ -434,14 +507,16 @@ hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, cons
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
                                  T* xb, T* pbar, T* slab, int64_t K, hipStream_t st) {
-    (void)slab;
-    const dim3 gp((h.O + kWOB - 1) / kWOB, h.I), gx(h.I, col_tiles(K));
+    const int R = h.G + (h.use_base ? 1 : 0);
+    const dim3 gp((h.O + kWOB - 1) / kWOB, h.I), gd(h.I * R, col_tiles(K));
+    const unsigned gf = grid_for((int64_t)h.I * K, kBlock, kGridCap);
+    if (xb) hipLaunchKernelGGL((kd_vjp_wideout_dot_kernel<T>), gd, dim3(kWOX), 0, st, lc, p, yb, slab, K);
 #define KAN_WOV(PATH)                                                                                              \
     do {                                                                                                           \
-        if (pbar) hipLaunchKernelGGL((kd_vjp_wideout_param_kernel<T, PATH>), gp, dim3(kWOB), 0, st, lc, x, yb, pbar, \
+        if (pbar) hipLaunchKernelGGL((kd_vjp_wideout_param_kernel<T, PATH>), gp, dim3(kWOB * kSW), 0, st, lc, x, yb, pbar, \
                                      K);                                                                          \
-        if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xbar_kernel<T, PATH>), gx, dim3(kWOX), 0, st, lc, p, x, yb, xb,   \
-                                   K);                                                                            \
+        if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xfin_kernel<T, PATH>), dim3(gf), dim3(kBlock), 0, st, lc, x, slab, \
+                                   xb, K);                                                                        \
     } while (0)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WOV(PATH_REC_CORR); break;
@@ -457,11 +532,12 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
                                 T* pbar, int64_t K, hipStream_t st) {
     const int nblk = (h.I + kWIB - 1) / kWIB;
     const int np = pbar ? h.O : 0;
-    const int nx = xb ? (int)(K < 4096 ? K : 4096) : 0;
+    const int64_t kc = K < 4096 ? K : 4096;
+    const int nx = xb ? (int)((kc + kSW - 1) / kSW) : 0;
     if (np + nx == 0) return hipSuccess;
     const dim3 grid(nblk, np + nx);
 #define KAN_WIV(PATH)                                                                                              \
-    hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH>), grid, dim3(kWIB), 0, st, lc, p, x, yb, xb, pbar, K, np, nx)
+    hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH>), grid, dim3(kWIB * kSW), 0, st, lc, p, x, yb, xb, pbar, K, np, nx)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WIV(PATH_REC_CORR); break;
     case PATH_REC: KAN_WIV(PATH_REC); break;
