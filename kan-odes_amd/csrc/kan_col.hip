@@ -205,7 +205,7 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
         if (j < OL) {
             y[(int64_t)OL * k + j] = a;
             if (want_err) {
-                const double e = ::fma(sa.ec[sa.nk] * sc, (double)a, ev);
+                const double e = ::fma(stage_ec_last(sa) * sc, (double)a, ev);
                 const double sk = ::fma(sa.reltol, fmax(kabs((double)x0), kabs((double)yin)), sa.abstol);
                 const double r = e / sk;
                 eacc = ::fma(r, r, eacc);
@@ -388,7 +388,7 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
         if (j < N0) {
             lamJ[idx] = ybar;
             if (want_err) {
-                const double e = ::fma(sl.ec[sl.nk] * slc, (double)ybar, ev);
+                const double e = ::fma(stage_ec_last(sl) * slc, (double)ybar, ev);
                 const double sk = ::fma(sl.reltol, fmax(kabs((double)l0), kabs((double)lj)), sl.abstol);
                 const double r = e / sk;
                 eacc = ::fma(r, r, eacc);

@@ -33,6 +33,16 @@ struct StageArgs {
 };
 __device__ __forceinline__ double stage_scale(const double* cscale) { return cscale ? *cscale : 1.0; }
 __device__ __forceinline__ bool stage_skip(const int32_t* skip) { return skip && *skip; }
+// ec[nk] with static indices only: a runtime index into the by-value StageArgs would make the
+// compiler copy the whole struct to scratch
+template <typename SA>
+__device__ __forceinline__ double stage_ec_last(const SA& sa) {
+    double e = 0.0;
+#pragma unroll
+    for (int j = 0; j <= kMaxStages; ++j)
+        if (j == sa.nk) e = sa.ec[j];
+    return e;
+}
 template <typename T>
 hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st);
 // per-block partials into `slab` (<= slab_blocks rows), then out[0] = ordered total

@@ -328,6 +328,53 @@ __device__ __forceinline__ kd2 ld_stream(const double* p) {
     return *reinterpret_cast<const kd2*>(p);
 #endif
 }
+
+// a[k] += Σ_{j<N} (sc·c_j)·K_j[k], e[k] += Σ_{j<N} (sc·ec_j)·K_j[k] (E) over the NP pairs of one
+// row at offset off: all N·NP loads are issued before the first FMA.  (An unrolled loop over
+// j < kMaxStages guarded by j < nk compiles to one branch per array, and the loads, which
+// cannot move above their guard, then wait one after the other.)
+template <int N, int NP, bool E>
+__device__ __forceinline__ void stage_sum_n(const StageArgs<double>& sa, int64_t off, double sc, kd2 (&a)[NP],
+                                            kd2 (&e)[NP]) {
+    kd2 v[N][NP];
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v[j][k] = ld_stream(sa.k[j] + off + 128 * k);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double cj = sa.c[j] * sc;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            a[k].x = ::fma(cj, v[j][k].x, a[k].x);
+            a[k].y = ::fma(cj, v[j][k].y, a[k].y);
+        }
+        if constexpr (E) {
+            const double ej = sa.ec[j] * sc;
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                e[k].x = ::fma(ej, v[j][k].x, e[k].x);
+                e[k].y = ::fma(ej, v[j][k].y, e[k].y);
+            }
+        }
+    }
+}
+template <int NP, bool E>
+__device__ __forceinline__ void stage_sum(const StageArgs<double>& sa, int64_t off, double sc, kd2 (&a)[NP],
+                                          kd2 (&e)[NP]) {
+    switch (sa.nk) {
+    case 1: stage_sum_n<1, NP, E>(sa, off, sc, a, e); break;
+    case 2: stage_sum_n<2, NP, E>(sa, off, sc, a, e); break;
+    case 3: stage_sum_n<3, NP, E>(sa, off, sc, a, e); break;
+    case 4: stage_sum_n<4, NP, E>(sa, off, sc, a, e); break;
+    case 5: stage_sum_n<5, NP, E>(sa, off, sc, a, e); break;
+    case 6: stage_sum_n<6, NP, E>(sa, off, sc, a, e); break;
+    case 7: stage_sum_n<7, NP, E>(sa, off, sc, a, e); break;
+    case 8: stage_sum_n<8, NP, E>(sa, off, sc, a, e); break;
+    default: break;
+    }
+}
+static_assert(kMaxStages == 8, "stage_sum covers nk <= 8");
 __device__ __forceinline__ void st_stream(double* p, kd2 v) {
 #if KAN_PP_NT
     __builtin_nontemporal_store(v, reinterpret_cast<kd2*>(p));
@@ -543,6 +590,10 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 #ifndef KAN_VJP_WPE
 #define KAN_VJP_WPE 3
 #endif
+#ifndef KAN_VJP_STG_WPE
+#define KAN_VJP_STG_WPE 3
+#endif
+
 constexpr int kVjpBlock = KAN_VJP_BLOCK;
 // Nx = 128·NP, one wave per trajectory row (as fk_rhs_pp_wave_kernel): u and λ by
 // nontemporal 16-B loads, λ's stencil neighbours by wave rotation, λᵀJ by
@@ -554,7 +605,7 @@ constexpr int kVjpBlock = KAN_VJP_BLOCK;
 // to lam_out when non-null); with err_slab the λ error Σ (e/sk)², e = Σ sl.ec_j sl.k_j +
 // sl.ec_nk λᵀJ, sk = abstol + reltol·max(|lam|,|λs|), is block-summed into err_slab[block].
 template <int NORM, int PATH, int GT, int NP, bool STG>
-__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VJP_WPE)))
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(STG ? KAN_VJP_STG_WPE : KAN_VJP_WPE)))
 fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                       const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
@@ -602,33 +653,28 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                 l0[k] = lv[k];
                 ev[k] = kd2{0.0, 0.0};
             }
+            // Σ c_j k_j with the kernel-argument coefficients as the scalar operands, scaled
+            // once at the end (device step control: c_j·dt): premultiplied coefficients
+            // would occupy VGPRs for the whole kernel and push it into scratch
+            kd2 ta[NP], te[NP];
 #pragma unroll
-            for (int j = 0; j < kMaxStages; ++j) {
-                if (j < su.nk) {
-                    const double cj = su.c[j] * suc;
+            for (int k = 0; k < NP; ++k) ta[k] = kd2{0.0, 0.0};
+            stage_sum<NP, false>(su, rb, 1.0, ta, te);
 #pragma unroll
-                    for (int k = 0; k < NP; ++k) {
-                        const kd2 kj = ld_stream(su.k[j] + rb + 128 * k);
-                        uv[k].x = ::fma(cj, kj.x, uv[k].x);
-                        uv[k].y = ::fma(cj, kj.y, uv[k].y);
-                    }
-                }
+            for (int k = 0; k < NP; ++k) {
+                uv[k].x = ::fma(suc, ta[k].x, uv[k].x);
+                uv[k].y = ::fma(suc, ta[k].y, uv[k].y);
+                ta[k] = kd2{0.0, 0.0};
+                te[k] = kd2{0.0, 0.0};
             }
+            if (want_err) stage_sum<NP, true>(sl, rb, 1.0, ta, te);
+            else stage_sum<NP, false>(sl, rb, 1.0, ta, te);
 #pragma unroll
-            for (int j = 0; j < kMaxStages; ++j) {
-                if (j < sl.nk) {
-                    const double cj = sl.c[j] * slc, ej = sl.ec[j] * slc;
-#pragma unroll
-                    for (int k = 0; k < NP; ++k) {
-                        const kd2 kj = ld_stream(sl.k[j] + rb + 128 * k);
-                        lv[k].x = ::fma(cj, kj.x, lv[k].x);
-                        lv[k].y = ::fma(cj, kj.y, lv[k].y);
-                        if (want_err) {
-                            ev[k].x = ::fma(ej, kj.x, ev[k].x);
-                            ev[k].y = ::fma(ej, kj.y, ev[k].y);
-                        }
-                    }
-                }
+            for (int k = 0; k < NP; ++k) {
+                lv[k].x = ::fma(slc, ta[k].x, lv[k].x);
+                lv[k].y = ::fma(slc, ta[k].y, lv[k].y);
+                ev[k].x = slc * te[k].x;
+                ev[k].y = slc * te[k].y;
             }
             if (lam_out) {
 #pragma unroll
@@ -677,7 +723,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             o.y = a1 + x1b;
             st_stream(lamJ + rb + 128 * k, o);
             if (want_err) {
-                const double en = sl.ec[sl.nk] * slc;
+                const double en = stage_ec_last(sl) * slc;
                 const double ex = ::fma(en, o.x, ek.x), ey = ::fma(en, o.y, ek.y);
                 const double sx = ::fma(sl.reltol, fmax(kabs(l0k.x), kabs(lk.x)), sl.abstol);
                 const double sy = ::fma(sl.reltol, fmax(kabs(l0k.y), kabs(lk.y)), sl.abstol);
@@ -762,22 +808,8 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             y[k] = uv[k];
             e[k] = kd2{0.0, 0.0};
         }
-#pragma unroll
-        for (int j = 0; j < kMaxStages; ++j) {
-            if (j < sa.nk) {
-                const double cj = sa.c[j] * sac, ej = sa.ec[j] * sac;
-#pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    const kd2 kj = ld_stream(sa.k[j] + rb + 128 * k);
-                    y[k].x = ::fma(cj, kj.x, y[k].x);
-                    y[k].y = ::fma(cj, kj.y, y[k].y);
-                    if (want_err) {
-                        e[k].x = ::fma(ej, kj.x, e[k].x);
-                        e[k].y = ::fma(ej, kj.y, e[k].y);
-                    }
-                }
-            }
-        }
+        if (want_err) stage_sum<NP, true>(sa, rb, sac, y, e);
+        else stage_sum<NP, false>(sa, rb, sac, y, e);
         double rr[NP], rl[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -805,7 +837,7 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             st_stream(du + b * Nx + i, o);
             if (y_out) st_stream(y_out + b * Nx + i, y[k]);
             if (want_err) {
-                const double en = sa.ec[sa.nk] * sac;
+                const double en = stage_ec_last(sa) * sac;
                 const double ex = ::fma(en, o.x, e[k].x), ey = ::fma(en, o.y, e[k].y);
                 const double sx = ::fma(sa.reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), sa.abstol);
                 const double sy = ::fma(sa.reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), sa.abstol);
@@ -948,7 +980,10 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds, kVjpBlock);            \
-        grid = grid_for(B, kVjpBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        const char* ovs = getenv("KANODE_VJP_GRID");   /* experiments: grid override */           \
+        const int ovr = ovs ? atoi(ovs) : 0;                                                                     \
+        const int gcap = ovr > 0 ? ovr : cap;                                                                    \
+        grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kVjpBlock), lds, st,  \
                            lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
                            su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr);               \

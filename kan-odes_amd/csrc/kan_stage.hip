@@ -41,7 +41,7 @@ stage_error_kernel(const T* __restrict__ u, const T* __restrict__ y, const T* __
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j)
             if (j < sa.nk) e = ::fma(sa.ec[j] * sc, (double)sa.k[j][i], e);
-        e = ::fma(sa.ec[sa.nk] * sc, (double)du[i], e);
+        e = ::fma(stage_ec_last(sa) * sc, (double)du[i], e);
         const double sk = ::fma(sa.reltol, fmax(kabs((double)u[i]), kabs((double)y[i])), sa.abstol);
         const double r = e / sk;
         acc = ::fma(r, r, acc);
