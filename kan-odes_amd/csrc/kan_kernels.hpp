@@ -78,7 +78,25 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
                                   const double* p, double* tables, double cd, double co, int Nx, const double* u,
                                   const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
                                   double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
-                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build = true);
+                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build = true,
+                                  int* deferred_grid = nullptr);
+// The reductions of several adjoint stages launched with deferred_grid (their slabs in
+// separate regions) in one launch: job j sums slab_j rows into dp_j (= or +=) and err_slab_j
+// into err_out_j, each in the fixed order of vjp_finish_kernel.
+constexpr int kMaxFinishJobs = 8;
+struct FinishJob {
+    const double* slab;
+    const double* err_slab;
+    double* dp;
+    double* err_out;
+    int64_t nblk;
+    int32_t assign;
+    int32_t pad;
+};
+struct FinishJobs {
+    FinishJob j[kMaxFinishJobs];
+};
+hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, hipStream_t st);
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                              hipStream_t st);

@@ -774,6 +774,39 @@ vjp_finish_kernel(const double* __restrict__ slab, int64_t nblk, int64_t P, doub
     }
 }
 
+// vjp_finish_kernel over several jobs: blockIdx.y = job, blockIdx.x = q (< P: dp_q; == P: error)
+__global__ void __launch_bounds__(kBlock) vjp_finish_jobs_kernel(FinishJobs jobs, int64_t P) {
+    __shared__ double red[kBlock / kWave];
+    FinishJob jb{};
+#pragma unroll
+    for (int j = 0; j < kMaxFinishJobs; ++j)   // static indices: no copy of the argument to scratch
+        if (j == (int)blockIdx.y) jb = jobs.j[j];
+    const int64_t q = blockIdx.x;
+    if (q < P ? !jb.dp : !jb.err_out) return;
+    double s = 0.0;
+    if (q < P) {
+        for (int64_t b = threadIdx.x; b < jb.nblk; b += blockDim.x) s += jb.slab[b * P + q];
+    } else {
+        for (int64_t b = threadIdx.x; b < jb.nblk; b += blockDim.x) s += jb.err_slab[b];
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        if (q < P) jb.dp[q] = jb.assign ? t : jb.dp[q] + t;
+        else jb.err_out[0] = t;
+    }
+}
+
+hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, hipStream_t st) {
+    if (njobs <= 0) return hipSuccess;
+    if (njobs > kMaxFinishJobs) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vjp_finish_jobs_kernel, dim3((unsigned)P + 1, (unsigned)njobs), dim3(kBlock), 0, st, jobs, P);
+    return hipGetLastError();
+}
+
 // Runge-Kutta stage, fused (kanode_rhs_stage): the stage input y = u + Σ_j c_j k_j is
 // formed in registers from nontemporal loads of u and the k_j, the stencil
 // neighbours of y come from the wave rotations, du = f(y) as above.  Optionally y
@@ -1038,18 +1071,24 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
                                   const double* p, double* tables, double cd, double co, int Nx, const double* u,
                                   const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
                                   double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
-                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build) {
+                                  double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build,
+                                  int* deferred_grid) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
     if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st)) != hipSuccess) return e;
     int grid = 0;
-    // slab: [grid][P] dC/dW partials, then [grid] error partials (grid <= slab_blocks / 2)
+    // slab: [grid][P] dC/dW partials, then [grid] error partials (grid <= slab_blocks / 2);
+    // with deferred_grid the reduction is left to launch_vjp_finish_jobs
     const int cap = slab_blocks / 2;
     e = fk_vjp_pp_dispatch<true>(hpc, hlc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, cap, B, grid, su, sl,
                                  lam_out, err_out ? slab : nullptr, st);
     if (e != hipSuccess) return e;
     const int P = hlc.G + (hlc.use_base ? 1 : 0);
+    if (deferred_grid) {
+        *deferred_grid = grid;
+        return hipSuccess;
+    }
     if (!dp && !err_out) return hipSuccess;
     hipLaunchKernelGGL(vjp_finish_kernel, dim3((unsigned)(dp ? P : 0) + (err_out ? 1 : 0)), dim3(kBlock), 0, st,
                        slab, (int64_t)grid, (int64_t)P, dp, dp_assign ? 1 : 0,

@@ -60,6 +60,10 @@ struct kanode_handle {
     // table reuse inside one integrator solve (p constant): build each table set once
     bool hold_tables = false;
     bool built_phi = false, built_vjp = false;
+    // adjoint stages whose dp / error reductions wait for kanode_internal_vjp_flush (one launch)
+    void* defer_slab = nullptr;
+    kan::FinishJobs jobs{};
+    int njobs = 0;
     // stage input y for kanode_rhs_stage's unfused path
     void* stage_ws = nullptr;
     size_t stage_ws_bytes = 0;
@@ -518,10 +522,21 @@ kanode_status stage_args(kanode_handle* h, const kanode_stage* sg, kan::StageArg
     return KANODE_OK;
 }
 
+// one region of the deferred reduction slab: [grid][G+1] partials + [grid] error partials, grid <= kSlabBlocks/2
+constexpr size_t kDeferRegion = (size_t)(kSlabBlocks / 2) * (kan::kMaxGrid + 2);
+
+kanode_status vjp_flush(kanode_handle* h, hipStream_t st) {
+    if (h->njobs == 0) return KANODE_OK;
+    const int n = h->njobs;
+    h->njobs = 0;
+    HIP_TRY(h, kan::launch_vjp_finish_jobs(h->jobs, n, h->hlc[0].G + (h->hlc[0].use_base ? 1 : 0), st));
+    return KANODE_OK;
+}
+
 template <typename T>
 kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode_stage* state, const T* lam,
                           const kanode_stage* adj, T* lamJ, T* dp, int64_t B, hipStream_t st, bool dp_assign = false,
-                          const double* su_scale = nullptr, const double* sl_scale = nullptr) {
+                          const double* su_scale = nullptr, const double* sl_scale = nullptr, bool defer = false) {
     if (h->n_in != h->n_out) return fail(h, KANODE_ERR_INVALID_ARG, "adjoint stage needs an RHS with N_in == N_out");
     if (adj->want_error && !adj->error_sumsq) return fail(h, KANODE_ERR_INVALID_ARG, "want_error needs error_sumsq");
     kan::StageArgs<T> su, sl;
@@ -538,10 +553,34 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
             kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx)) {
             const double dx2 = h->spec.dx * h->spec.dx;
             const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+            double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
+            if (defer && (dp || err_out)) {
+                if (h->njobs == kan::kMaxFinishJobs && (s = vjp_flush(h, st)) != KANODE_OK) return s;
+                if (!h->defer_slab && hipMalloc(&h->defer_slab, kDeferRegion * sizeof(double) * kan::kMaxFinishJobs) !=
+                                          hipSuccess) {
+                    (void)hipGetLastError();
+                    h->defer_slab = nullptr;
+                    return fail(h, KANODE_ERR_ALLOC, "adjoint stage reduction slab");
+                }
+                double* region = (double*)h->defer_slab + (size_t)h->njobs * kDeferRegion;
+                int grid = 0;
+                HIP_TRY(h, kan::launch_fk_vjp_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
+                                                       (int)h->spec.nx, u, su, lam, sl, (double*)adj->y_out, lamJ,
+                                                       dp, dp_assign, err_out, region, kSlabBlocks, B, st,
+                                                       table_build(h, h->built_vjp), &grid));
+                kan::FinishJob& jb = h->jobs.j[h->njobs++];
+                jb.slab = region;
+                jb.err_slab = region + (int64_t)grid * (h->hlc[0].G + 1);
+                jb.dp = dp;
+                jb.err_out = err_out;
+                jb.nblk = grid;
+                jb.assign = dp_assign ? 1 : 0;
+                return KANODE_OK;
+            }
             HIP_TRY(h, kan::launch_fk_vjp_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                    (int)h->spec.nx, u, su, lam, sl, (double*)adj->y_out, lamJ, dp,
-                                                   dp_assign, adj->want_error ? (double*)adj->error_sumsq : nullptr,
-                                                   (double*)h->slab, kSlabBlocks, B, st, table_build(h, h->built_vjp)));
+                                                   dp_assign, err_out, (double*)h->slab, kSlabBlocks, B, st,
+                                                   table_build(h, h->built_vjp)));
             return KANODE_OK;
         }
     }
@@ -687,6 +726,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->dpc) (void)hipFree(h->dpc);
     if (h->stage_ws) (void)hipFree(h->stage_ws);
     if (h->dtable) (void)hipFree(h->dtable);
+    if (h->defer_slab) (void)hipFree(h->defer_slab);
     if (h->solve_cache) kanode_solution_free(h->solve_cache);
     delete h;
 }
@@ -921,16 +961,21 @@ double* kanode_internal_scratch(kanode_handle* h) { return (double*)h->slab; }
 void* kanode_internal_solution_cache(kanode_handle* h) { return &h->solve_cache; }
 int kanode_internal_scratch_rows(const kanode_handle*) { return kSlabBlocks; }
 kanode_status kanode_internal_check(kanode_handle* h) { return check_handle(h); }
+kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream) {
+    return vjp_flush(h, (hipStream_t)stream);
+}
+void kanode_internal_vjp_discard(kanode_handle* h) { h->njobs = 0; }
 kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
                                         const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
-                                        int64_t batch, void* stream, const double* su_scale, const double* sl_scale) {
+                                        int64_t batch, void* stream, const double* su_scale, const double* sl_scale,
+                                        bool defer) {
     kanode_status s = check_handle(h);
     if (s != KANODE_OK) return s;
     if (!p || !u || !lam || !state || !adj || batch < 1) return fail(h, KANODE_ERR_INVALID_ARG, "null argument or batch < 1");
     hipStream_t st = (hipStream_t)stream;
     if (h->spec.dtype == KANODE_F64)
         return vjp_stage_t<double>(h, (const double*)p, (const double*)u, state, (const double*)lam, adj, (double*)lamJ,
-                                   (double*)dp, batch, st, dp_assign, su_scale, sl_scale);
+                                   (double*)dp, batch, st, dp_assign, su_scale, sl_scale, defer);
     return vjp_stage_t<float>(h, (const float*)p, (const float*)u, state, (const float*)lam, adj, (float*)lamJ,
                               (float*)dp, batch, st, dp_assign, su_scale, sl_scale);
 }

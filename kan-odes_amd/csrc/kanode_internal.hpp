@@ -23,10 +23,16 @@ int kanode_internal_scratch_rows(const kanode_handle* h);
 // kanode_vjp_stage with dp either accumulated (+=, the C-ABI semantics) or assigned (dp_assign)
 // su_scale / sl_scale (nullable, device): the state / adjoint stage coefficients are multiplied
 // by *scale in the kernels (device-resident step sizes)
+// defer: on the Fisher-KPP table path, leave the stage's dp / error reduction pending until
+// kanode_internal_vjp_flush (up to kMaxFinishJobs stages reduced in one launch); the stage's
+// dp and error_sumsq outputs are valid only after the flush
 kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
                                         const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
                                         int64_t batch, void* stream, const double* su_scale = nullptr,
-                                        const double* sl_scale = nullptr);
+                                        const double* sl_scale = nullptr,
+                                        bool defer = false);
+kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream);
+void kanode_internal_vjp_discard(kanode_handle* h);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;
 // while *skip != 0 (device, nullable) the stage kernels return at once (a finished graph-mode solve)
 kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,

@@ -667,8 +667,10 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
 
     // adjoint RHS at τ: u(tf - τ) from the dense output, λ stage input l + Σ lc_j lks_j
     // (-> lam_out), lamJ = λsᵀ∂f/∂u, dpo = λsᵀ∂f/∂p; ec != NULL adds the λ error total -> err
+    // defer: the dp / error reductions of this stage wait for flush() (one launch per step)
+    kanode_internal_vjp_discard(h);   // nothing pending from an earlier failed call
     auto adj_rhs = [&](double tau, const void* l, int nl, void* const* lks, const double* lc, void* lamJ, void* dpo,
-                       void* lam_out, const double* ec, double* err) -> kanode_status {
+                       void* lam_out, const double* ec, double* err, bool defer = false) -> kanode_status {
         const double t = tf - tau;
         int64_t i = (int64_t)(std::upper_bound(s->ts.begin(), s->ts.end(), t) - s->ts.begin()) - 1;
         i = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, i));
@@ -689,7 +691,8 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             sl.reltol = o.reltol;
             sl.error_sumsq = err;
         }
-        return kanode_internal_vjp_stage(h, p, s->u(i), &su, l, &sl, lamJ, dpo, true, s->batch, st);
+        return kanode_internal_vjp_stage(h, p, s->u(i), &su, l, &sl, lamJ, dpo, true, s->batch, st, nullptr, nullptr,
+                                         defer);
     };
     const int64_t ntot = n + P;
     int cur = 0;   // lam[cur], mu[cur] hold λ, μ
@@ -738,12 +741,13 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                 double ec[7];
                 for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
                 SOLVE_TRY(adj_rhs(tau + hstep, lam[cur], 6, kl, lc, kl[6], km[6], lam[nxt], o.adaptive ? ec : nullptr,
-                                  s->dscal + 0));
+                                  s->dscal + 0, true));
             } else {
                 SOLVE_TRY(adj_rhs(tau + TC[i] * hstep, lam[cur], i + 1, kl, lc, kl[i + 1], km[i + 1], nullptr,
-                                  nullptr, nullptr));
+                                  nullptr, nullptr, true));
             }
         }
+        SOLVE_TRY(kanode_internal_vjp_flush(h, st));   // km[1..6] and the λ error
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
