@@ -116,8 +116,57 @@ kd_fwd_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, c
 // 16x the waves of a thread-per-column kernel, each with 1/I of the serial work: at 4096
 // columns the per-column latency chain, not launch count, bounds it.  The parameter vector
 // and the layers' constants are staged in LDS once per block (wave-uniform LDS reads).
+// The forward of a whole small chain for one column group (16 lanes, lane j holds entry j of the
+// activation): lane i evaluates the basis and swish of input i and its partial sums for every
+// output o, butterfly shuffles sum them over the group, lane o keeps output o.
+template <typename T, int NORM, int PATH>
+__device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a);
+
 constexpr int kChainBlock = 256;
 constexpr int kChainDim = 16;    // lanes per column = max layer width
+template <typename T, int NORM, int PATH>
+__device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a) {
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& lc = lcl[l];
+        const int I = lc.I, O = lc.O, G = lc.G;
+        const T* __restrict__ C = ps + lc.p_off;
+        const T* __restrict__ W = ps + lc.w_off;
+        T acc[kChainDim], bas[kChainDim];
+#pragma unroll
+        for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
+        if (j < I) {
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                const T phi = bs.next(M, lc, g, z, aux);
+                const T* Cc = C + O * (g + G * j);
+#pragma unroll
+                for (int o = 0; o < kChainDim; ++o)
+                    if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
+            }
+            if (lc.use_base) {
+                const T sw = swish<T>(M, a);
+                const T* Wj = W + O * j;
+#pragma unroll
+                for (int o = 0; o < kChainDim; ++o)
+                    if (o < O) bas[o] = Wj[o] * sw;
+            }
+        }
+        T out = T(0);
+#pragma unroll
+        for (int o = 0; o < kChainDim; ++o) {
+            if (o < O) {
+                const T s = row16_sum(acc[o]);
+                const T bsum = lc.use_base ? row16_sum(bas[o]) : T(0);   // (DPP: every lane of the row takes part)
+                if (o == j) out = lc.use_base ? s + bsum : s;
+            }
+        }
+        a = out;
+    }
+    return a;
+}
+
 template <typename T, int NORM, int PATH>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
@@ -160,48 +209,7 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
             if (y_out) y_out[idx] = a;
         }
         const T yin = a;
-        for (int l = 0; l < nl; ++l) {
-            const LayerConst& lc = lcl[l];
-            const int I = lc.I, O = lc.O, G = lc.G;
-            const T* __restrict__ C = ps + lc.p_off;
-            const T* __restrict__ W = ps + lc.w_off;
-            T acc[kChainDim], bas[kChainDim];
-#pragma unroll
-            for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
-            if (j < I) {
-                BasisStream<T, PATH> bs;
-                bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
-                for (int g = 0; g < G; ++g) {
-                    T z, aux;
-                    const T phi = bs.next(M, lc, g, z, aux);
-                    const T* Cc = C + O * (g + G * j);
-#pragma unroll
-                    for (int o = 0; o < kChainDim; ++o)
-                        if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
-                }
-                if (lc.use_base) {
-                    const T sw = swish<T>(M, a);
-                    const T* Wj = W + O * j;
-#pragma unroll
-                    for (int o = 0; o < kChainDim; ++o)
-                        if (o < O) bas[o] = Wj[o] * sw;
-                }
-            }
-            T out = T(0);
-#pragma unroll
-            for (int o = 0; o < kChainDim; ++o) {
-                if (o < O) {
-                    T s = acc[o], b = bas[o];
-#pragma unroll
-                    for (int m = 1; m < kChainDim; m <<= 1) {
-                        s += __shfl_xor(s, m, kChainDim);
-                        if (lc.use_base) b += __shfl_xor(b, m, kChainDim);
-                    }
-                    if (o == j) out = lc.use_base ? s + b : s;
-                }
-            }
-            a = out;
-        }
+        a = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, a);
         if (j < OL) {
             y[(int64_t)OL * k + j] = a;
             if (want_err) {
@@ -216,6 +224,164 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
         __shared__ double red[kChainBlock / kWave];
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_direct ? err_direct : err_slab + blockIdx.x);
+    }
+}
+
+// The whole Tsit5 solve of a small chain in ONE workgroup (kanode_solve_tsit5 for the
+// Lotka-Volterra shape, LV_driver_KANODE.jl:180-184, a batch of <= 16 trajectories): column
+// group g (16 lanes) owns trajectory g, lane j < N holds u_j and its seven stage values in
+// registers, every stage is chain_forward, and the embedded-error norm over the whole state
+// is a block sum that every lane receives, so every lane takes the same step-control decision
+// (the arithmetic and order of kanode_solve.cpp solve_t / tsit5_post_kernel: Hairer-Wanner
+// initial step, PI controller, saveat from the dense output, FSAL).  No launch or host
+// round trip per stage or step: the host loop pays ~6 launches + one 8-byte read per step.
+template <typename T, int NORM, int PATH>
+__global__ void __launch_bounds__(kChainBlock)
+kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
+                      const T* __restrict__ u0, int64_t B, ChainSolveArgs a) {
+    constexpr double TA[6][6] = {
+        {0.161, 0, 0, 0, 0, 0},
+        {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
+        {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
+        {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
+        {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
+        {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
+    };
+    constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
+                              -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
+                              0.015151515151515152};
+    extern __shared__ __attribute__((aligned(16))) unsigned char cs_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cs_raw);
+    T* ps = reinterpret_cast<T*>(cs_raw + nl * sizeof(LayerConst));
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cs_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    __shared__ double red[kChainBlock / kWave];
+    const Math<T> M{tab};
+    const int N = lcl[0].I;
+    const int j = threadIdx.x & (kChainDim - 1);
+    const int64_t col = threadIdx.x / kChainDim;
+    const bool act = col < B && j < N;
+    const int64_t idx = (int64_t)N * col + j;
+    const int64_t n = (int64_t)N * B;
+    T* __restrict__ usave = reinterpret_cast<T*>(a.u_save);
+    T* __restrict__ rec = reinterpret_cast<T*>(a.rec);
+    // Σ over the state of v (inactive lanes give 0), the same ordered total in every lane
+    auto bsum = [&](double v) -> double {
+        v = wave_sum(act ? v : 0.0);
+        __syncthreads();
+        if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
+        __syncthreads();
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        return t;
+    };
+    T u = act ? u0[idx] : T(0);
+    T k[7];
+    k[0] = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, u);
+    if (rec && act) reinterpret_cast<T*>(a.k1_0)[idx] = k[0];
+    const double t0 = a.t0, tf = a.tf;
+    int64_t si = 0;
+    while (si < a.n_save && a.saveat[si] <= t0 + 1e-14 * ::fmax(1.0, ::fabs(t0))) {
+        if (act && usave) usave[si * n + idx] = u;
+        ++si;
+    }
+    double dt = a.dt;
+    if (a.adaptive && !(a.dt > 0)) {   // Hairer & Wanner (solve_t initdt)
+        const double sk = ::fma(a.reltol, kabs((double)u), a.abstol);
+        const double d0 = ::sqrt(bsum(((double)u / sk) * ((double)u / sk)) / (double)n);
+        const double d1 = ::sqrt(bsum(((double)k[0] / sk) * ((double)k[0] / sk)) / (double)n);
+        double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        dt0 = ::fmin(dt0, tf - t0);
+        const T f1 = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, kfma<T>((T)dt0, k[0], u));
+        const double e = ::fma(-1.0, (double)k[0], (double)f1) / sk;
+        const double d2 = ::sqrt(bsum(e * e) / (double)n) / dt0;
+        const double mx = ::fmax(d1, d2);
+        const double dt1 = mx <= 1e-15 ? ::fmax(1e-6, dt0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
+        dt = ::fmin(::fmin(100 * dt0, dt1), tf - t0);
+    }
+    double qold = a.qoldinit, t = t0;
+    int64_t naccept = 0, nreject = 0, nf = 0, it = 0, status = 0;
+    for (; it < a.maxiters; ++it) {
+        if (t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf))) break;
+        dt = ::fmin(dt, tf - t);
+        T y = u;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            y = u;
+#pragma unroll
+            for (int m = 0; m <= i; ++m) y = kfma<T>((T)(dt * TA[i][m]), k[m], y);
+            k[i + 1] = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, y);
+        }
+        nf += 6;
+        double dtnew = dt;
+        if (a.adaptive) {
+            double ev = 0.0;
+#pragma unroll
+            for (int m = 0; m < 6; ++m) ev = ::fma(dt * BT[m], (double)k[m], ev);
+            const double e = ::fma(dt * BT[6], (double)k[6], ev);
+            const double sk = ::fma(a.reltol, ::fmax(kabs((double)u), kabs((double)y)), a.abstol);
+            const double r = e / sk;
+            const double eest = ::sqrt(bsum(r * r) / (double)n);
+            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            if (eest > 1.0 && dt > a.dtmin) {
+                ++nreject;
+                dt = dt / ::fmin(1.0 / a.qmin, q11 / a.gamma);
+                continue;
+            }
+            double q = q11 / ::pow(qold, a.beta2);
+            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
+            if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
+            dtnew = q > 0 ? dt / q : dt * a.qmax;
+            qold = ::fmax(eest, a.qoldinit);
+        }
+        if (rec && naccept >= a.cap) {   // dense-output storage exhausted
+            status = 2;
+            break;
+        }
+        const double tn = t + dt;
+        while (si < a.n_save && a.saveat[si] <= tn + 1e-12 * ::fmax(1.0, ::fabs(tn))) {
+            const double tsv = a.saveat[si];
+            T v = y;
+            if (!(::fabs(tsv - tn) <= 1e-12 * ::fmax(1.0, ::fabs(tn)))) {
+                double w[7];
+                tsit5_interp_weights((tsv - t) / dt, w);
+                v = u;
+#pragma unroll
+                for (int m = 0; m < 7; ++m) v = kfma<T>((T)(w[m] * dt), k[m], v);
+            }
+            if (act && usave) usave[si * n + idx] = v;
+            ++si;
+        }
+        if (rec) {
+            T* __restrict__ r = rec + naccept * 7 * n;
+            if (act) {
+                r[idx] = u;
+#pragma unroll
+                for (int m = 1; m < 7; ++m) r[(int64_t)m * n + idx] = k[m];
+            }
+            if (threadIdx.x == 0) {
+                a.ts[naccept] = t;
+                a.dts[naccept] = dt;
+            }
+        }
+        u = y;   // commit u <- u_new, k_1 <- k_7 (FSAL)
+        k[0] = k[6];
+        t = tn;
+        ++naccept;
+        dt = dtnew;
+    }
+    if (status == 0 && it == a.maxiters && !(t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf)))) status = 1;
+    if (threadIdx.x == 0) {
+        a.out[0] = naccept;
+        a.out[1] = nreject;
+        a.out[2] = nf + 1;
+        a.out[3] = status;
     }
 }
 
@@ -316,13 +482,9 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
 #pragma unroll
                 for (int o = 0; o < kChainDim; ++o) {
                     if (o < O) {
-                        T s = acc[o], b = bas[o];
-#pragma unroll
-                        for (int m = 1; m < kChainDim; m <<= 1) {
-                            s += __shfl_xor(s, m, kChainDim);
-                            if (lc.use_base) b += __shfl_xor(b, m, kChainDim);
-                        }
-                        if (o == j) out = lc.use_base ? s + b : s;
+                        const T s = row16_sum(acc[o]);
+                        const T bsum = lc.use_base ? row16_sum(bas[o]) : T(0);
+                        if (o == j) out = lc.use_base ? s + bsum : s;
                     }
                 }
                 act[l + 1] = out;
@@ -339,7 +501,7 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
                 const T* __restrict__ W = ps + lc.w_off;
                 T yb[kChainDim];
 #pragma unroll
-                for (int o = 0; o < kChainDim; ++o) yb[o] = o < O ? __shfl(ybar, o, kChainDim) : T(0);
+                for (int o = 0; o < kChainDim; ++o) yb[o] = o < O ? row16_bcast(ybar, o) : T(0);
                 T xb = T(0);
                 if (j < I) {
                     const T a = act[l];
@@ -698,6 +860,33 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
     return launch_stage_error_final(err_slab, g, err_out, st);
 }
 
+// The one-workgroup solve (kd_chain_tsit5_kernel): every layer small, one normalizer/path
+// specialisation, N_in == N_out, B <= kChainSolveMaxBatch; hipErrorNotSupported otherwise.
+template <typename T>
+hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                 const T* u0, int64_t B, const ChainSolveArgs& a, hipStream_t st) {
+    if (nl < 1 || nl > 8 || B < 1 || B > kChainSolveMaxBatch || I_ne_O(hlcs, nl)) return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T);
+    if (lds > 48 * 1024) return hipErrorNotSupported;
+    const int threads = (int)((B * kChainDim + kWave - 1) / kWave) * kWave;
+    const LayerConst& h = hlcs[0];
+#define KAN_CSOLVE(NORM, PATH)                                                                                   \
+    hipLaunchKernelGGL((kd_chain_tsit5_kernel<T, NORM, PATH>), dim3(1), dim3(threads), lds, st, lcs, nl, p, (int)P, \
+                       u0, B, a)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CSOLVE(NORM_TANH_FAST, PATH_REC);
+    else if (h.path == PATH_REC_CORR) KAN_CSOLVE(NORM_RUNTIME, PATH_REC_CORR);
+    else if (h.path == PATH_REC) KAN_CSOLVE(NORM_RUNTIME, PATH_REC);
+    else KAN_CSOLVE(NORM_RUNTIME, PATH_DIRECT);
+#undef KAN_CSOLVE
+    return hipGetLastError();
+}
+
 // The fused adjoint stage of a small chain (kd_chain_vjp_stage_kernel) when every layer is
 // small (I, O <= 16), the layers share the normalizer/path specialisation, nl <= 4 and the
 // parameter vector plus the gradient rows fit in LDS; hipErrorNotSupported otherwise.
@@ -751,6 +940,8 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
                                                const T*, T*, int64_t, hipStream_t, const StageArgs<T>*, T*,       \
                                                double*, int, double*);                                            \
     template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
+    template hipError_t launch_kd_chain_tsit5<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,   \
+                                                 const T*, int64_t, const ChainSolveArgs&, hipStream_t);         \
     template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
                                              int64_t, hipStream_t);                                               \
     template hipError_t launch_kd_vjp_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, const T*,  \

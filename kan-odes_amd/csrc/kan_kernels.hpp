@@ -148,6 +148,46 @@ template <typename T>
 hipError_t launch_tsit5_post(const SolveCtl* cin, SolveCtl* cout, const double* sumsq, const Tsit5Bufs<T>& bf,
                              const Tsit5PostArgs& pa, int64_t n, hipStream_t st);
 
+// Tsit5Interp b_i(θ) = Σ_m RI[i][m] θ^(m+1) (OrdinaryDiffEqTsit5 1.1.0), on the device
+__device__ __forceinline__ void tsit5_interp_weights(double th, double w[7]) {
+    constexpr double RI[7][4] = {
+        {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
+        {0.0, 0.13169999999999998, -0.2234, 0.1017},
+        {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
+        {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
+        {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
+        {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
+        {0.0, 1.5, -4.0, 2.5},
+    };
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s += RI[i][m] * ::pow(th, (double)(m + 1));
+        w[i] = s;
+    }
+}
+
+// A whole Tsit5 solve of a small chain in one workgroup (kd_chain_tsit5_kernel, kan_col.hip):
+// the options and storage of kanode_solve_tsit5 (solve_t semantics), status out[3]:
+// 0 done, 1 maxiters, 2 dense-output capacity (the caller falls back to the host loop).
+struct ChainSolveArgs {
+    double t0, tf, dt, abstol, reltol, dtmin, beta1, beta2, gamma, qmin, qmax, qoldinit;
+    int32_t adaptive, pad;
+    int64_t maxiters, n_save, cap;
+    const double* saveat;
+    void* u_save;     // [n_save][n] or null
+    void* rec;        // [cap][7][n]: u_n, k_2..k_7 of accepted step n (null: no dense output)
+    void* k1_0;       // k_1 of step 0 (with rec)
+    double* ts;       // [cap] step start times (with rec)
+    double* dts;      // [cap] step sizes (with rec)
+    int64_t* out;     // naccept, nreject, nf, status
+};
+constexpr int kChainSolveMaxBatch = 16;   // columns of one workgroup (256 lanes / 16)
+template <typename T>
+hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                 const T* u0, int64_t B, const ChainSolveArgs& a, hipStream_t st);
+
 // surrogate shapes (kan_wide.hip)
 constexpr int kWideKT = 8;       // column tile of the wide-out kernels
 constexpr int kWideOMax = 16;    // max out_dims of a wide-in layer

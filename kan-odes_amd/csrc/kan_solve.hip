@@ -14,27 +14,6 @@
 
 namespace kan {
 
-namespace {
-// Tsit5Interp b_i(θ) = Σ_m RI[i][m] θ^(m+1)
-__device__ __forceinline__ void tsit5_interp_weights(double th, double w[7]) {
-    constexpr double RI[7][4] = {
-        {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
-        {0.0, 0.13169999999999998, -0.2234, 0.1017},
-        {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
-        {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
-        {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
-        {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
-        {0.0, 1.5, -4.0, 2.5},
-    };
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s += RI[i][m] * ::pow(th, (double)(m + 1));
-        w[i] = s;
-    }
-}
-}  // namespace
 
 template <typename T>
 __global__ void __launch_bounds__(kBlock)

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 
@@ -965,6 +966,28 @@ kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream) {
     return vjp_flush(h, (hipStream_t)stream);
 }
 void kanode_internal_vjp_discard(kanode_handle* h) { h->njobs = 0; }
+bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
+    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || batch < 1 || batch > kan::kChainSolveMaxBatch) return false;
+    if (std::getenv("KANODE_NO_FUSED_SOLVE")) return false;   // experiments: force the host loop
+    for (int l = 0; l < h->n_layers; ++l)
+        if (h->kind[l] != KIND_COL) return false;
+    return true;
+}
+kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
+                                          const kan::ChainSolveArgs* a, void* stream, bool& launched) {
+    launched = false;
+    const hipStream_t st = (hipStream_t)stream;
+    const hipError_t e =
+        h->spec.dtype == KANODE_F64
+            ? kan::launch_kd_chain_tsit5<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P,
+                                                 (const double*)u0, batch, *a, st)
+            : kan::launch_kd_chain_tsit5<float>(h->hlc, h->n_layers, h->dlc, (const float*)p, h->P, (const float*)u0,
+                                                batch, *a, st);
+    if (e == hipErrorNotSupported) return KANODE_OK;
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_tsit5: ") + hipGetErrorString(e));
+    launched = true;
+    return KANODE_OK;
+}
 kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* state,
                                         const void* lam, const kanode_stage* adj, void* lamJ, void* dp, bool dp_assign,
                                         int64_t batch, void* stream, const double* su_scale, const double* sl_scale,

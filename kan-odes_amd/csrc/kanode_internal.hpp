@@ -10,6 +10,10 @@
 
 #include "kanode.h"
 
+namespace kan {
+struct ChainSolveArgs;
+}
+
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
 kanode_status kanode_internal_check(kanode_handle* h);     // non-null, sets the handle's device
 int kanode_internal_dtype(const kanode_handle* h);
@@ -32,7 +36,12 @@ kanode_status kanode_internal_vjp_stage(kanode_handle* h, const void* p, const v
                                         const double* sl_scale = nullptr,
                                         bool defer = false);
 kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream);
-void kanode_internal_vjp_discard(kanode_handle* h);   // drop pending reductions (error paths)
+void kanode_internal_vjp_discard(kanode_handle* h);
+// the one-workgroup small-chain solve (kd_chain_tsit5_kernel): whether this handle's RHS and a
+// batch qualify, and the launch (launched = false when the kernel does not cover the shape)
+bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch);
+kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
+                                          const kan::ChainSolveArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;
 // while *skip != 0 (device, nullable) the stage kernels return at once (a finished graph-mode solve)
 kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,

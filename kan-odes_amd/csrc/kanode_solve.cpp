@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "kan_kernels.hpp"
@@ -94,8 +96,20 @@ struct kanode_solution {
     std::vector<double> saveat;
     std::vector<double> ts, dts;     // accepted steps: start time, step
     std::vector<void*> slots;
+    bool slots_borrowed = false;     // slots point into fused.block (one-workgroup solve), not owned
     void* k1_0 = nullptr;
     bool record = true;
+    // one-workgroup small-chain solve (kd_chain_tsit5_kernel): contiguous dense output and the
+    // device copies of saveat, step times and the result block
+    struct Fused {
+        void* block = nullptr;
+        int64_t cap = 0;                   // steps the block holds
+        double* saveat = nullptr;
+        int64_t saveat_cap = 0;
+        double* ts = nullptr;              // [cap] then dts [cap]
+        int64_t ts_cap = 0;
+        int64_t* out = nullptr;            // naccept, nreject, nf, status
+    } fused;
     double* dscal = nullptr;         // device scalars (norm totals)
     double* hscal = nullptr;         // pinned host mirror
     // adjoint scratch (sized on first use)
@@ -128,7 +142,10 @@ struct kanode_solution {
     } g;
 
     ~kanode_solution() {
-        for (void* s : slots) (void)hipFree(s);
+        if (!slots_borrowed)
+            for (void* s : slots) (void)hipFree(s);
+        for (void* q : {fused.block, (void*)fused.saveat, (void*)fused.ts, (void*)fused.out})
+            if (q) (void)hipFree(q);
         if (k1_0) (void)hipFree(k1_0);
         if (dscal) (void)hipFree(dscal);
         if (hscal) (void)hipHostFree(hscal);
@@ -173,6 +190,10 @@ bool capturing(hipStream_t st) {
 
 // slots [0, need) exist (allocating — not allowed during capture)
 kanode_status ensure_slots(kanode_handle* h, kanode_solution* s, int64_t need, hipStream_t st) {
+    if (s->slots_borrowed) {   // the previous solve used the fused block: start a slot list of our own
+        s->slots.clear();
+        s->slots_borrowed = false;
+    }
     if (!s->record) need = std::min<int64_t>(need, 2);
     if ((int64_t)s->slots.size() >= need) return KANODE_OK;
     if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "dense-output storage grows during capture");
@@ -364,6 +385,116 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         stats->nreject = nreject;
         stats->nf = nf + 1;
     }
+    return KANODE_OK;
+}
+
+// ---- one-workgroup solve of a small chain (kd_chain_tsit5_kernel) ------------------------
+// The whole forward solve in one launch for a chain of small layers and <= 16 trajectories (the
+// Lotka-Volterra shape).  done = false when the shape is not covered or the dense-output block
+// filled up: the caller then runs the host loop (solve_t) from scratch.
+template <typename T>
+kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, double t0, double tf, const double* saveat,
+                            int64_t n_save, void* u_save, const kanode_solver_options& o, kanode_solution* s,
+                            kanode_solve_stats* stats, hipStream_t st, bool& done) {
+    done = false;
+    if (capturing(st) || !kanode_internal_chain_tsit5_ok(h, s->batch)) return KANODE_OK;
+    const size_t sb = s->state_bytes();
+    auto& f = s->fused;
+    int64_t cap = 0;
+    if (s->record) {
+        if (!o.adaptive) {
+            for (double t = t0, dt = o.dt; cap < o.maxiters && !(t >= tf - 1e-14 * std::max(1.0, std::fabs(tf)));) {
+                dt = std::min(dt, tf - t);
+                t = t + dt;
+                ++cap;
+            }
+        } else {
+            cap = std::min<int64_t>(o.maxiters, 4096);
+            if (const char* e = std::getenv("KANODE_FUSED_CAP")) cap = std::max(1, std::atoi(e));   // tests only
+        }
+        cap = std::max<int64_t>(cap, 1);
+        if (f.cap < cap) {
+            if (s->slots_borrowed) s->slots.clear();
+            if (f.block) (void)hipFree(f.block);
+            f.block = nullptr;
+            f.cap = 0;
+            if (hipMalloc(&f.block, (size_t)cap * 7 * sb) != hipSuccess) {
+                (void)hipGetLastError();
+                return KANODE_OK;   // no room for the contiguous block: the host loop allocates per step
+            }
+            f.cap = cap;
+        }
+        if (f.ts_cap < f.cap) {
+            if (f.ts) (void)hipFree(f.ts);
+            f.ts = nullptr;
+            f.ts_cap = 0;
+            SOLVE_HIP(h, hipMalloc((void**)&f.ts, 2 * (size_t)f.cap * sizeof(double)));
+            f.ts_cap = f.cap;
+        }
+    }
+    if (f.saveat_cap < n_save) {
+        if (f.saveat) (void)hipFree(f.saveat);
+        f.saveat = nullptr;
+        f.saveat_cap = 0;
+        SOLVE_HIP(h, hipMalloc((void**)&f.saveat, (size_t)n_save * sizeof(double)));
+        f.saveat_cap = n_save;
+    }
+    if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
+    if (n_save > 0)
+        SOLVE_HIP(h, hipMemcpyAsync(f.saveat, saveat, (size_t)n_save * sizeof(double), hipMemcpyHostToDevice, st));
+    kan::ChainSolveArgs a{};
+    a.t0 = t0;
+    a.tf = tf;
+    a.dt = o.dt;
+    a.abstol = o.abstol;
+    a.reltol = o.reltol;
+    a.dtmin = o.dtmin;
+    a.beta1 = o.beta1;
+    a.beta2 = o.beta2;
+    a.gamma = o.gamma;
+    a.qmin = o.qmin;
+    a.qmax = o.qmax;
+    a.qoldinit = o.qoldinit;
+    a.adaptive = o.adaptive ? 1 : 0;
+    a.maxiters = o.maxiters;
+    a.n_save = n_save;
+    a.cap = s->record ? f.cap : 0;
+    a.saveat = f.saveat;
+    a.u_save = n_save > 0 ? u_save : nullptr;
+    a.rec = s->record ? f.block : nullptr;
+    a.k1_0 = s->k1_0;
+    a.ts = s->record ? f.ts : nullptr;
+    a.dts = s->record ? f.ts + f.cap : nullptr;
+    a.out = f.out;
+    bool launched = false;
+    SOLVE_TRY(kanode_internal_chain_tsit5(h, p, u0, s->batch, &a, st, launched));
+    if (!launched) return KANODE_OK;
+    SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    int64_t res[4];
+    std::memcpy(res, s->hscal, sizeof(res));
+    if (res[3] == 2) return KANODE_OK;   // dense output full: the host loop redoes the solve
+    if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
+    const int64_t na = res[0];
+    if (s->record) {
+        s->ts.resize(na);
+        s->dts.resize(na);
+        if (na > 0) {
+            SOLVE_HIP(h, hipMemcpy(s->ts.data(), f.ts, (size_t)na * sizeof(double), hipMemcpyDeviceToHost));
+            SOLVE_HIP(h, hipMemcpy(s->dts.data(), f.ts + f.cap, (size_t)na * sizeof(double), hipMemcpyDeviceToHost));
+        }
+        if (!s->slots_borrowed)
+            for (void* q : s->slots) (void)hipFree(q);
+        s->slots.resize(f.cap);
+        for (int64_t i = 0; i < f.cap; ++i) s->slots[i] = (char*)f.block + (size_t)i * 7 * sb;
+        s->slots_borrowed = true;
+    }
+    if (stats) {
+        stats->naccept = res[0];
+        stats->nreject = res[1];
+        stats->nf = res[2];
+    }
+    done = true;
     return KANODE_OK;
 }
 
@@ -878,8 +1009,16 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
             r = dtype == KANODE_F64 ? solve_graph_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
                                     : solve_graph_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
         } else {
-            r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
-                                    : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
+            // auto: a small chain (<= 16 trajectories) runs the whole solve in one workgroup
+            bool done = false;
+            r = KANODE_OK;
+            if (o.control == 0)
+                r = dtype == KANODE_F64
+                        ? solve_fused_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st, done)
+                        : solve_fused_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st, done);
+            if (r == KANODE_OK && !done)
+                r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
+                                        : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
         }
     }
     if (record || s->state_bytes() <= (size_t)64 << 20) {

@@ -300,3 +300,69 @@ def test_device_control_graph_reuse_and_limits():
         assert (g - gr).abs().max().item() <= 50 * opt.reltol * gr.abs().max().item()
     with pytest.raises(kanode.KanodeError, match="maxiters"):
         kanode.solve(rhs, u0, tspan, p0, ts, dataclasses.replace(opt, maxiters=10))
+
+
+# ---- one-workgroup solve of a small chain (kd_chain_tsit5_kernel) vs the host loop ------------
+def _lv_u0(B, seed=4):
+    return np.random.default_rng(seed).uniform(0.5, 2.0, (B, 2))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("B", [1, 3, 16])
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_fused_chain_solve_matches_host_loop(dtype, B, adaptive):
+    """control="auto" runs a <= 16-trajectory small chain as ONE workgroup (controller, saveat and
+    dense output on the device); it takes the host loop's steps and writes the same saveat values,
+    and its dense output feeds the same InterpolatingAdjoint."""
+    rhs = lv(dtype)
+    u0 = t(_lv_u0(B), dtype)
+    p0 = t(np.random.default_rng(7).uniform(-0.3, 0.3, 240), dtype)
+    tspan, ts = (0.0, 3.5), [0.1 * i for i in range(35)]
+    f64 = dtype == torch.float64
+    opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else 0.01, abstol=1e-8 if f64 else 1e-6,
+                              reltol=1e-7 if f64 else 1e-4)
+    w = t(np.random.default_rng(11).normal(size=(len(ts), B, 2)), dtype)
+    out = {}
+    for control in ("auto", "host"):
+        p = p0.clone().requires_grad_(True)
+        sol = kanode.solve(rhs, u0, tspan, p, ts, dataclasses.replace(opt, control=control),
+                           sensealg="interpolating_adjoint")
+        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+        out[control] = (sol, g)
+    (sf, gf), (sh, gh) = out["auto"], out["host"]
+    # adaptive: the error norm is one block sum (host: slab partials) and pow() runs on the device,
+    # so dt may differ in its last bits; fp32 adaptive may then flip a step decision
+    if f64 or not adaptive:
+        assert sf.stats["naccept"] == sh.stats["naccept"] and sf.stats["nreject"] == sh.stats["nreject"]
+        assert sf.stats["nf"] == sh.stats["nf"]
+    else:
+        assert abs(sf.stats["naccept"] - sh.stats["naccept"]) <= 2
+    scale = max(1.0, sh.u.abs().max().item())
+    tol = (1e-12 if f64 else 2e-6) if not adaptive else max(1e-12 if f64 else 2e-6, 1e-3 * opt.reltol)
+    if not f64 and adaptive:
+        tol = 20 * opt.reltol
+    assert (sf.u - sh.u).abs().max().item() <= tol * scale
+    gtol = 1e-9 if f64 else 5e-3
+    assert (gf - gh).abs().max().item() <= gtol * gh.abs().max().item()
+
+
+def test_fused_chain_solve_falls_back_when_dense_output_fills(monkeypatch):
+    """A dense output larger than the fused block (KANODE_FUSED_CAP, tests only) falls back to the
+    host loop: same steps, same values, a usable dense output."""
+    rhs = lv()
+    u0 = t(_lv_u0(2))
+    p0 = t(np.random.default_rng(7).uniform(-0.3, 0.3, 240))
+    ts = [0.1 * i for i in range(35)]
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7)
+    w = t(np.random.default_rng(2).normal(size=(len(ts), 2, 2)))
+    ref_p = p0.clone().requires_grad_(True)
+    ref = kanode.solve(rhs, u0, (0.0, 3.5), ref_p, ts, dataclasses.replace(opt, control="host"),
+                       sensealg="interpolating_adjoint")
+    (gr,) = torch.autograd.grad((ref.u * w).sum(), [ref_p])
+    monkeypatch.setenv("KANODE_FUSED_CAP", "3")
+    p = p0.clone().requires_grad_(True)
+    sol = kanode.solve(rhs, u0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
+    (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+    assert sol.stats["naccept"] == ref.stats["naccept"] > 3
+    assert (sol.u - ref.u).abs().max().item() <= 1e-12 * max(1.0, ref.u.abs().max().item())
+    assert (g - gr).abs().max().item() <= 1e-12 * gr.abs().max().item()

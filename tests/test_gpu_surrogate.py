@@ -43,10 +43,12 @@ def _glorot_params(rng, specs):
     return np.concatenate(parts)
 
 
-@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (2048, 10, 8), (300, 7, 3), (2048, 10, 1), (64, 5, 11)])
+@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (2048, 10, 8), (300, 7, 3), (2048, 10, 1), (64, 5, 11),
+                                   (512, 5, 200), (96, 5, 133)])
 def test_surrogate_baseline_sizes(N, G, B):
-    """BU512: KAN [512,10,512] G=5; SC1024: KAN [2048,10,2048] G=10 (state [Re; Im]); odd sizes and
-    a column count that is not a multiple of the 8-column tile."""
+    """BU512: KAN [512,10,512] G=5; SC1024: KAN [2048,10,2048] G=10 (state [Re; Im]); odd sizes,
+    a column count that is not a multiple of the 8-column tile, and batches past the 128-column
+    basis staging of the wide-out parameter pullback (kan_wide.hip kWOPK)."""
     rng = np.random.default_rng(N + G + B)
     specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
     p = _glorot_params(rng, specs)

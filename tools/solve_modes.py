@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Forward-solve wall time per step control mode (kanode_solve_tsit5 control = host / device),
+"""Forward-solve wall time per step control mode (kanode_solve_tsit5 control = host / device /
+auto: auto runs a small chain of <= 16 trajectories as one workgroup),
 with and without the dense output kept, for a few problem sizes.
 
     python3 tools/solve_modes.py
@@ -25,7 +26,7 @@ def main():
     chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
     lv = kanode.ChainRHS(chain, device=dev)
     plv = torch.as_tensor(chain.setup(np.random.default_rng(0))[0].astype(np.float64) / 10, device=dev)
-    for B in (1, 4096):
+    for B in (1, 16, 4096):
         cases.append((f"lv B={B}", lv, torch.ones(B, 2, dtype=torch.float64, device=dev), plv, (0.0, 3.5),
                       [0.1 * i for i in range(35)], 0.01))
     kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
@@ -38,7 +39,7 @@ def main():
         for adaptive in (True, False):
             for keep in (False, True):
                 row = []
-                for control in ("host", "device"):
+                for control in ("host", "device", "auto"):
                     opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else dt, control=control).to_c()
                     dense = None
                     for it in range(4):
@@ -51,7 +52,8 @@ def main():
                     torch.cuda.synchronize()
                     row.append((time.perf_counter() - t0) / 3 * 1e3)
                 print(f"{name:14s} {'adaptive' if adaptive else 'fixed   '} {'dense' if keep else '     '} "
-                      f"steps {st['naccept']:4d}  host {row[0]:7.2f} ms  device {row[1]:7.2f} ms", flush=True)
+                      f"steps {st['naccept']:4d}  host {row[0]:7.2f} ms  device {row[1]:7.2f} ms  auto {row[2]:7.2f} ms",
+                      flush=True)
 
 
 if __name__ == "__main__":
