@@ -395,6 +395,119 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
 // its slab row; chain_vjp_finish_kernel reduces the slab rows (dp) and the λ error partials.
 constexpr int kChainVjpBlock = 64;               // 4 columns per block
 constexpr int kChainMaxLayers = 4;
+// The pullback of a whole small chain for one column group (lane j holds entry j): the forward
+// keeps each layer's input activation in registers, the backward walks the layers in reverse;
+// ȳ of the last layer is lj, lane i of layer l turns it into x̄_i and adds ȳ_o φ_g(x_i),
+// ȳ_o swish(x_i) into its own entries of the group's LDS gradient row (disjoint per lane).
+// Returns λᵀ∂f/∂u (lane j: entry j).
+template <typename T, int NORM, int PATH>
+__device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps,
+                                            T* __restrict__ row, int j, T yj, T lj) {
+    // forward: the input activation of every layer (lane j holds entry j)
+    T act[kChainMaxLayers];
+    act[0] = yj;
+#pragma unroll
+    for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
+        act[l + 1] = T(0);
+        if (l + 1 < nl) {
+            const LayerConst& lc = lcl[l];
+            const int I = lc.I, O = lc.O, G = lc.G;
+            const T* __restrict__ C = ps + lc.p_off;
+            const T* __restrict__ W = ps + lc.w_off;
+            T acc[kChainDim], bas[kChainDim];
+#pragma unroll
+            for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
+            if (j < I) {
+                const T a = act[l];
+                BasisStream<T, PATH> bs;
+                bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
+                for (int g = 0; g < G; ++g) {
+                    T z, aux;
+                    const T phi = bs.next(M, lc, g, z, aux);
+                    const T* Cc = C + O * (g + G * j);
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o)
+                        if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
+                }
+                if (lc.use_base) {
+                    const T sw = swish<T>(M, a);
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o)
+                        if (o < O) bas[o] = W[O * j + o] * sw;
+                }
+            }
+            T out = T(0);
+#pragma unroll
+            for (int o = 0; o < kChainDim; ++o) {
+                if (o < O) {
+                    const T s = row16_sum(acc[o]);
+                    const T bsum = lc.use_base ? row16_sum(bas[o]) : T(0);
+                    if (o == j) out = lc.use_base ? s + bsum : s;
+                }
+            }
+            act[l + 1] = out;
+        }
+    }
+    // backward: ȳ of the last layer is λs; lane i of layer l turns it into x̄_i
+    T ybar = lj;
+#pragma unroll
+    for (int l = kChainMaxLayers - 1; l >= 0; --l) {
+        if (l < nl) {
+            const LayerConst& lc = lcl[l];
+            const int I = lc.I, O = lc.O, G = lc.G;
+            const T* __restrict__ C = ps + lc.p_off;
+            const T* __restrict__ W = ps + lc.w_off;
+            T yb[kChainDim];
+#pragma unroll
+            for (int o = 0; o < kChainDim; ++o) yb[o] = o < O ? row16_bcast(ybar, o) : T(0);
+            T xb = T(0);
+            if (j < I) {
+                const T a = act[l];
+                const T n = normalize<NORM, T>(M, lc.norm, a);
+                BasisStream<T, PATH> bs;
+                bs.init(M, lc, n);
+                const T invh = T(lc.invh);
+                T nbar = T(0);
+                for (int g = 0; g < G; ++g) {
+                    T z, aux;
+                    const T phi = bs.next(M, lc, g, z, aux);
+                    const int c = g + G * j;
+                    const T* Cc = C + O * c;
+                    T* __restrict__ rc = row + lc.p_off + O * c;
+                    T bb = T(0);
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o) {
+                        if (o < O) {
+                            bb = kfma<T>(Cc[o], yb[o], bb);
+                            rc[o] = kfma<T>(yb[o], phi, rc[o]);
+                        }
+                    }
+                    const T zb = basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb);
+                    nbar = nbar + zb * invh;
+                }
+                xb = nbar * dnormalize<NORM, T>(lc.norm, n);
+                if (lc.use_base) {
+                    T sw, dsw;
+                    swish_and_grad<T>(M, a, sw, dsw);
+                    const T* Wj = W + O * j;
+                    T* __restrict__ rw = row + lc.w_off + O * j;
+                    T sb = T(0);
+#pragma unroll
+                    for (int o = 0; o < kChainDim; ++o) {
+                        if (o < O) {
+                            sb = kfma<T>(Wj[o], yb[o], sb);
+                            rw[o] = kfma<T>(yb[o], sw, rw[o]);
+                        }
+                    }
+                    xb = xb + sb * dsw;
+                }
+            }
+            ybar = xb;
+        }
+    }
+    return ybar;
+}
+
 template <typename T, int NORM, int PATH>
 __global__ void __launch_bounds__(kChainVjpBlock)
 kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
@@ -445,108 +558,7 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
             }
             if (lam_out) lam_out[idx] = lj;
         }
-        // forward: the input activation of every layer (lane j holds entry j)
-        T act[kChainMaxLayers];
-        act[0] = yj;
-#pragma unroll
-        for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
-            act[l + 1] = T(0);
-            if (l + 1 < nl) {
-                const LayerConst& lc = lcl[l];
-                const int I = lc.I, O = lc.O, G = lc.G;
-                const T* __restrict__ C = ps + lc.p_off;
-                const T* __restrict__ W = ps + lc.w_off;
-                T acc[kChainDim], bas[kChainDim];
-#pragma unroll
-                for (int o = 0; o < kChainDim; ++o) { acc[o] = T(0); bas[o] = T(0); }
-                if (j < I) {
-                    const T a = act[l];
-                    BasisStream<T, PATH> bs;
-                    bs.init(M, lc, normalize<NORM, T>(M, lc.norm, a));
-                    for (int g = 0; g < G; ++g) {
-                        T z, aux;
-                        const T phi = bs.next(M, lc, g, z, aux);
-                        const T* Cc = C + O * (g + G * j);
-#pragma unroll
-                        for (int o = 0; o < kChainDim; ++o)
-                            if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
-                    }
-                    if (lc.use_base) {
-                        const T sw = swish<T>(M, a);
-#pragma unroll
-                        for (int o = 0; o < kChainDim; ++o)
-                            if (o < O) bas[o] = W[O * j + o] * sw;
-                    }
-                }
-                T out = T(0);
-#pragma unroll
-                for (int o = 0; o < kChainDim; ++o) {
-                    if (o < O) {
-                        const T s = row16_sum(acc[o]);
-                        const T bsum = lc.use_base ? row16_sum(bas[o]) : T(0);
-                        if (o == j) out = lc.use_base ? s + bsum : s;
-                    }
-                }
-                act[l + 1] = out;
-            }
-        }
-        // backward: ȳ of the last layer is λs; lane i of layer l turns it into x̄_i
-        T ybar = lj;
-#pragma unroll
-        for (int l = kChainMaxLayers - 1; l >= 0; --l) {
-            if (l < nl) {
-                const LayerConst& lc = lcl[l];
-                const int I = lc.I, O = lc.O, G = lc.G;
-                const T* __restrict__ C = ps + lc.p_off;
-                const T* __restrict__ W = ps + lc.w_off;
-                T yb[kChainDim];
-#pragma unroll
-                for (int o = 0; o < kChainDim; ++o) yb[o] = o < O ? row16_bcast(ybar, o) : T(0);
-                T xb = T(0);
-                if (j < I) {
-                    const T a = act[l];
-                    const T n = normalize<NORM, T>(M, lc.norm, a);
-                    BasisStream<T, PATH> bs;
-                    bs.init(M, lc, n);
-                    const T invh = T(lc.invh);
-                    T nbar = T(0);
-                    for (int g = 0; g < G; ++g) {
-                        T z, aux;
-                        const T phi = bs.next(M, lc, g, z, aux);
-                        const int c = g + G * j;
-                        const T* Cc = C + O * c;
-                        T* __restrict__ rc = row + lc.p_off + O * c;
-                        T bb = T(0);
-#pragma unroll
-                        for (int o = 0; o < kChainDim; ++o) {
-                            if (o < O) {
-                                bb = kfma<T>(Cc[o], yb[o], bb);
-                                rc[o] = kfma<T>(yb[o], phi, rc[o]);
-                            }
-                        }
-                        const T zb = basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb);
-                        nbar = nbar + zb * invh;
-                    }
-                    xb = nbar * dnormalize<NORM, T>(lc.norm, n);
-                    if (lc.use_base) {
-                        T sw, dsw;
-                        swish_and_grad<T>(M, a, sw, dsw);
-                        const T* Wj = W + O * j;
-                        T* __restrict__ rw = row + lc.w_off + O * j;
-                        T sb = T(0);
-#pragma unroll
-                        for (int o = 0; o < kChainDim; ++o) {
-                            if (o < O) {
-                                sb = kfma<T>(Wj[o], yb[o], sb);
-                                rw[o] = kfma<T>(yb[o], sw, rw[o]);
-                            }
-                        }
-                        xb = xb + sb * dsw;
-                    }
-                }
-                ybar = xb;
-            }
-        }
+        const T ybar = chain_pullback<T, NORM, PATH>(M, lcl, nl, ps, row, j, yj, lj);
         if (j < N0) {
             lamJ[idx] = ybar;
             if (want_err) {
@@ -860,6 +872,296 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
     return launch_stage_error_final(err_slab, g, err_out, st);
 }
 
+// The InterpolatingAdjoint of a small chain in ONE workgroup (kanode_adjoint_tsit5 after a
+// kd_chain_tsit5_kernel forward): the backward Tsit5 over [λ; μ] with the steps, stops, jumps,
+// FSAL re-evaluation and controller of kanode_solve.cpp adjoint_t.  Column group g holds λ of
+// trajectory g and its seven stage values in registers; every adjoint stage interpolates the
+// forward dense output u(tf - τ), forms λs = λ + h Σ a_sj kλ_j, runs chain_pullback (each group
+// adds into its own LDS gradient row) and reduces the rows into the stage's kμ (LDS), in the
+// order kd_chain_vjp_stage_kernel + chain_vjp_finish_kernel use (4 groups per block, then the
+// blocks).  μ and its seven stage vectors live in LDS; the error norm covers λ and μ.
+template <typename T, int NORM, int PATH>
+__global__ void __launch_bounds__(kChainBlock)
+kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t B,
+                        ChainAdjointArgs a) {
+    constexpr double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
+    constexpr double TA[6][6] = {
+        {0.161, 0, 0, 0, 0, 0},
+        {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
+        {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
+        {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
+        {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
+        {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
+    };
+    constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
+                              -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
+                              0.015151515151515152};
+    constexpr double RI[7][4] = {
+        {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
+        {0.0, 0.13169999999999998, -0.2234, 0.1017},
+        {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
+        {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
+        {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
+        {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
+        {0.0, 1.5, -4.0, 2.5},
+    };
+    extern __shared__ __attribute__((aligned(16))) unsigned char ca_raw[];
+    const int NG = blockDim.x / kChainDim;
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(ca_raw);
+    T* ps = reinterpret_cast<T*>(ca_raw + nl * sizeof(LayerConst));
+    T* rows = ps + P;                        // [NG][P] gradient rows
+    T* mu = rows + (size_t)NG * P;           // [2][P]
+    T* km = mu + 2 * (size_t)P;              // [7][P]
+    double* tsl = reinterpret_cast<double*>(km + 7 * (size_t)P);   // [nsteps] (8-byte aligned: P·sizeof(T) offsets)
+    double* dtsl = tsl + a.nsteps;
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(ca_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int i = threadIdx.x; i < NG * P + 9 * P; i += blockDim.x) rows[i] = T(0);
+        for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
+            tsl[i] = a.ts[i];
+            dtsl[i] = a.dts[i];
+        }
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    __shared__ double red[kChainBlock / kWave];
+    const Math<T> M{tab};
+    const int N = lcl[0].I;
+    const int j = threadIdx.x & (kChainDim - 1);
+    const int grp = threadIdx.x / kChainDim;
+    const int64_t col = grp;
+    const bool act = col < B && j < N;
+    const int64_t idx = (int64_t)N * col + j;
+    const int64_t n = (int64_t)N * B;
+    const T* __restrict__ rec = reinterpret_cast<const T*>(a.rec);
+    const T* __restrict__ dl = reinterpret_cast<const T*>(a.dl_du);
+    T* __restrict__ row = rows + (size_t)grp * P;
+    const double t0 = a.t0, tf = a.tf, TT = tf - t0;
+    const int64_t ntot = n + P;
+    auto bsum = [&](double v) -> double {   // Σ over the block, every thread gets the ordered total
+        v = wave_sum(v);
+        __syncthreads();
+        if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
+        __syncthreads();
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        return t;
+    };
+    auto add_rows = [&](int gidx, T l) -> T {   // λ += Σ dl_du[r] (rows in order)
+        for (int32_t q = a.joff[gidx]; q < a.joff[gidx + 1]; ++q)
+            if (act) l = l + dl[(int64_t)a.jrows[q] * n + idx];
+        return l;
+    };
+    int64_t cur = a.nsteps - 1;   // forward step holding t (moves back as τ grows)
+    // adjoint RHS at τ with adjoint stage input ls: returns λsᵀ∂f/∂u, kμ -> km[slot]
+    auto adj = [&](double tau, T ls, int slot) -> T {
+        const double t = tf - tau;
+        while (cur > 0 && tsl[cur] > t) --cur;
+        while (cur + 1 < a.nsteps && tsl[cur + 1] <= t) ++cur;
+        const double dti = dtsl[cur];
+        const double th = ::fmin(1.0, ::fmax(0.0, (t - tsl[cur]) / dti));
+        T y = T(0);
+        if (act) {
+            const T* __restrict__ r = rec + cur * 7 * n;
+            const T* __restrict__ k1 = cur == 0 ? reinterpret_cast<const T*>(a.k1_0) : rec + (cur - 1) * 7 * n + 6 * n;
+            T kv[7];
+            kv[0] = k1[idx];
+#pragma unroll
+            for (int m = 1; m < 7; ++m) kv[m] = r[(int64_t)m * n + idx];
+            y = r[idx];
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                const double b = th * (RI[m][0] + th * (RI[m][1] + th * (RI[m][2] + th * RI[m][3])));
+                y = kfma<T>((T)(b * dti), kv[m], y);
+            }
+        }
+        const T lj = chain_pullback<T, NORM, PATH>(M, lcl, nl, ps, row, j, y, act ? ls : T(0));
+        __syncthreads();
+        // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order
+        for (int q = threadIdx.x; q < P; q += blockDim.x) {
+            T tot = T(0);
+            for (int g0 = 0; g0 < NG; g0 += 4) {
+                T sblk = rows[(size_t)g0 * P + q];
+                for (int g = g0 + 1; g < g0 + 4 && g < NG; ++g) sblk = sblk + rows[(size_t)g * P + q];
+                tot = g0 == 0 ? sblk : tot + sblk;
+            }
+            km[(size_t)slot * P + q] = tot;
+            for (int g = 0; g < NG; ++g) rows[(size_t)g * P + q] = T(0);
+        }
+        __syncthreads();
+        return act ? lj : T(0);
+    };
+    T lam = T(0);
+    if (dl) lam = add_rows(0, lam);
+    int mc = 0;   // mu[mc] holds μ (zero)
+    T kl[7];
+    kl[0] = adj(0.0, lam, 0);
+    int64_t nf = 1;
+    double h = a.dt;
+    if (a.adaptive && !(a.dt > 0)) {   // Hairer-Wanner on [λ; μ]
+        double s0 = 0.0, s1 = 0.0;
+        {
+            const double sk = ::fma(a.reltol, kabs((double)lam), a.abstol);
+            const double r0 = (double)lam / sk, r1 = (double)kl[0] / sk;
+            s0 = act ? r0 * r0 : 0.0;
+            s1 = act ? r1 * r1 : 0.0;
+        }
+        for (int q = threadIdx.x; q < P; q += blockDim.x) {
+            const double m = (double)mu[q];
+            const double sk = ::fma(a.reltol, kabs(m), a.abstol);
+            const double r0 = m / sk, r1 = (double)km[q] / sk;
+            s0 += r0 * r0;
+            s1 += r1 * r1;
+        }
+        const double d0 = ::sqrt(bsum(s0) / (double)ntot), d1 = ::sqrt(bsum(s1) / (double)ntot);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = ::fmin(h0, TT);
+        kl[1] = adj(h0, kfma<T>((T)h0, kl[0], lam), 1);
+        ++nf;
+        double s2 = 0.0;
+        {
+            const double sk = ::fma(a.reltol, kabs((double)lam), a.abstol);
+            const double e = ::fma(-1.0, (double)kl[0], (double)kl[1]) / sk;
+            s2 = act ? e * e : 0.0;
+        }
+        for (int q = threadIdx.x; q < P; q += blockDim.x) {
+            const double sk = ::fma(a.reltol, kabs((double)mu[q]), a.abstol);
+            const double e = ::fma(-1.0, (double)km[q], (double)km[P + q]) / sk;
+            s2 += e * e;
+        }
+        const double d2 = ::sqrt(bsum(s2) / (double)ntot) / h0;
+        const double mx = ::fmax(d1, d2);
+        const double h1 = mx <= 1e-15 ? ::fmax(1e-6, h0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
+        h = ::fmin(::fmin(100 * h0, h1), TT);
+    }
+    double qold = a.qoldinit, tau = 0.0;
+    int64_t si = 0, naccept = 0, nreject = 0, it = 0, status = 0;
+    int k0 = 0;   // km slot of kμ_1 (FSAL swaps slots 0 and 6)
+    for (; it < a.maxiters; ++it) {
+        if (tau >= TT - 1e-14 * ::fmax(1.0, TT)) break;
+        h = ::fmin(h, a.stops[si] - tau);
+        int ks[7];
+        ks[0] = k0;
+#pragma unroll
+        for (int m = 1; m < 6; ++m) ks[m] = m;
+        ks[6] = k0 == 0 ? 6 : 0;
+        T ls = lam;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            ls = lam;
+#pragma unroll
+            for (int m = 0; m <= i; ++m) ls = kfma<T>((T)(h * TA[i][m]), kl[m], ls);
+            kl[i + 1] = adj(i == 5 ? tau + h : tau + TC[i] * h, ls, ks[i + 1]);
+        }
+        nf += 6;
+        // μ_new = μ + h Σ a_6j kμ_j (and its error), λ error
+        T* __restrict__ mu0 = mu + (size_t)mc * P;
+        T* __restrict__ mu1 = mu + (size_t)(mc ^ 1) * P;
+        double s = 0.0;
+        for (int q = threadIdx.x; q < P; q += blockDim.x) {
+            T v = mu0[q];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) v = kfma<T>((T)(h * TA[5][m]), km[(size_t)ks[m] * P + q], v);
+            mu1[q] = v;
+            if (a.adaptive) {
+                double ev = 0.0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], (double)km[(size_t)ks[m] * P + q], ev);
+                const double e = ::fma(h * BT[6], (double)km[(size_t)ks[6] * P + q], ev);
+                const double sk = ::fma(a.reltol, ::fmax(kabs((double)mu0[q]), kabs((double)v)), a.abstol);
+                s += (e / sk) * (e / sk);
+            }
+        }
+        double hnew = h;
+        if (a.adaptive) {
+            if (act) {
+                double ev = 0.0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], (double)kl[m], ev);
+                const double e = ::fma(h * BT[6], (double)kl[6], ev);
+                const double sk = ::fma(a.reltol, ::fmax(kabs((double)lam), kabs((double)ls)), a.abstol);
+                s += (e / sk) * (e / sk);
+            }
+            const double eest = ::sqrt(bsum(s) / (double)ntot);
+            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            if (eest > 1.0 && h > a.dtmin) {
+                ++nreject;
+                h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
+                __syncthreads();   // mu1 is rewritten by the retry
+                continue;
+            }
+            double q = q11 / ::pow(qold, a.beta2);
+            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
+            if (1.0 <= q && q <= 1.0) q = 1.0;
+            hnew = q > 0 ? h / q : h * a.qmax;
+            qold = ::fmax(eest, a.qoldinit);
+        }
+        __syncthreads();   // mu1 complete
+        tau = tau + h;
+        lam = ls;          // λ <- the last stage input (λ + h Σ a_6j kλ_j)
+        mc ^= 1;
+        kl[0] = kl[6];     // FSAL
+        k0 = ks[6];
+        ++naccept;
+        if (::fabs(tau - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT)) {
+            tau = a.stops[si];
+            if (si + 1 < a.nstops) {
+                if (dl && a.joff[si + 2] > a.joff[si + 1]) {
+                    lam = add_rows((int)si + 1, lam);   // callback: λ += ∂L/∂u(t_j)
+                    kl[0] = adj(tau, lam, k0);          // u_modified!: FSAL re-evaluated
+                    ++nf;
+                }
+            }
+            si = si + 1 < a.nstops ? si + 1 : a.nstops - 1;
+        }
+        h = hnew;
+    }
+    if (it == a.maxiters && !(tau >= TT - 1e-14 * ::fmax(1.0, TT))) status = 1;
+    if (dl) lam = add_rows((int)a.nstops, lam);
+    if (a.du0 && act) reinterpret_cast<T*>(a.du0)[idx] = lam;
+    if (a.dp)
+        for (int q = threadIdx.x; q < P; q += blockDim.x) reinterpret_cast<T*>(a.dp)[q] = mu[(size_t)mc * P + q];
+    if (threadIdx.x == 0) {
+        a.out[0] = naccept;
+        a.out[1] = nreject;
+        a.out[2] = nf;
+        a.out[3] = status;
+    }
+}
+
+// The one-workgroup adjoint (kd_chain_adjoint_kernel): the small-chain conditions of
+// launch_kd_chain_tsit5 plus nsteps <= kChainAdjointMaxSteps and the LDS budget.
+template <typename T>
+hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st) {
+    if (nl < 1 || nl > kChainMaxLayers || B < 1 || B > kChainSolveMaxBatch || I_ne_O(hlcs, nl) || a.nsteps < 1 ||
+        a.nsteps > kChainAdjointMaxSteps)
+        return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    const int threads = (int)((B * kChainDim + kWave - 1) / kWave) * kWave;
+    const int NG = threads / kChainDim;
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + NG + 9) + 2 * sizeof(double) * a.nsteps + 16;
+    if (lds > 60 * 1024 || (P * sizeof(T)) % 8) return hipErrorNotSupported;
+    const LayerConst& h = hlcs[0];
+#define KAN_CADJ(NORM, PATH)                                                                                     \
+    hipLaunchKernelGGL((kd_chain_adjoint_kernel<T, NORM, PATH>), dim3(1), dim3(threads), lds, st, lcs, nl, p,     \
+                       (int)P, B, a)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CADJ(NORM_TANH_FAST, PATH_REC);
+    else if (h.path == PATH_REC_CORR) KAN_CADJ(NORM_RUNTIME, PATH_REC_CORR);
+    else if (h.path == PATH_REC) KAN_CADJ(NORM_RUNTIME, PATH_REC);
+    else KAN_CADJ(NORM_RUNTIME, PATH_DIRECT);
+#undef KAN_CADJ
+    return hipGetLastError();
+}
+
 // The one-workgroup solve (kd_chain_tsit5_kernel): every layer small, one normalizer/path
 // specialisation, N_in == N_out, B <= kChainSolveMaxBatch; hipErrorNotSupported otherwise.
 template <typename T>
@@ -942,6 +1244,8 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
     template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
     template hipError_t launch_kd_chain_tsit5<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,   \
                                                  const T*, int64_t, const ChainSolveArgs&, hipStream_t);         \
+    template hipError_t launch_kd_chain_adjoint<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t, \
+                                                   int64_t, const ChainAdjointArgs&, hipStream_t);               \
     template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
                                              int64_t, hipStream_t);                                               \
     template hipError_t launch_kd_vjp_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, const T*,  \

@@ -183,6 +183,32 @@ struct ChainSolveArgs {
     double* dts;      // [cap] step sizes (with rec)
     int64_t* out;     // naccept, nreject, nf, status
 };
+// InterpolatingAdjoint of a small chain in one workgroup (kd_chain_adjoint_kernel): the backward
+// Tsit5 over [λ; μ] of kanode_solve.cpp adjoint_t, reading the dense output that
+// kd_chain_tsit5_kernel recorded.  Jump rows of dl_du come grouped: group 0 at τ = 0 (t = tf),
+// group 1 + si at stop si (si < nstops - 1), group nstops at t0 (after the loop).
+struct ChainAdjointArgs {
+    double t0, tf, dt, abstol, reltol, dtmin, beta1, beta2, gamma, qmin, qmax, qoldinit;
+    int32_t adaptive, pad;
+    int64_t maxiters;
+    const void* rec;        // [nsteps][7][n] (kd_chain_tsit5_kernel layout)
+    const void* k1_0;
+    const double* ts;       // [nsteps]
+    const double* dts;      // [nsteps]
+    int64_t nsteps;
+    const void* dl_du;      // [n_save][n] or null
+    const double* stops;    // [nstops], ascending τ, the last = tf - t0
+    int64_t nstops;
+    const int32_t* jrows;   // dl_du rows, grouped
+    const int32_t* joff;    // [nstops + 2] group offsets into jrows
+    void* du0;              // [n] or null
+    void* dp;               // [P] or null
+    int64_t* out;           // naccept, nreject, nf, status (0 ok, 1 maxiters)
+};
+constexpr int kChainAdjointMaxSteps = 1024;   // forward steps held in LDS
+template <typename T>
+hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st);
 constexpr int kChainSolveMaxBatch = 16;   // columns of one workgroup (256 lanes / 16)
 template <typename T>
 hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,

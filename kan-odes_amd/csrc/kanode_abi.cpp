@@ -973,6 +973,19 @@ bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
         if (h->kind[l] != KIND_COL) return false;
     return true;
 }
+kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
+                                            const kan::ChainAdjointArgs* a, void* stream, bool& launched) {
+    launched = false;
+    const hipStream_t st = (hipStream_t)stream;
+    const hipError_t e =
+        h->spec.dtype == KANODE_F64
+            ? kan::launch_kd_chain_adjoint<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P, batch, *a, st)
+            : kan::launch_kd_chain_adjoint<float>(h->hlc, h->n_layers, h->dlc, (const float*)p, h->P, batch, *a, st);
+    if (e == hipErrorNotSupported) return KANODE_OK;
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_adjoint: ") + hipGetErrorString(e));
+    launched = true;
+    return KANODE_OK;
+}
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched) {
     launched = false;

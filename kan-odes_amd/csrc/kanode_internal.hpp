@@ -12,6 +12,7 @@
 
 namespace kan {
 struct ChainSolveArgs;
+struct ChainAdjointArgs;
 }
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -41,7 +42,9 @@ void kanode_internal_vjp_discard(kanode_handle* h);
 // batch qualify, and the launch (launched = false when the kernel does not cover the shape)
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch);
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
-                                          const kan::ChainSolveArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
+                                          const kan::ChainSolveArgs* a, void* stream, bool& launched);
+kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
+                                            const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;
 // while *skip != 0 (device, nullable) the stage kernels return at once (a finished graph-mode solve)
 kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,

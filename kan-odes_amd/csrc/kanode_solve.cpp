@@ -109,6 +109,8 @@ struct kanode_solution {
         double* ts = nullptr;              // [cap] then dts [cap]
         int64_t ts_cap = 0;
         int64_t* out = nullptr;            // naccept, nreject, nf, status
+        void* adj_meta = nullptr;          // adjoint: stops, jump rows and offsets
+        size_t adj_meta_bytes = 0;
     } fused;
     double* dscal = nullptr;         // device scalars (norm totals)
     double* hscal = nullptr;         // pinned host mirror
@@ -144,7 +146,7 @@ struct kanode_solution {
     ~kanode_solution() {
         if (!slots_borrowed)
             for (void* s : slots) (void)hipFree(s);
-        for (void* q : {fused.block, (void*)fused.saveat, (void*)fused.ts, (void*)fused.out})
+        for (void* q : {fused.block, (void*)fused.saveat, (void*)fused.ts, (void*)fused.out, fused.adj_meta})
             if (q) (void)hipFree(q);
         if (k1_0) (void)hipFree(k1_0);
         if (dscal) (void)hipFree(dscal);
@@ -935,6 +937,120 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     return KANODE_OK;
 }
 
+// ---- one-workgroup adjoint of a small chain (kd_chain_adjoint_kernel) ---------------------
+// Needs the contiguous dense output of the one-workgroup forward solve; done = false when not
+// covered (the host loop adjoint_t runs instead).
+template <typename T>
+kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0,
+                              void* dp, const kanode_solver_options& o, kanode_solve_stats* stats, hipStream_t st,
+                              bool& done) {
+    done = false;
+    const int64_t nsteps = (int64_t)s->ts.size();
+    if (o.control != 0 || capturing(st) || !s->slots_borrowed || nsteps < 1 ||
+        !kanode_internal_chain_tsit5_ok(h, s->batch))
+        return KANODE_OK;
+    if (!o.adaptive && !(o.dt > 0))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step adjoint needs opt->dt > 0");
+    const double t0 = s->t0, tf = s->tf, TT = tf - t0;
+    const double eps = 1e-12 * std::max(1.0, std::fabs(tf));
+    // the jump groups of adjoint_t: distinct saveat values and their dl_du rows
+    struct Jump { double ts; std::vector<int32_t> rows; };
+    std::vector<Jump> jumps;
+    for (int64_t jx = 0; jx < (int64_t)s->saveat.size(); ++jx) {
+        auto f = std::find_if(jumps.begin(), jumps.end(), [&](const Jump& x) { return x.ts == s->saveat[jx]; });
+        if (f == jumps.end()) jumps.push_back({s->saveat[jx], {(int32_t)jx}});
+        else f->rows.push_back((int32_t)jx);
+    }
+    std::vector<std::pair<double, int>> st_j;   // (τ of the stop, jump)
+    std::vector<int32_t> init_rows, final_rows;
+    if (dl_du) {
+        for (int q = 0; q < (int)jumps.size(); ++q) {
+            const Jump& jm = jumps[q];
+            if (jm.ts == tf) init_rows.insert(init_rows.end(), jm.rows.begin(), jm.rows.end());
+            else if (t0 + eps < jm.ts && jm.ts < tf - eps) st_j.push_back({tf - jm.ts, q});
+            else if (std::fabs(jm.ts - t0) <= eps) final_rows.insert(final_rows.end(), jm.rows.begin(), jm.rows.end());
+        }
+    }
+    std::sort(st_j.begin(), st_j.end());
+    std::vector<double> stops;
+    std::vector<int32_t> rows(init_rows), off{0, (int32_t)init_rows.size()};
+    for (auto& x : st_j) {
+        stops.push_back(x.first);
+        const Jump& jm = jumps[x.second];
+        const bool hit = std::fabs(jm.ts - (tf - x.first)) <= eps;
+        if (hit) rows.insert(rows.end(), jm.rows.begin(), jm.rows.end());
+        off.push_back((int32_t)rows.size());
+    }
+    stops.push_back(TT);
+    rows.insert(rows.end(), final_rows.begin(), final_rows.end());
+    off.push_back((int32_t)rows.size());
+    const int64_t ns = (int64_t)stops.size();
+    // device copies: stops | joff | jrows
+    const size_t bytes = ns * sizeof(double) + off.size() * sizeof(int32_t) + (rows.size() + 1) * sizeof(int32_t) + 64;
+    auto& f = s->fused;
+    if (f.adj_meta_bytes < bytes) {
+        if (f.adj_meta) (void)hipFree(f.adj_meta);
+        f.adj_meta = nullptr;
+        f.adj_meta_bytes = 0;
+        SOLVE_HIP(h, hipMalloc(&f.adj_meta, bytes));
+        f.adj_meta_bytes = bytes;
+    }
+    std::vector<char> host(bytes, 0);
+    double* dstops = (double*)f.adj_meta;
+    int32_t* djoff = (int32_t*)((char*)f.adj_meta + ns * sizeof(double));
+    int32_t* djrows = djoff + off.size();
+    std::memcpy(host.data(), stops.data(), ns * sizeof(double));
+    std::memcpy(host.data() + ns * sizeof(double), off.data(), off.size() * sizeof(int32_t));
+    if (!rows.empty())
+        std::memcpy(host.data() + ns * sizeof(double) + off.size() * sizeof(int32_t), rows.data(),
+                    rows.size() * sizeof(int32_t));
+    SOLVE_HIP(h, hipMemcpy(f.adj_meta, host.data(), bytes, hipMemcpyHostToDevice));
+    if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
+    kan::ChainAdjointArgs a{};
+    a.t0 = t0;
+    a.tf = tf;
+    a.dt = o.dt;
+    a.abstol = o.abstol;
+    a.reltol = o.reltol;
+    a.dtmin = o.dtmin;
+    a.beta1 = o.beta1;
+    a.beta2 = o.beta2;
+    a.gamma = o.gamma;
+    a.qmin = o.qmin;
+    a.qmax = o.qmax;
+    a.qoldinit = o.qoldinit;
+    a.adaptive = o.adaptive ? 1 : 0;
+    a.maxiters = o.maxiters;
+    a.rec = f.block;
+    a.k1_0 = s->k1_0;
+    a.ts = f.ts;
+    a.dts = f.ts + f.cap;
+    a.nsteps = nsteps;
+    a.dl_du = dl_du;
+    a.stops = dstops;
+    a.nstops = ns;
+    a.jrows = djrows;
+    a.joff = djoff;
+    a.du0 = du0;
+    a.dp = dp;
+    a.out = f.out;
+    bool launched = false;
+    SOLVE_TRY(kanode_internal_chain_adjoint(h, p, s->batch, &a, st, launched));
+    if (!launched) return KANODE_OK;
+    SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    int64_t res[4];
+    std::memcpy(res, s->hscal, sizeof(res));
+    if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
+    if (stats) {
+        stats->naccept = res[0];
+        stats->nreject = res[1];
+        stats->nf = res[2];
+    }
+    done = true;
+    return KANODE_OK;
+}
+
 kanode_status check_opts(kanode_handle* h, const kanode_solver_options& o) {
     if (!(o.abstol >= 0) || !(o.reltol >= 0) || o.maxiters < 1 || !(o.qmin > 0) || !(o.qmax > 0) || !(o.gamma > 0))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solver options out of range");
@@ -1043,6 +1159,10 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint: dense output of another handle or not recorded");
     hipStream_t st = (hipStream_t)stream;
     TableHold hold(h);
+    bool done = false;
+    SOLVE_TRY(s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
+                                     : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done));
+    if (done) return KANODE_OK;
     return s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
                                   : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);
 }

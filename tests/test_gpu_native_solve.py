@@ -346,6 +346,29 @@ def test_fused_chain_solve_matches_host_loop(dtype, B, adaptive):
     assert (gf - gh).abs().max().item() <= gtol * gh.abs().max().item()
 
 
+@pytest.mark.parametrize("ts", [[0.0, 0.5, 0.5, 1.2, 3.5], [0.25, 3.0], [3.5]])
+def test_fused_chain_adjoint_saveat_edges(ts):
+    """The one-workgroup adjoint's jumps: saveat at t0 (applied after the loop), duplicates (rows
+    summed), tf (the initial λ) and interior stops, against the host loop."""
+    rhs = lv()
+    u0 = t(_lv_u0(3, 6))
+    p0 = t(np.random.default_rng(8).uniform(-0.3, 0.3, 240))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7)
+    w = t(np.random.default_rng(3).normal(size=(len(ts), 3, 2)))
+    res = {}
+    for control in ("auto", "host"):
+        p = p0.clone().requires_grad_(True)
+        u = u0.clone().requires_grad_(True)
+        sol = kanode.solve(rhs, u, (0.0, 3.5), p, ts, dataclasses.replace(opt, control=control),
+                           sensealg="interpolating_adjoint")
+        gp, gu = torch.autograd.grad((sol.u * w).sum(), [p, u])
+        res[control] = (sol, gp, gu)
+    (sa, pa, ua), (sh, ph, uh) = res["auto"], res["host"]
+    assert sa.stats["adjoint"]["naccept"] == sh.stats["adjoint"]["naccept"]
+    assert (pa - ph).abs().max().item() <= 1e-9 * ph.abs().max().item()
+    assert (ua - uh).abs().max().item() <= 1e-9 * max(1e-300, uh.abs().max().item())
+
+
 def test_fused_chain_solve_falls_back_when_dense_output_fills(monkeypatch):
     """A dense output larger than the fused block (KANODE_FUSED_CAP, tests only) falls back to the
     host loop: same steps, same values, a usable dense output."""
