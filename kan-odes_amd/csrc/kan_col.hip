@@ -116,19 +116,58 @@ kd_fwd_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, c
 // 16x the waves of a thread-per-column kernel, each with 1/I of the serial work: at 4096
 // columns the per-column latency chain, not launch count, bounds it.  The parameter vector
 // and the layers' constants are staged in LDS once per block (wave-uniform LDS reads).
+// Layer dimensions of a small chain: read from the layer constants (ChainShapeAny) or fixed at
+// compile time for the Lotka-Volterra KAN [2,10,2], G = 5 (LV_driver_KANODE.jl:139-142), where
+// the loops over outputs and knots then unroll to exactly the live iterations (the generic code
+// runs all 16 output slots per layer: ~3x the instructions on a latency-bound single wave).
+struct ChainShapeAny {
+    static constexpr int NL = 0;
+    static constexpr int dim(int) { return 0; }
+    static constexpr int GG = 0;
+};
+template <int D0, int D1, int D2, int G_>
+struct ChainShape2 {
+    static constexpr int NL = 2;
+    static constexpr int dim(int l) { return l == 0 ? D0 : (l == 1 ? D1 : D2); }
+    static constexpr int GG = G_;
+};
+using ChainShapeLV = ChainShape2<2, 10, 2, 5>;
+template <class S> __device__ __forceinline__ int sh_nl(int nl) {
+    if constexpr (S::NL > 0) return S::NL;
+    else return nl;
+}
+template <class S> __device__ __forceinline__ int sh_I(const LayerConst& lc, int l) {
+    if constexpr (S::NL > 0) return S::dim(l);
+    else return lc.I;
+}
+template <class S> __device__ __forceinline__ int sh_O(const LayerConst& lc, int l) {
+    if constexpr (S::NL > 0) return S::dim(l + 1);
+    else return lc.O;
+}
+template <class S> __device__ __forceinline__ int sh_G(const LayerConst& lc) {
+    if constexpr (S::NL > 0) return S::GG;
+    else return lc.G;
+}
+static bool chain_is_lv(const LayerConst* hlcs, int nl) {
+    return nl == 2 && hlcs[0].I == 2 && hlcs[0].O == 10 && hlcs[1].I == 10 && hlcs[1].O == 2 && hlcs[0].G == 5 &&
+           hlcs[1].G == 5;
+}
+
 // The forward of a whole small chain for one column group (16 lanes, lane j holds entry j of the
 // activation): lane i evaluates the basis and swish of input i and its partial sums for every
 // output o, butterfly shuffles sum them over the group, lane o keeps output o.
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S = ChainShapeAny>
 __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a);
 
 constexpr int kChainBlock = 256;
 constexpr int kChainDim = 16;    // lanes per column = max layer width
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S>
 __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a) {
-    for (int l = 0; l < nl; ++l) {
+    const int nlc = sh_nl<S>(nl);
+#pragma unroll
+    for (int l = 0; l < nlc; ++l) {
         const LayerConst& lc = lcl[l];
-        const int I = lc.I, O = lc.O, G = lc.G;
+        const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
         const T* __restrict__ C = ps + lc.p_off;
         const T* __restrict__ W = ps + lc.w_off;
         T acc[kChainDim], bas[kChainDim];
@@ -167,7 +206,7 @@ __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* l
     return a;
 }
 
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
                     const T* __restrict__ x, T* __restrict__ y, int64_t K, StageArgs<T> sa, T* __restrict__ y_out,
@@ -209,7 +248,7 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
             if (y_out) y_out[idx] = a;
         }
         const T yin = a;
-        a = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, a);
+        a = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, a);
         if (j < OL) {
             y[(int64_t)OL * k + j] = a;
             if (want_err) {
@@ -235,7 +274,7 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
 // (the arithmetic and order of kanode_solve.cpp solve_t / tsit5_post_kernel: Hairer-Wanner
 // initial step, PI controller, saveat from the dense output, FSAL).  No launch or host
 // round trip per stage or step: the host loop pays ~6 launches + one 8-byte read per step.
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
                       const T* __restrict__ u0, int64_t B, ChainSolveArgs a) {
@@ -283,7 +322,7 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
     };
     T u = act ? u0[idx] : T(0);
     T k[7];
-    k[0] = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, u);
+    k[0] = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, u);
     if (rec && act) reinterpret_cast<T*>(a.k1_0)[idx] = k[0];
     const double t0 = a.t0, tf = a.tf;
     int64_t si = 0;
@@ -298,7 +337,7 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
         const double d1 = ::sqrt(bsum(((double)k[0] / sk) * ((double)k[0] / sk)) / (double)n);
         double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         dt0 = ::fmin(dt0, tf - t0);
-        const T f1 = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, kfma<T>((T)dt0, k[0], u));
+        const T f1 = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, kfma<T>((T)dt0, k[0], u));
         const double e = ::fma(-1.0, (double)k[0], (double)f1) / sk;
         const double d2 = ::sqrt(bsum(e * e) / (double)n) / dt0;
         const double mx = ::fmax(d1, d2);
@@ -316,7 +355,7 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
             y = u;
 #pragma unroll
             for (int m = 0; m <= i; ++m) y = kfma<T>((T)(dt * TA[i][m]), k[m], y);
-            k[i + 1] = chain_forward<T, NORM, PATH>(M, lcl, nl, ps, j, y);
+            k[i + 1] = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, y);
         }
         nf += 6;
         double dtnew = dt;
@@ -400,7 +439,7 @@ constexpr int kChainMaxLayers = 4;
 // ȳ of the last layer is lj, lane i of layer l turns it into x̄_i and adds ȳ_o φ_g(x_i),
 // ȳ_o swish(x_i) into its own entries of the group's LDS gradient row (disjoint per lane).
 // Returns λᵀ∂f/∂u (lane j: entry j).
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S = ChainShapeAny>
 __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps,
                                             T* __restrict__ row, int j, T yj, T lj) {
     // forward: the input activation of every layer (lane j holds entry j)
@@ -409,9 +448,9 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
 #pragma unroll
     for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
         act[l + 1] = T(0);
-        if (l + 1 < nl) {
+        if (l + 1 < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
-            const int I = lc.I, O = lc.O, G = lc.G;
+            const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
             const T* __restrict__ C = ps + lc.p_off;
             const T* __restrict__ W = ps + lc.w_off;
             T acc[kChainDim], bas[kChainDim];
@@ -452,9 +491,9 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
     T ybar = lj;
 #pragma unroll
     for (int l = kChainMaxLayers - 1; l >= 0; --l) {
-        if (l < nl) {
+        if (l < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
-            const int I = lc.I, O = lc.O, G = lc.G;
+            const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
             const T* __restrict__ C = ps + lc.p_off;
             const T* __restrict__ W = ps + lc.w_off;
             T yb[kChainDim];
@@ -508,7 +547,7 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
     return ybar;
 }
 
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainVjpBlock)
 kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
                           const T* __restrict__ u, StageArgs<T> su, const T* __restrict__ lam, StageArgs<T> sl,
@@ -558,7 +597,7 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
             }
             if (lam_out) lam_out[idx] = lj;
         }
-        const T ybar = chain_pullback<T, NORM, PATH>(M, lcl, nl, ps, row, j, yj, lj);
+        const T ybar = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, row, j, yj, lj);
         if (j < N0) {
             lamJ[idx] = ybar;
             if (want_err) {
@@ -859,14 +898,16 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
     double* es = err_out && !one ? err_slab : nullptr;
     double* ed = err_out && one ? err_out : nullptr;
     const LayerConst& h = hlcs[0];
-#define KAN_CHAIN(NORM, PATH)                                                                                    \
-    hipLaunchKernelGGL((kd_chain_col_kernel<T, NORM, PATH>), dim3(g), dim3(kChainBlock), lds, st, lcs, nl, p,     \
+#define KAN_CHAIN_S(NORM, PATH, S)                                                                                    \
+    hipLaunchKernelGGL((kd_chain_col_kernel<T, NORM, PATH, S>), dim3(g), dim3(kChainBlock), lds, st, lcs, nl, p,     \
                        (int)P, x, y, K, s, y_out, es, ed)
-    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CHAIN(NORM_TANH_FAST, PATH_REC);
-    else if (h.path == PATH_REC_CORR) KAN_CHAIN(NORM_RUNTIME, PATH_REC_CORR);
-    else if (h.path == PATH_REC) KAN_CHAIN(NORM_RUNTIME, PATH_REC);
-    else KAN_CHAIN(NORM_RUNTIME, PATH_DIRECT);
-#undef KAN_CHAIN
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CHAIN_S(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CHAIN_S(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CHAIN_S(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CHAIN_S(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CHAIN_S(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
+#undef KAN_CHAIN_S
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !es) return e;
     return launch_stage_error_final(err_slab, g, err_out, st);
@@ -880,7 +921,7 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
 // adds into its own LDS gradient row) and reduces the rows into the stage's kμ (LDS), in the
 // order kd_chain_vjp_stage_kernel + chain_vjp_finish_kernel use (4 groups per block, then the
 // blocks).  μ and its seven stage vectors live in LDS; the error norm covers λ and μ.
-template <typename T, int NORM, int PATH>
+template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t B,
                         ChainAdjointArgs a) {
@@ -978,7 +1019,7 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
                 y = kfma<T>((T)(b * dti), kv[m], y);
             }
         }
-        const T lj = chain_pullback<T, NORM, PATH>(M, lcl, nl, ps, row, j, y, act ? ls : T(0));
+        const T lj = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, row, j, y, act ? ls : T(0));
         __syncthreads();
         // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order
         for (int q = threadIdx.x; q < P; q += blockDim.x) {
@@ -1151,14 +1192,16 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
     const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + NG + 9) + 2 * sizeof(double) * a.nsteps + 16;
     if (lds > 60 * 1024 || (P * sizeof(T)) % 8) return hipErrorNotSupported;
     const LayerConst& h = hlcs[0];
-#define KAN_CADJ(NORM, PATH)                                                                                     \
-    hipLaunchKernelGGL((kd_chain_adjoint_kernel<T, NORM, PATH>), dim3(1), dim3(threads), lds, st, lcs, nl, p,     \
+#define KAN_CADJ_S(NORM, PATH, S)                                                                                     \
+    hipLaunchKernelGGL((kd_chain_adjoint_kernel<T, NORM, PATH, S>), dim3(1), dim3(threads), lds, st, lcs, nl, p,     \
                        (int)P, B, a)
-    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CADJ(NORM_TANH_FAST, PATH_REC);
-    else if (h.path == PATH_REC_CORR) KAN_CADJ(NORM_RUNTIME, PATH_REC_CORR);
-    else if (h.path == PATH_REC) KAN_CADJ(NORM_RUNTIME, PATH_REC);
-    else KAN_CADJ(NORM_RUNTIME, PATH_DIRECT);
-#undef KAN_CADJ
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CADJ_S(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CADJ_S(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CADJ_S(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CADJ_S(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CADJ_S(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
+#undef KAN_CADJ_S
     return hipGetLastError();
 }
 
@@ -1178,14 +1221,16 @@ hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerCons
     if (lds > 48 * 1024) return hipErrorNotSupported;
     const int threads = (int)((B * kChainDim + kWave - 1) / kWave) * kWave;
     const LayerConst& h = hlcs[0];
-#define KAN_CSOLVE(NORM, PATH)                                                                                   \
-    hipLaunchKernelGGL((kd_chain_tsit5_kernel<T, NORM, PATH>), dim3(1), dim3(threads), lds, st, lcs, nl, p, (int)P, \
+#define KAN_CSOLVE_S(NORM, PATH, S)                                                                                   \
+    hipLaunchKernelGGL((kd_chain_tsit5_kernel<T, NORM, PATH, S>), dim3(1), dim3(threads), lds, st, lcs, nl, p, (int)P, \
                        u0, B, a)
-    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CSOLVE(NORM_TANH_FAST, PATH_REC);
-    else if (h.path == PATH_REC_CORR) KAN_CSOLVE(NORM_RUNTIME, PATH_REC_CORR);
-    else if (h.path == PATH_REC) KAN_CSOLVE(NORM_RUNTIME, PATH_REC);
-    else KAN_CSOLVE(NORM_RUNTIME, PATH_DIRECT);
-#undef KAN_CSOLVE
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CSOLVE_S(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CSOLVE_S(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CSOLVE_S(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CSOLVE_S(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CSOLVE_S(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
+#undef KAN_CSOLVE_S
     return hipGetLastError();
 }
 
@@ -1217,14 +1262,16 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
     double* eslab = err_out ? (double*)((char*)slab + (((size_t)grid * P * sizeof(T) + 255) & ~(size_t)255)) : nullptr;
     const LayerConst& h = hlcs[0];
     const bool one = grid == 1;   // a single block writes dp and the error total itself
-#define KAN_CVJP(NORM, PATH)                                                                                     \
-    hipLaunchKernelGGL((kd_chain_vjp_stage_kernel<T, NORM, PATH>), dim3(grid), dim3(kChainVjpBlock), lds, st,    \
+#define KAN_CVJP(NORM, PATH, S)                                                                                  \
+    hipLaunchKernelGGL((kd_chain_vjp_stage_kernel<T, NORM, PATH, S>), dim3(grid), dim3(kChainVjpBlock), lds, st, \
                        lcs, nl, p, (int)P, u, su, lam, sl, lam_out, lamJ, one ? nullptr : tslab,                  \
                        one ? nullptr : eslab, K, one ? dp : nullptr, dp_assign ? 1 : 0, one ? err_out : nullptr)
-    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CVJP(NORM_TANH_FAST, PATH_REC);
-    else if (h.path == PATH_REC_CORR) KAN_CVJP(NORM_RUNTIME, PATH_REC_CORR);
-    else if (h.path == PATH_REC) KAN_CVJP(NORM_RUNTIME, PATH_REC);
-    else KAN_CVJP(NORM_RUNTIME, PATH_DIRECT);
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CVJP(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CVJP(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CVJP(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CVJP(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CVJP(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
 #undef KAN_CVJP
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || one || (!dp && !err_out)) return e;
