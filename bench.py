@@ -178,6 +178,47 @@ def lv4096_bench(dev, steps: int = 200):
             "note": f"device time per RHS from a hipGraph of {steps} launches (one fused-chain kernel each)"}
 
 
+def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
+    """BASELINE configs[0] shape: one LV_driver_KANODE.jl training iteration (KAN [2,10,2] G=5,
+    u0 = [1, 1], tspan (0, 3.5), saveat 0:0.1:3.4, adaptive Tsit5 at the default tolerances,
+    InterpolatingAdjoint, Adam; LV_driver_KANODE.jl:119-122,139-143,175-219).  On the GPU a
+    single trajectory runs the forward solve and the adjoint as one workgroup each
+    (kd_chain_tsit5_kernel, kd_chain_adjoint_kernel).  CPU: the oracle chain driven by the same
+    integrator statement in Python (kind "port"); Julia is not available to time the reference."""
+    from scipy.integrate import solve_ivp
+    ts = [0.1 * i for i in range(35)]
+    f = lambda t, x: [1.5 * x[0] - x[0] * x[1], x[0] * x[1] - 3.0 * x[1]]   # noqa: E731
+    target = solve_ivp(f, (0.0, 3.5), [1.0, 1.0], t_eval=ts, method="DOP853", rtol=1e-10,
+                       atol=1e-12).y.T[:, None, :]
+    chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
+    p0 = chain.setup(np.random.default_rng(0))[0].astype(np.float64) / 1e5 * 1e4   # a mid-training scale
+    legs = [("gpu", dev, kanode.ChainRHS(chain, device=dev), reps)]
+    if with_cpu:
+        from oracle import oracle as O
+        from oracle.oracle_rhs import OracleChainRHS
+        legs.append(("cpu", "cpu", OracleChainRHS([O.LayerSpec(2, 10, 5, "tanh_fast"),
+                                                   O.LayerSpec(10, 2, 5, "tanh_fast")]), 2))
+    out = {"unit": "ms/iteration", "batch": 1, "dtype": "f64",
+           "what": "adaptive Tsit5 solve + InterpolatingAdjoint + Adam, LV KAN [2,10,2] G=5, one trajectory"}
+    for name, d, rhs, n in legs:
+        tr = kanode.Trainer(rhs, torch.tensor([[1.0, 1.0]], dtype=torch.float64, device=d), (0.0, 3.5), ts,
+                            torch.as_tensor(target, device=d), torch.as_tensor(p0, device=d), eta=1e-3,
+                            sensealg="interpolating_adjoint")
+        tr.step()
+        if name == "gpu":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            tr.step()
+        if name == "gpu":
+            torch.cuda.synchronize()
+        out[name] = (time.perf_counter() - t0) / n * 1e3
+    if with_cpu:
+        out.update({"cpu_cores": 1, "cpu_kind": "port (oracle chain, numpy; Python Tsit5 + adjoint driver)",
+                    "speedup": out["cpu"] / out["gpu"]})
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,6 +366,7 @@ def main() -> None:
 
     if rank == 0 and not args.no_vjp:
         out["lv4096"] = lv4096_bench(dev)
+        out["lv1_train"] = lv1_train_bench(dev, world == 1 and not args.no_cpu_baseline)
 
     if not args.no_epoch and rank == 0:
         out["epoch"] = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch,
