@@ -159,11 +159,12 @@ __device__ __forceinline__ void tsit5_interp_weights(double th, double w[7]) {
         {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
         {0.0, 1.5, -4.0, 2.5},
     };
+    const double th2 = th * th, tp[4] = {th, th2, th2 * th, th2 * th2};   // θ^(m+1) (pow would cost ~4 calls)
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
         double s = 0.0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) s += RI[i][m] * ::pow(th, (double)(m + 1));
+        for (int m = 0; m < 4; ++m) s += RI[i][m] * tp[m];
         w[i] = s;
     }
 }
