@@ -807,6 +807,119 @@ hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, 
     return hipGetLastError();
 }
 
+// du = D·lap·y + KAN(y) for one trajectory row held by one wave (lane: pairs 128k + 2·lane),
+// stencil neighbours by wave rotation, the KAN from the LDS table (direct formula off-table)
+template <int NORM, int BASIS, int NP>
+__device__ __forceinline__ void fk_row_rhs(const Math<double>& M, const LayerConst& lc, const double* __restrict__ p,
+                                           const double2* __restrict__ tl, int ni, double inv_w, double x0, double cd,
+                                           double co, int lane, const kd2 (&y)[NP], kd2 (&du)[NP]) {
+    constexpr int Nx = 128 * NP;
+    double rr[NP], rl[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        rr[k] = wave_ror1(y[k].y);
+        rl[k] = wave_rol1(y[k].x);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+        const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+        const int i = 128 * k + 2 * lane;
+        bool ok0, ok1;
+        double k0 = pp_eval(tl, ni, inv_w, x0, y[k].x, ok0);
+        double k1 = pp_eval(tl, ni, inv_w, x0, y[k].y, ok1);
+        if (__builtin_expect(!(ok0 && ok1), 0)) {
+            double sc;
+            if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].x, sc);
+            if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].y, sc);
+        }
+        double l0, l1;
+        lap_pair<double>(um, y[k].x, y[k].y, up, i, Nx, cd, co, l0, l1);
+        du[k].x = l0 + k0;
+        du[k].y = l1 + k1;
+    }
+}
+
+// A whole Tsit5 step per trajectory row (kanode_solve_tsit5, host control, Fisher-KPP table
+// path): the Laplacian stencil couples only the points of one row, so the six stages run
+// with the row in registers: u and k_1 are read once, k_2..k_7 and u_new written once (the
+// dense output slot), instead of six stage launches re-reading u and k_1..k_s.  Same
+// arithmetic and order as six fk_stage_pp_wave_kernel launches (bitwise equal results);
+// the embedded-error partial Σ (e/sk)² goes to err_slab[block] (ordered).
+struct StepCoef {
+    double a[6][6];   // dt·a_sj
+    double e[7];      // dt·btilde_j
+    double abstol, reltol;
+};
+struct StepOut {
+    double* k[6];     // k_2..k_7
+    double* u_new;
+};
+template <int NORM, int BASIS, int NP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                       const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
+                       const double* __restrict__ u, const double* __restrict__ k1, StepOut so, StepCoef sc,
+                       double* __restrict__ err_slab, int64_t B) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    __shared__ double red[kBlock / kWave];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    const Math<double> M{tab};
+    const LayerConst& lc = *lcp;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool want_err = err_slab != nullptr;
+    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
+    double eacc = 0.0;
+    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+        const int64_t rb = b * Nx + 2 * lane;
+        kd2 uv[NP], kk[7][NP], y[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            uv[k] = ld_stream(u + rb + 128 * k);
+            kk[0][k] = ld_stream(k1 + rb + 128 * k);
+        }
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                y[k] = uv[k];
+#pragma unroll
+                for (int j = 0; j <= s; ++j) {
+                    y[k].x = ::fma(sc.a[s][j], kk[j][k].x, y[k].x);
+                    y[k].y = ::fma(sc.a[s][j], kk[j][k].y, y[k].y);
+                }
+            }
+            fk_row_rhs<NORM, BASIS, NP>(M, lc, p, tl, ni, inv_w, x0, cd, co, lane, y, kk[s + 1]);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) st_stream(so.k[s] + rb + 128 * k, kk[s + 1][k]);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            st_stream(so.u_new + rb + 128 * k, y[k]);
+            if (want_err) {
+                kd2 e{0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    e.x = ::fma(sc.e[j], kk[j][k].x, e.x);
+                    e.y = ::fma(sc.e[j], kk[j][k].y, e.y);
+                }
+                const double ex = ::fma(sc.e[6], kk[6][k].x, e.x), ey = ::fma(sc.e[6], kk[6][k].y, e.y);
+                const double sx = ::fma(sc.reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), sc.abstol);
+                const double sy = ::fma(sc.reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), sc.abstol);
+                const double rx = ex / sx, ry = ey / sy;
+                eacc = ::fma(rx, rx, eacc);
+                eacc = ::fma(ry, ry, eacc);
+            }
+        }
+    }
+    if (want_err) {
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+    }
+}
+
 // Runge-Kutta stage, fused (kanode_rhs_stage): the stage input y = u + Σ_j c_j k_j is
 // formed in registers from nontemporal loads of u and the k_j, the stencil
 // neighbours of y come from the wave rotations, du = f(y) as above.  Optionally y
@@ -843,30 +956,12 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         }
         if (want_err) stage_sum<NP, true>(sa, rb, sac, y, e);
         else stage_sum<NP, false>(sa, rb, sac, y, e);
-        double rr[NP], rl[NP];
+        kd2 dv[NP];
+        fk_row_rhs<NORM, BASIS, NP>(M, lc, p, tl, ni, inv_w, x0, cd, co, lane, y, dv);
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            rr[k] = wave_ror1(y[k].y);
-            rl[k] = wave_rol1(y[k].x);
-        }
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            const double um = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
-            const double up = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
             const int i = 128 * k + 2 * lane;
-            bool ok0, ok1;
-            double k0 = pp_eval(tl, ni, inv_w, x0, y[k].x, ok0);
-            double k1 = pp_eval(tl, ni, inv_w, x0, y[k].y, ok1);
-            if (__builtin_expect(!(ok0 && ok1), 0)) {
-                double sc;
-                if (!ok0) k0 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].x, sc);
-                if (!ok1) k1 = pp_direct<NORM, BASIS>(M, lc, p, lc.grid, y[k].y, sc);
-            }
-            double l0, l1;
-            lap_pair<double>(um, y[k].x, y[k].y, up, i, Nx, cd, co, l0, l1);
-            kd2 o;
-            o.x = l0 + k0;
-            o.y = l1 + k1;
+            const kd2 o = dv[k];
             st_stream(du + b * Nx + i, o);
             if (y_out) st_stream(y_out + b * Nx + i, y[k]);
             if (want_err) {
@@ -989,6 +1084,51 @@ hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const L
     else KAN_STAGE_GO(NORM_RUNTIME, -1);
 #undef KAN_STAGE_GO
 #undef KAN_STAGE_WAVE
+    e = hipGetLastError();
+    if (e != hipSuccess || !err_out) return e;
+    return launch_stage_error_final(err_slab, grid, err_out, st);
+}
+
+hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                             const double* p, double* table, double cd, double co, int Nx, const double* u,
+                             const double* k1, double* const* kout, double* u_new, const double* a6x6,
+                             const double* e7, double abstol, double reltol, double* err_slab, int slab_blocks,
+                             double* err_out, int64_t B, hipStream_t st, bool build) {
+    if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
+    const int fn_phi = PP_PHI;
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, table, &fn_phi, 1, st)) != hipSuccess) return e;
+    const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+    StepOut so{};
+    for (int j = 0; j < 6; ++j) so.k[j] = kout[j];
+    so.u_new = u_new;
+    StepCoef sc{};
+    for (int s = 0; s < 6; ++s)
+        for (int j = 0; j < 6; ++j) sc.a[s][j] = a6x6[6 * s + j];
+    for (int j = 0; j < 7; ++j) sc.e[j] = e7 ? e7[j] : 0.0;
+    sc.abstol = abstol;
+    sc.reltol = reltol;
+    int grid = 0;
+    double* slab = err_out ? err_slab : nullptr;
+#define KAN_STEP_WAVE(NORM, BASIS, NP)                                                                           \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_step_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
+        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,  \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, k1, so, sc, slab, B);    \
+    } while (0)
+#define KAN_STEP_GO(NORM, BASIS)                                                                                 \
+    do {                                                                                                         \
+        if (Nx == 256) KAN_STEP_WAVE(NORM, BASIS, 2);                                                            \
+        else if (Nx == 128) KAN_STEP_WAVE(NORM, BASIS, 1);                                                       \
+        else KAN_STEP_WAVE(NORM, BASIS, 4);                                                                      \
+    } while (0)
+    if (hlc.basis == BASIS_RBF && hlc.norm == NORM_SOFTSIGN) KAN_STEP_GO(NORM_SOFTSIGN, BASIS_RBF);
+    else if (hlc.basis == BASIS_RBF && hlc.norm == NORM_TANH_FAST) KAN_STEP_GO(NORM_TANH_FAST, BASIS_RBF);
+    else KAN_STEP_GO(NORM_RUNTIME, -1);
+#undef KAN_STEP_GO
+#undef KAN_STEP_WAVE
     e = hipGetLastError();
     if (e != hipSuccess || !err_out) return e;
     return launch_stage_error_final(err_slab, grid, err_out, st);

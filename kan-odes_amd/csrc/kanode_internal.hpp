@@ -43,6 +43,12 @@ void kanode_internal_vjp_discard(kanode_handle* h);
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch);
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched);
+// a whole Tsit5 step per row on the Fisher-KPP table path (fk_step_pp_wave_kernel); launched =
+// false when the handle is not that path (the caller runs the six stages)
+kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
+                                      void* const* kout, void* u_new, const double* a6x6, const double* e7,
+                                      double abstol, double reltol, double* err_out, int64_t batch, void* stream,
+                                      bool& launched);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

@@ -326,7 +326,17 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         SOLVE_TRY(ensure_slots(h, s, step + 2, st));
         void* ks[7];
         for (int j = 0; j < 7; ++j) ks[j] = s->k(step, j + 1);
-        for (int i = 0; i < 6; ++i) {
+        bool fused_step = false;   // Fisher-KPP table path: the six stages in one launch
+        {
+            double a66[36] = {}, e7[7];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j <= i; ++j) a66[6 * i + j] = dt * TA[i][j];
+            for (int j = 0; j < 7; ++j) e7[j] = dt * BT[j];
+            SOLVE_TRY(kanode_internal_fk_step(h, p, s->u(step), ks[0], ks + 1, s->u(step + 1), a66,
+                                              o.adaptive ? e7 : nullptr, o.abstol, o.reltol,
+                                              o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
+        }
+        for (int i = 0; i < 6 && !fused_step; ++i) {
             double c[6];
             for (int j = 0; j <= i; ++j) c[j] = dt * TA[i][j];
             kanode_stage sg = make_stage(i + 1, ks, c);
