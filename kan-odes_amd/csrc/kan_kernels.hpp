@@ -68,12 +68,13 @@ hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const L
                               const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
                               double* err_out, double* du, int64_t B, hipStream_t st, bool build = true);
 // A whole Tsit5 step of the Fisher-KPP table RHS per trajectory row (fk_step_pp_wave_kernel):
-// a6x6[6s + j] = dt·a_sj, e7 = dt·btilde (error with err_out), k_2..k_7 -> kout[0..5]
+// a6x6[6s + j] = dt·a_sj, e7 = dt·btilde (error with err_out), k_2..k_7 -> kout[0..5]; with
+// q4x7[7m + i] = dt·RI[i][m] the dense output is Q_1..Q_4 -> kout[0..3] and k_7 -> kout[5]
 hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                              const double* p, double* table, double cd, double co, int Nx, const double* u,
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
-                             const double* e7, double abstol, double reltol, double* err_slab, int slab_blocks,
-                             double* err_out, int64_t B, hipStream_t st, bool build);
+                             const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
+                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,

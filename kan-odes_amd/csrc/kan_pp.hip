@@ -849,11 +849,13 @@ __device__ __forceinline__ void fk_row_rhs(const Math<double>& M, const LayerCon
 struct StepCoef {
     double a[6][6];   // dt·a_sj
     double e[7];      // dt·btilde_j
+    double q[4][7];   // dt·RI[i][m] (qform)
     double abstol, reltol;
 };
 struct StepOut {
-    double* k[6];     // k_2..k_7
+    double* k[6];     // k_2..k_7, or (qform) Q_1..Q_4, -, k_7
     double* u_new;
+    int32_t qform;    // dense output as u_n + Σ_m θ^(m+1) Q_m, Q_m = dt Σ_i RI[i][m] k_i
 };
 template <int NORM, int BASIS, int NP>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
@@ -892,8 +894,27 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                 }
             }
             fk_row_rhs<NORM, BASIS, NP>(M, lc, p, tl, ni, inv_w, x0, cd, co, lane, y, kk[s + 1]);
+            if (!so.qform) {
 #pragma unroll
-            for (int k = 0; k < NP; ++k) st_stream(so.k[s] + rb + 128 * k, kk[s + 1][k]);
+                for (int k = 0; k < NP; ++k) st_stream(so.k[s] + rb + 128 * k, kk[s + 1][k]);
+            }
+        }
+        if (so.qform) {   // the interpolation polynomials of the dense output, then k_7 (FSAL)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    kd2 q{0.0, 0.0};
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) {
+                        q.x = ::fma(sc.q[m][i], kk[i][k].x, q.x);
+                        q.y = ::fma(sc.q[m][i], kk[i][k].y, q.y);
+                    }
+                    st_stream(so.k[m] + rb + 128 * k, q);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k) st_stream(so.k[5] + rb + 128 * k, kk[6][k]);
         }
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -1092,8 +1113,8 @@ hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const L
 hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                              const double* p, double* table, double cd, double co, int Nx, const double* u,
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
-                             const double* e7, double abstol, double reltol, double* err_slab, int slab_blocks,
-                             double* err_out, int64_t B, hipStream_t st, bool build) {
+                             const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
+                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build) {
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
     hipError_t e = hipSuccess;
@@ -1102,7 +1123,11 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
     StepOut so{};
     for (int j = 0; j < 6; ++j) so.k[j] = kout[j];
     so.u_new = u_new;
+    so.qform = q4x7 ? 1 : 0;
     StepCoef sc{};
+    if (q4x7)
+        for (int m = 0; m < 4; ++m)
+            for (int i = 0; i < 7; ++i) sc.q[m][i] = q4x7[7 * m + i];
     for (int s = 0; s < 6; ++s)
         for (int j = 0; j < 6; ++j) sc.a[s][j] = a6x6[6 * s + j];
     for (int j = 0; j < 7; ++j) sc.e[j] = e7 ? e7[j] : 0.0;

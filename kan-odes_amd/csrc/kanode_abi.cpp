@@ -973,20 +973,22 @@ bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
         if (h->kind[l] != KIND_COL) return false;
     return true;
 }
+bool kanode_internal_fk_step_ok(const kanode_handle* h) {
+    return h->spec.dtype == KANODE_F64 && h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on &&
+           kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) && !std::getenv("KANODE_NO_FUSED_STEP");
+}
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
-                                      double abstol, double reltol, double* err_out, int64_t batch, void* stream,
-                                      bool& launched) {
+                                      const double* q4x7, double abstol, double reltol, double* err_out,
+                                      int64_t batch, void* stream, bool& launched) {
     launched = false;
-    if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
-        !kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) || std::getenv("KANODE_NO_FUSED_STEP"))
-        return KANODE_OK;
+    if (!kanode_internal_fk_step_ok(h)) return KANODE_OK;
     const double dx2 = h->spec.dx * h->spec.dx;
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     HIP_TRY(h, kan::launch_fk_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                       (int)h->spec.nx, (const double*)u, (const double*)k1, (double* const*)kout,
-                                      (double*)u_new, a6x6, e7, abstol, reltol, (double*)h->slab, kSlabBlocks, err_out,
-                                      batch, (hipStream_t)stream, table_build(h, h->built_phi)));
+                                      (double*)u_new, a6x6, e7, q4x7, abstol, reltol, (double*)h->slab, kSlabBlocks,
+                                      err_out, batch, (hipStream_t)stream, table_build(h, h->built_phi)));
     launched = true;
     return KANODE_OK;
 }

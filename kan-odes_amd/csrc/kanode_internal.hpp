@@ -45,10 +45,12 @@ kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched);
 // a whole Tsit5 step per row on the Fisher-KPP table path (fk_step_pp_wave_kernel); launched =
 // false when the handle is not that path (the caller runs the six stages)
+// (q4x7: write the dense output as the interpolation polynomials Q_1..Q_4 and k_7)
+bool kanode_internal_fk_step_ok(const kanode_handle* h);
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
-                                      double abstol, double reltol, double* err_out, int64_t batch, void* stream,
-                                      bool& launched);
+                                      const double* q4x7, double abstol, double reltol, double* err_out,
+                                      int64_t batch, void* stream, bool& launched);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

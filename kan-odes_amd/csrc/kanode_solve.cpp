@@ -97,6 +97,7 @@ struct kanode_solution {
     std::vector<double> ts, dts;     // accepted steps: start time, step
     std::vector<void*> slots;
     bool slots_borrowed = false;     // slots point into fused.block (one-workgroup solve), not owned
+    bool qform = false;              // slots hold u_n, Q_1..Q_4, k_7 (fk_step_pp_wave_kernel) instead of u_n, k_2..k_7
     void* k1_0 = nullptr;
     bool record = true;
     // one-workgroup small-chain solve (kd_chain_tsit5_kernel): contiguous dense output and the
@@ -164,8 +165,11 @@ struct kanode_solution {
     // stage vector k_j (j = 1..7) of step i
     void* k(int64_t i, int j) const {
         if (j == 1) return i == 0 ? k1_0 : k(i - 1, 7);
+        if (qform && j == 7) return slot(i) + 5 * state_bytes();
         return slot(i) + (size_t)(j - 1) * state_bytes();
     }
+    // interpolation polynomial Q_m (m = 1..4) of step i (qform): u(t_i + θ dt_i) = u_i + Σ_m θ^m Q_m
+    void* q(int64_t i, int m) const { return slot(i) + (size_t)m * state_bytes(); }
 };
 
 extern "C" void kanode_solution_free(kanode_solution* s) { delete s; }
@@ -311,11 +315,13 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
     } else {
         SOLVE_TRY(ensure_slots(h, s, 2, st));
     }
+    // Fisher-KPP table path: one launch per step and the dense output in Q form
+    s->qform = kanode_internal_fk_step_ok(h);
     SOLVE_HIP(h, hipMemcpyAsync(s->u(0), u0, sb, hipMemcpyDeviceToDevice, st));
     kanode_stage s0{};
     SOLVE_TRY(kanode_rhs_stage(h, p, s->u(0), &s0, s->k1_0, s->batch, st));   // k1 = f(u0)
     double dt = o.dt;
-    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st, s->k(0, 2)));
+    if (o.adaptive && !(o.dt > 0)) SOLVE_TRY(initdt<T>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st, s->q(0, 1)));
     double qold = o.qoldinit;
     double t = t0;
     int64_t step = 0, naccept = 0, nreject = 0, nf = 0;
@@ -327,14 +333,18 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         void* ks[7];
         for (int j = 0; j < 7; ++j) ks[j] = s->k(step, j + 1);
         bool fused_step = false;   // Fisher-KPP table path: the six stages in one launch
-        {
-            double a66[36] = {}, e7[7];
+        if (s->qform) {
+            double a66[36] = {}, e7[7], q47[28];
             for (int i = 0; i < 6; ++i)
                 for (int j = 0; j <= i; ++j) a66[6 * i + j] = dt * TA[i][j];
             for (int j = 0; j < 7; ++j) e7[j] = dt * BT[j];
-            SOLVE_TRY(kanode_internal_fk_step(h, p, s->u(step), ks[0], ks + 1, s->u(step + 1), a66,
-                                              o.adaptive ? e7 : nullptr, o.abstol, o.reltol,
+            for (int m = 0; m < 4; ++m)
+                for (int i = 0; i < 7; ++i) q47[7 * m + i] = dt * RI[i][m];
+            void* kout[6] = {s->q(step, 1), s->q(step, 2), s->q(step, 3), s->q(step, 4), nullptr, s->k(step, 7)};
+            SOLVE_TRY(kanode_internal_fk_step(h, p, s->u(step), ks[0], kout, s->u(step + 1), a66,
+                                              o.adaptive ? e7 : nullptr, q47, o.abstol, o.reltol,
                                               o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
+            if (!fused_step) return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5: fused step not launched");
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double c[6];
@@ -375,6 +385,11 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             void* dst = (char*)u_save + si * sb;
             if (std::fabs(tsv - tn) <= 1e-12 * std::max(1.0, std::fabs(tn))) {
                 SOLVE_HIP(h, hipMemcpyAsync(dst, s->u(step + 1), sb, hipMemcpyDeviceToDevice, st));
+            } else if (s->qform) {
+                const double th = (tsv - t) / dt;
+                const double w[4] = {th, th * th, th * th * th, th * th * th * th};
+                const void* qs[4] = {s->q(step, 1), s->q(step, 2), s->q(step, 3), s->q(step, 4)};
+                SOLVE_TRY(lincomb<T>(h, s->u(step), 4, qs, w, dst, s->n, st));
             } else {
                 double w[7];
                 interp_weights((tsv - t) / dt, w);
@@ -819,12 +834,19 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         i = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, i));
         const double dti = s->dts[i];
         const double theta = std::min(1.0, std::max(0.0, (t - s->ts[i]) / dti));
-        double c[7];
-        interp_weights(theta, c);
-        for (double& x : c) x *= dti;
-        void* ks[7];
-        for (int j = 0; j < 7; ++j) ks[j] = s->k(i, j + 1);
-        kanode_stage su = make_stage(7, ks, c);
+        kanode_stage su;
+        if (s->qform) {   // u_i + Σ_m θ^m Q_m
+            const double c[4] = {theta, theta * theta, theta * theta * theta, theta * theta * theta * theta};
+            void* qs[4] = {s->q(i, 1), s->q(i, 2), s->q(i, 3), s->q(i, 4)};
+            su = make_stage(4, qs, c);
+        } else {
+            double c[7];
+            interp_weights(theta, c);
+            for (double& x : c) x *= dti;
+            void* ks[7];
+            for (int j = 0; j < 7; ++j) ks[j] = s->k(i, j + 1);
+            su = make_stage(7, ks, c);
+        }
         kanode_stage sl = make_stage(nl, lks, lc);
         sl.y_out = lam_out;
         if (ec) {
@@ -1122,6 +1144,7 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
     s->saveat.assign(saveat, saveat + n_save);
     s->ts.clear();
     s->dts.clear();
+    s->qform = false;   // K-form dense output unless the host loop takes the Fisher-KPP step path
     kanode_status r;
     {
         TableHold hold(h);
