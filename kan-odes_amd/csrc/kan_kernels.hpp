@@ -91,6 +91,26 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 // The reductions of several adjoint stages launched with deferred_grid (their slabs in
 // separate regions) in one launch: job j sums slab_j rows into dp_j (= or +=) and err_slab_j
 // into err_out_j, each in the fixed order of vjp_finish_kernel.
+// One InterpolatingAdjoint step (six stages) of the Fisher-KPP table path in one launch
+// (fk_vjp_step_pp_wave_kernel); the dense output must be in Q form.  slab_base receives the six
+// stages' [grid][P] moment rows and then the [grid] error partials; grid_out the grid.
+struct AdjStepArgs {
+    double* kl[7];             // kλ_1 (FSAL, read) .. kλ_7 (written by stage s into kl[s + 1])
+    double a[6][6];            // h·a_sj
+    const double* su_u[6];     // u_i of the forward step holding stage s
+    const double* su_q[6][4];  // its Q_1..Q_4
+    double su_c[6][4];         // θ_s^m
+    double ec[7];              // h·btilde (stage 6 error)
+    double abstol, reltol;
+    const double* lam;
+    double* lam_out;
+    double* slab[6];           // per stage: [grid][P] moment rows
+    double* err_slab;          // [grid] (null: no error)
+};
+hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                 const double* p, double* tables, double cd, double co, int Nx,
+                                 const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
+                                 hipStream_t st, bool build);
 constexpr int kMaxFinishJobs = 8;
 struct FinishJob {
     const double* slab;

@@ -750,6 +750,182 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     }
 }
 
+// The six stages of one InterpolatingAdjoint step in ONE launch (Fisher-KPP table path, dense
+// output in Q form): the stage loop runs inside the kernel and every wave keeps its rows across
+// the stages (row b -> the same wave in every stage), so stage s+1 reads the kλ_{s+1} values its
+// own wave wrote in stage s and no grid barrier is needed.  Per stage the same arithmetic as
+// fk_vjp_pp_wave_kernel<…, STG>: u(t_s) = u_i + Σ_m θ^m Q_m, λs = λ + Σ_{j<=s} h a_sj kλ_j, the
+// pullback, the moments block-summed into that stage's slab rows; stage 6 also writes λs (the
+// new λ) and the λ error partials.  The tables are staged and the kernel launched once per step
+// instead of once per stage.
+template <int NORM, int PATH, int GT, int NP>
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VJP_STG_WPE)))
+fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                           const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
+                           int64_t B, AdjStepArgs a) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
+    const int tsz = (kPPCoef / 2) * ni;
+    for (int i = threadIdx.x; i < tsz; i += kBlock) {
+        tl[i] = tables[PP_DPHI * tsz + i];
+        tl[tsz + i] = tables[PP_SWISH * tsz + i];
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<double> M{tab};
+    const double2* __restrict__ td = tl;
+    const double2* __restrict__ ts = tl + tsz;
+    const LayerConst& lc = *lcp;
+    const RecScalars<double> rc(lc);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t rstride = (int64_t)gridDim.x * (kVjpBlock / kWave);
+    const int P = GT + (lc.use_base ? 1 : 0);
+    double eacc = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < 6; ++s) {
+        double S0[GT];
+        float S1[GT], S2[GT];
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            S0[j] = 0.0;
+            S1[j] = S2[j] = 0.0f;
+        }
+        double dW = 0.0;
+        const bool last = s == 5;
+        const bool want_err = last && a.err_slab != nullptr;
+        const double* __restrict__ uu = a.su_u[s];
+        for (int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+            const int64_t rb = b * Nx + 2 * lane;
+            kd2 uv[NP], lv[NP], l0[NP], ev[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                uv[k] = ld_stream(uu + rb + 128 * k);
+                lv[k] = ld_stream(a.lam + rb + 128 * k);
+                l0[k] = lv[k];
+            }
+            {   // u(t_s) = u_i + Σ_m θ^m Q_m (stage_sum order: Σ first, then added)
+                kd2 q[4][NP];
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int k = 0; k < NP; ++k) q[m][k] = ld_stream(a.su_q[s][m] + rb + 128 * k);
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    kd2 t{0.0, 0.0};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        t.x = ::fma(a.su_c[s][m], q[m][k].x, t.x);
+                        t.y = ::fma(a.su_c[s][m], q[m][k].y, t.y);
+                    }
+                    uv[k].x = ::fma(1.0, t.x, uv[k].x);
+                    uv[k].y = ::fma(1.0, t.y, uv[k].y);
+                }
+            }
+            {   // λs = λ + Σ_{j<=s} h a_sj kλ_j (and the error sum at the last stage)
+                kd2 t[NP], e[NP];
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    t[k] = kd2{0.0, 0.0};
+                    e[k] = kd2{0.0, 0.0};
+                }
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    if (j <= s) {
+                        const double c = a.a[s][j], ce = a.ec[j];
+#pragma unroll
+                        for (int k = 0; k < NP; ++k) {
+                            const kd2 kj = ld_stream(a.kl[j] + rb + 128 * k);
+                            t[k].x = ::fma(c, kj.x, t[k].x);
+                            t[k].y = ::fma(c, kj.y, t[k].y);
+                            if (want_err) {
+                                e[k].x = ::fma(ce, kj.x, e[k].x);
+                                e[k].y = ::fma(ce, kj.y, e[k].y);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    lv[k].x = ::fma(1.0, t[k].x, lv[k].x);
+                    lv[k].y = ::fma(1.0, t[k].y, lv[k].y);
+                    ev[k] = e[k];
+                }
+            }
+            if (last && a.lam_out) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) st_stream(a.lam_out + rb + 128 * k, lv[k]);
+            }
+            double rr[NP], rl[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                rr[k] = wave_ror1(lv[k].y);
+                rl[k] = wave_rol1(lv[k].x);
+            }
+            double la[NP][2];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+                const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, la[k][0], la[k][1]);
+            }
+            double* __restrict__ out = a.kl[s + 1];
+#pragma unroll 1
+            for (int k = 0; k < NP; ++k) {
+                kd2 uk = uv[0], lk = lv[0], l0k = l0[0], ek = ev[0];
+                double a0 = la[0][0], a1 = la[0][1];
+#pragma unroll
+                for (int q = 1; q < NP; ++q) {
+                    if (k == q) {
+                        uk = uv[q];
+                        lk = lv[q];
+                        a0 = la[q][0];
+                        a1 = la[q][1];
+                        l0k = l0[q];
+                        ek = ev[q];
+                    }
+                }
+                const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0,
+                                                               S1, S2, dW);
+                __builtin_amdgcn_sched_barrier(0);
+                const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.y, lk.y, S0,
+                                                               S1, S2, dW);
+                kd2 o;
+                o.x = a0 + x0b;
+                o.y = a1 + x1b;
+                st_stream(out + rb + 128 * k, o);
+                if (want_err) {
+                    const double en = a.ec[6];
+                    const double ex = ::fma(en, o.x, ek.x), ey = ::fma(en, o.y, ek.y);
+                    const double sx = ::fma(a.reltol, fmax(kabs(l0k.x), kabs(lk.x)), a.abstol);
+                    const double sy = ::fma(a.reltol, fmax(kabs(l0k.y), kabs(lk.y)), a.abstol);
+                    const double rx = ex / sx, ry = ey / sy;
+                    eacc = ::fma(rx, rx, eacc);
+                    eacc = ::fma(ry, ry, eacc);
+                }
+            }
+        }
+        double acc[GT + 1];
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            const double e = lc.e[j];
+            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+                                           : lc.K[j] * S0[j];
+        }
+        acc[GT] = dW;
+        block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+        // kλ_{s+1} written by this wave is read back by it in the next stage: a workgroup-scope
+        // release/acquire (wait for the stores, invalidate the CU's L1) suffices, the rows never
+        // change wave; an agent-scope __threadfence would write back the whole L2 every stage
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();   // (red is reused)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (a.err_slab) {
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, a.err_slab + blockIdx.x);
+    }
+}
+
 // dp[q] (= or +=) Σ_b slab[b·P + q] for q < P (block q), and err_out[0] = Σ_b err_slab[b]
 // (block P): the adjoint stage's reductions in one launch, fixed order.
 __global__ void __launch_bounds__(kBlock)
@@ -940,6 +1116,7 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
     }
 }
+
 
 // Runge-Kutta stage, fused (kanode_rhs_stage): the stage input y = u + Σ_j c_j k_j is
 // formed in registers from nontemporal loads of u and the k_j, the stencil
@@ -1258,6 +1435,51 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
     hipLaunchKernelGGL(vjp_finish_kernel, dim3((unsigned)(dp ? P : 0) + (err_out ? 1 : 0)), dim3(kBlock), 0, st,
                        slab, (int64_t)grid, (int64_t)P, dp, dp_assign ? 1 : 0,
                        slab + (int64_t)grid * (hlc.G + 1), err_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                 const double* p, double* tables, double cd, double co, int Nx,
+                                 const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
+                                 int* grid_out, hipStream_t st, bool build) {
+    if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
+    const int fns[2] = {PP_DPHI, PP_SWISH};
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st)) != hipSuccess) return e;
+    const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+    const int P = hlc.G + (hlc.use_base ? 1 : 0);
+    AdjStepArgs a = a_in;
+    int grid = 0;
+#define KAN_VSTEP(NORM, PATH, GT, NP)                                                                              \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>, lds, kVjpBlock);             \
+        grid = grid_for(B, kVjpBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                                \
+        if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                           \
+        hipLaunchKernelGGL((fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>), dim3(grid), dim3(kVjpBlock), lds, st,  \
+                           lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, B, a);              \
+    } while (0)
+#define KAN_VSTEP_NP(NORM, PATH, GT)                                                                              \
+    do {                                                                                                         \
+        if (Nx == 256) KAN_VSTEP(NORM, PATH, GT, 2);                                                             \
+        else if (Nx == 128) KAN_VSTEP(NORM, PATH, GT, 1);                                                        \
+        else KAN_VSTEP(NORM, PATH, GT, 4);                                                                       \
+    } while (0)
+    if (hlc.path == PATH_REC_CORR) {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_VSTEP_NP(NORM_SOFTSIGN, PATH_REC_CORR, 10);
+        else if (hlc.G == 10) KAN_VSTEP_NP(NORM_TANH_FAST, PATH_REC_CORR, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_VSTEP_NP(NORM_SOFTSIGN, PATH_REC_CORR, 5);
+        else KAN_VSTEP_NP(NORM_TANH_FAST, PATH_REC_CORR, 5);
+    } else {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_VSTEP_NP(NORM_SOFTSIGN, PATH_REC, 10);
+        else if (hlc.G == 10) KAN_VSTEP_NP(NORM_TANH_FAST, PATH_REC, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_VSTEP_NP(NORM_SOFTSIGN, PATH_REC, 5);
+        else KAN_VSTEP_NP(NORM_TANH_FAST, PATH_REC, 5);
+    }
+#undef KAN_VSTEP_NP
+#undef KAN_VSTEP
+    *grid_out = grid;
     return hipGetLastError();
 }
 

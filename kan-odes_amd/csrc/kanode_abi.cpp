@@ -63,6 +63,7 @@ struct kanode_handle {
     bool built_phi = false, built_vjp = false;
     // adjoint stages whose dp / error reductions wait for kanode_internal_vjp_flush (one launch)
     void* defer_slab = nullptr;
+    void* step_slab = nullptr;        // fused adjoint step: six stages' moment rows + error partials
     kan::FinishJobs jobs{};
     int njobs = 0;
     // stage input y for kanode_rhs_stage's unfused path
@@ -728,6 +729,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->stage_ws) (void)hipFree(h->stage_ws);
     if (h->dtable) (void)hipFree(h->dtable);
     if (h->defer_slab) (void)hipFree(h->defer_slab);
+    if (h->step_slab) (void)hipFree(h->step_slab);
     if (h->solve_cache) kanode_solution_free(h->solve_cache);
     delete h;
 }
@@ -989,6 +991,46 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
                                       (int)h->spec.nx, (const double*)u, (const double*)k1, (double* const*)kout,
                                       (double*)u_new, a6x6, e7, q4x7, abstol, reltol, (double*)h->slab, kSlabBlocks,
                                       err_out, batch, (hipStream_t)stream, table_build(h, h->built_phi)));
+    launched = true;
+    return KANODE_OK;
+}
+kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
+                                              double* err_out, int64_t batch, void* stream, bool& launched) {
+    launched = false;
+    if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
+        !kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx) || std::getenv("KANODE_NO_FUSED_STEP"))
+        return KANODE_OK;
+    const hipStream_t st = (hipStream_t)stream;
+    const int P = h->hlc[0].G + (h->hlc[0].use_base ? 1 : 0);
+    const size_t need = (size_t)(kSlabBlocks / 2) * (6 * P + 1);
+    if (!h->step_slab) {
+        if (hipMalloc(&h->step_slab, need * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            h->step_slab = nullptr;
+            return fail(h, KANODE_ERR_ALLOC, "adjoint step reduction slab");
+        }
+    }
+    const double dx2 = h->spec.dx * h->spec.dx;
+    const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+    a->err_slab = err_out ? (double*)h->step_slab : nullptr;   // relocated by the launcher
+    int grid = 0;
+    HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
+                                          (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
+                                          table_build(h, h->built_vjp)));
+    kan::FinishJobs jobs{};
+    double* base = (double*)h->step_slab;
+    for (int s = 0; s < 6; ++s) {
+        kan::FinishJob& jb = jobs.j[s];
+        jb.slab = base + (int64_t)s * grid * P;
+        jb.dp = (double*)km[s];
+        jb.nblk = grid;
+        jb.assign = 1;
+        if (s == 5 && err_out) {
+            jb.err_slab = base + (int64_t)6 * grid * P;
+            jb.err_out = err_out;
+        }
+    }
+    HIP_TRY(h, kan::launch_vjp_finish_jobs(jobs, 6, P, st));
     launched = true;
     return KANODE_OK;
 }

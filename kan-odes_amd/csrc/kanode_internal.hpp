@@ -13,6 +13,7 @@
 namespace kan {
 struct ChainSolveArgs;
 struct ChainAdjointArgs;
+struct AdjStepArgs;
 }
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -51,6 +52,10 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
                                       int64_t batch, void* stream, bool& launched);
+// one InterpolatingAdjoint step on the Fisher-KPP table path (fk_vjp_step_pp_wave_kernel) plus
+// its reductions: kμ of the six stages -> km[0..5] (assigned), the λ error -> err_out
+kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
+                                              double* err_out, int64_t batch, void* stream, bool& launched);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

@@ -899,7 +899,33 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         if (tau >= TT - 1e-14 * std::max(1.0, TT)) break;
         hstep = std::min(hstep, stops[si] - tau);
         const int nxt = cur ^ 1;
-        for (int i = 0; i < 6; ++i) {
+        bool fused_step = false;   // Fisher-KPP table path, Q-form dense output: the six stages in one launch
+        if (s->qform) {
+            kan::AdjStepArgs a{};
+            for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j <= i; ++j) a.a[i][j] = hstep * TA[i][j];
+                const double t = tf - (i == 5 ? tau + hstep : tau + TC[i] * hstep);
+                int64_t fi = (int64_t)(std::upper_bound(s->ts.begin(), s->ts.end(), t) - s->ts.begin()) - 1;
+                fi = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, fi));
+                const double th = std::min(1.0, std::max(0.0, (t - s->ts[fi]) / s->dts[fi]));
+                a.su_u[i] = (const double*)s->u(fi);
+                for (int m = 0; m < 4; ++m) a.su_q[i][m] = (const double*)s->q(fi, m + 1);
+                a.su_c[i][0] = th;
+                a.su_c[i][1] = th * th;
+                a.su_c[i][2] = th * th * th;
+                a.su_c[i][3] = th * th * th * th;
+            }
+            for (int j = 0; j < 7; ++j) a.ec[j] = hstep * BT[j];
+            a.abstol = o.abstol;
+            a.reltol = o.reltol;
+            a.lam = (const double*)lam[cur];
+            a.lam_out = (double*)lam[nxt];
+            void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
+            SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? s->dscal + 0 : nullptr, s->batch,
+                                                      st, fused_step));
+        }
+        for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];
             for (int j = 0; j <= i; ++j) lc[j] = hstep * TA[i][j];
             if (i == 5) {
@@ -912,7 +938,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                                   nullptr, nullptr, true));
             }
         }
-        SOLVE_TRY(kanode_internal_vjp_flush(h, st));   // km[1..6] and the λ error
+        if (!fused_step) SOLVE_TRY(kanode_internal_vjp_flush(h, st));   // km[1..6] and the λ error
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
