@@ -389,3 +389,32 @@ def test_fused_chain_solve_falls_back_when_dense_output_fills(monkeypatch):
     assert sol.stats["naccept"] == ref.stats["naccept"] > 3
     assert (sol.u - ref.u).abs().max().item() <= 1e-12 * max(1.0, ref.u.abs().max().item())
     assert (g - gr).abs().max().item() <= 1e-12 * gr.abs().max().item()
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_fused_fk_step_matches_stage_launches(monkeypatch, adaptive):
+    """The one-launch Tsit5 step (fk_step_pp_wave_kernel, Q-form dense output) and adjoint step
+    (fk_vjp_step_pp_wave_kernel) against the per-stage launches with the K-form dense output
+    (KANODE_NO_FUSED_STEP): same steps, saveat values and gradients."""
+    rhs, u0, p0, tspan, ts = _setup("fk256")
+    if not adaptive:
+        tspan, dt = FIXED["fk256"]
+        ts = [x for x in ts if x <= tspan[1]] + [tspan[1]]
+    opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else 5e-4, abstol=1e-8, reltol=1e-7)
+    w = t(np.random.default_rng(12).normal(size=(len(ts),) + tuple(u0.shape)))
+    out = {}
+    for fused in (True, False):
+        if fused:
+            monkeypatch.delenv("KANODE_NO_FUSED_STEP", raising=False)
+        else:
+            monkeypatch.setenv("KANODE_NO_FUSED_STEP", "1")
+        p = p0.clone().requires_grad_(True)
+        sol = kanode.solve(rhs, u0, tspan, p, ts, opt, sensealg="interpolating_adjoint")
+        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+        out[fused] = (sol, g)
+    (sf, gf), (ss, gs) = out[True], out[False]
+    assert sf.stats["naccept"] == ss.stats["naccept"] and sf.stats["nreject"] == ss.stats["nreject"]
+    assert abs(sf.stats["adjoint"]["naccept"] - ss.stats["adjoint"]["naccept"]) <= 1
+    scale = max(1.0, ss.u.abs().max().item())
+    assert (sf.u - ss.u).abs().max().item() <= 1e-12 * scale
+    assert (gf - gs).abs().max().item() <= 1e-9 * gs.abs().max().item()
