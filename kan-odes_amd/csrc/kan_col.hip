@@ -163,9 +163,7 @@ constexpr int kChainBlock = 256;
 constexpr int kChainDim = 16;    // lanes per column = max layer width
 template <typename T, int NORM, int PATH, class S>
 __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a) {
-    const int nlc = sh_nl<S>(nl);
-#pragma unroll
-    for (int l = 0; l < nlc; ++l) {
+    auto layer = [&](int l) {
         const LayerConst& lc = lcl[l];
         const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
         const T* __restrict__ C = ps + lc.p_off;
@@ -202,6 +200,12 @@ __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* l
             }
         }
         a = out;
+    };
+    if constexpr (S::NL > 0) {   // fixed shape: unrolled, every layer's loops folded
+#pragma unroll
+        for (int l = 0; l < S::NL; ++l) layer(l);
+    } else {
+        for (int l = 0; l < nl; ++l) layer(l);
     }
     return a;
 }
@@ -921,6 +925,10 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
 // adds into its own LDS gradient row) and reduces the rows into the stage's kμ (LDS), in the
 // order kd_chain_vjp_stage_kernel + chain_vjp_finish_kernel use (4 groups per block, then the
 // blocks).  μ and its seven stage vectors live in LDS; the error norm covers λ and μ.
+// (the generic-shape instantiations are too large for the stage loop to be unrolled; their
+// stage values then live in scratch, which only the non-LV small chains pay for)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
 template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t B,
@@ -1172,6 +1180,7 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
         a.out[3] = status;
     }
 }
+#pragma clang diagnostic pop
 
 // The one-workgroup adjoint (kd_chain_adjoint_kernel): the small-chain conditions of
 // launch_kd_chain_tsit5 plus nsteps <= kChainAdjointMaxSteps and the LDS budget.
