@@ -201,12 +201,19 @@ kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const v
  *     step size, saveat, dense-output record, u <- u_new commit) and the solve is a
  *     hipGraph of graph_steps step slots (stage launches read the step size from device
  *     memory) replayed until done: one host read per replay instead of per step.  The
- *     graph is cached in the kanode_solution.  auto = device for states up to 64 MB.
+ *     graph is cached in the kanode_solution.  Opt-in (it rarely pays on ROCm 7.2).
+ *   control = auto: a chain of small layers (<= 16 wide) with <= 16 trajectories runs
+ *     the whole solve in ONE workgroup (controller, saveat and dense output on the
+ *     device), and with its dense output kept the whole adjoint too; everything else
+ *     runs as control = host.  On the Fisher-KPP table path (fp64, Nx = 128/256/512)
+ *     the host loop issues one launch per Tsit5 step (all six stages per trajectory
+ *     row) and keeps the dense output as u_n and the interpolation polynomials Q_1..Q_4
+ *     (plus k_7), and the adjoint issues one launch per step.
  * kanode_adjoint_tsit5 is SciMLSensitivity 7.69's InterpolatingAdjoint (the NeuralODE
  * default; the reference's gradients): the adjoint ODE [λ; μ] integrated backward
  * with Tsit5 at the same tolerances, u(t) from the forward dense output, λ += ∂L/∂u
- * at every saveat time (tstops, FSAL re-evaluated after each jump); every adjoint
- * stage is one kanode_vjp_stage. */
+ * at every saveat time (tstops, FSAL re-evaluated after each jump); an adjoint stage
+ * is one kanode_vjp_stage (or the fused step / one-workgroup kernels above). */
 typedef struct {
     double abstol, reltol;          /* 1e-6, 1e-3 */
     double dt;                      /* adaptive = 0: the fixed step; adaptive = 1: initial step, 0 = Hairer-Wanner */
@@ -215,8 +222,9 @@ typedef struct {
     double dtmin;                   /* 0 */
     double beta1, beta2, gamma;     /* 7/50, 2/25, 9/10 */
     double qmin, qmax, qoldinit;    /* 1/5, 10, 1e-4 */
-    int32_t control;                /* step control: 0 = auto, 1 = host (one 8-byte norm read per step),
-                                       2 = device (hipGraph of graph_steps step slots, replayed until done) */
+    int32_t control;                /* step control: 0 = auto (one-workgroup solve for small chains, else
+                                       host), 1 = host (one 8-byte norm read per step), 2 = device (hipGraph
+                                       of graph_steps step slots, replayed until done) */
     int32_t graph_steps;            /* step slots per graph replay (device control; even, 0 = 16) */
 } kanode_solver_options;
 void kanode_solver_options_default(kanode_solver_options* opt);
