@@ -925,6 +925,68 @@ hipError_t launch_kd_chain_col(const LayerConst* hlcs, int nl, const LayerConst*
 // adds into its own LDS gradient row) and reduces the rows into the stage's kμ (LDS), in the
 // order kd_chain_vjp_stage_kernel + chain_vjp_finish_kernel use (4 groups per block, then the
 // blocks).  μ and its seven stage vectors live in LDS; the error norm covers λ and μ.
+// A whole Tsit5 step of a small chain per trajectory column, in one launch (kanode_solve_tsit5's
+// host loop for batches the one-workgroup solve does not take): column group g keeps u, k_1..k_7
+// of its column in registers through the six stages (chain_forward each), writes k_2..k_7 and
+// u_new once, and adds its embedded-error partial to the block's slab row.  Same arithmetic as
+// six kd_chain_col_kernel stage launches.
+template <typename T, int NORM, int PATH, class S>
+__global__ void __launch_bounds__(kChainBlock)
+kd_chain_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t K,
+                     ChainStepArgs a, double* __restrict__ err_slab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cst_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cst_raw);
+    T* ps = reinterpret_cast<T*>(cst_raw + nl * sizeof(LayerConst));
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cst_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const int N = lcl[0].I;
+    const int j = threadIdx.x & (kChainDim - 1);
+    const T* __restrict__ u = reinterpret_cast<const T*>(a.u);
+    const T* __restrict__ k1 = reinterpret_cast<const T*>(a.k1);
+    double eacc = 0.0;
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kChainDim;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kChainDim; k < K; k += stride) {
+        const bool act = j < N;
+        const int64_t idx = (int64_t)N * k + j;
+        const T uv = act ? u[idx] : T(0);
+        T kk[7];
+        kk[0] = act ? k1[idx] : T(0);
+        T y = uv;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            y = uv;
+#pragma unroll
+            for (int m = 0; m <= s; ++m) y = kfma<T>((T)a.a[s][m], kk[m], y);
+            kk[s + 1] = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, y);
+            if (act) reinterpret_cast<T*>(a.k[s])[idx] = kk[s + 1];
+        }
+        if (act) {
+            reinterpret_cast<T*>(a.u_new)[idx] = y;
+            if (err_slab) {
+                double ev = 0.0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) ev = ::fma(a.e[m], (double)kk[m], ev);
+                const double e = ::fma(a.e[6], (double)kk[6], ev);
+                const double sk = ::fma(a.reltol, fmax(kabs((double)uv), kabs((double)y)), a.abstol);
+                const double r = e / sk;
+                eacc = ::fma(r, r, eacc);
+            }
+        }
+    }
+    if (err_slab) {
+        __shared__ double red[kChainBlock / kWave];
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+    }
+}
+
 // (the generic-shape instantiations are too large for the stage loop to be unrolled; their
 // stage values then live in scratch, which only the non-LV small chains pay for)
 #pragma clang diagnostic push
@@ -1243,6 +1305,39 @@ hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerCons
     return hipGetLastError();
 }
 
+// One Tsit5 step of a small chain per column (kd_chain_step_kernel); err_out (with err_slab of
+// slab_rows rows) receives Σ (e/sk)².  hipErrorNotSupported outside the small-chain shapes.
+template <typename T>
+hipError_t launch_kd_chain_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                int64_t K, const ChainStepArgs& a, double* err_slab, int slab_rows, double* err_out,
+                                hipStream_t st) {
+    if (nl < 1 || nl > 8 || K > 32768 || I_ne_O(hlcs, nl)) return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T);
+    if (lds > 48 * 1024) return hipErrorNotSupported;
+    const int g = grid_for(K * kChainDim, kChainBlock, slab_rows < kGridCap ? slab_rows : kGridCap);
+    double* es = err_out ? err_slab : nullptr;
+    const LayerConst& h = hlcs[0];
+#define KAN_CSTEP(NORM, PATH, S)                                                                                 \
+    hipLaunchKernelGGL((kd_chain_step_kernel<T, NORM, PATH, S>), dim3(g), dim3(kChainBlock), lds, st, lcs, nl, p,  \
+                       (int)P, K, a, es)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CSTEP(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CSTEP(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CSTEP(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CSTEP(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CSTEP(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
+#undef KAN_CSTEP
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !es) return e;
+    return launch_stage_error_final(err_slab, g, err_out, st);
+}
+
 // The fused adjoint stage of a small chain (kd_chain_vjp_stage_kernel) when every layer is
 // small (I, O <= 16), the layers share the normalizer/path specialisation, nl <= 4 and the
 // parameter vector plus the gradient rows fit in LDS; hipErrorNotSupported otherwise.
@@ -1298,6 +1393,8 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
                                                const T*, T*, int64_t, hipStream_t, const StageArgs<T>*, T*,       \
                                                double*, int, double*);                                            \
     template hipError_t launch_slab_reduce<T>(const T*, int64_t, int64_t, T*, hipStream_t);                       \
+    template hipError_t launch_kd_chain_step<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,    \
+                                                int64_t, const ChainStepArgs&, double*, int, double*, hipStream_t); \
     template hipError_t launch_kd_chain_tsit5<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,   \
                                                  const T*, int64_t, const ChainSolveArgs&, hipStream_t);         \
     template hipError_t launch_kd_chain_adjoint<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t, \

@@ -238,6 +238,20 @@ constexpr int kChainAdjointMaxSteps = 1024;   // forward steps held in LDS
 template <typename T>
 hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
                                    int64_t B, const ChainAdjointArgs& a, hipStream_t st);
+// One Tsit5 step of a small chain per trajectory column (kd_chain_step_kernel, kan_col.hip)
+struct ChainStepArgs {
+    double a[6][6];   // dt·a_sj
+    double e[7];      // dt·btilde_j
+    double abstol, reltol;
+    const void* u;
+    const void* k1;
+    void* k[6];       // k_2..k_7
+    void* u_new;
+};
+template <typename T>
+hipError_t launch_kd_chain_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                int64_t K, const ChainStepArgs& a, double* err_slab, int slab_rows, double* err_out,
+                                hipStream_t st);
 constexpr int kChainSolveMaxBatch = 16;   // columns of one workgroup (256 lanes / 16)
 template <typename T>
 hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,

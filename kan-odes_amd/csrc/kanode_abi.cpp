@@ -994,6 +994,36 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
     launched = true;
     return KANODE_OK;
 }
+kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
+                                         void* const* kout, void* u_new, const double* a6x6, const double* e7,
+                                         double abstol, double reltol, double* err_out, int64_t batch, void* stream,
+                                         bool& launched) {
+    launched = false;
+    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || std::getenv("KANODE_NO_FUSED_STEP")) return KANODE_OK;
+    for (int l = 0; l < h->n_layers; ++l)
+        if (h->kind[l] != KIND_COL) return KANODE_OK;
+    kan::ChainStepArgs a{};
+    for (int s = 0; s < 6; ++s)
+        for (int j = 0; j < 6; ++j) a.a[s][j] = a6x6[6 * s + j];
+    for (int j = 0; j < 7; ++j) a.e[j] = e7 ? e7[j] : 0.0;
+    a.abstol = abstol;
+    a.reltol = reltol;
+    a.u = u;
+    a.k1 = k1;
+    for (int j = 0; j < 6; ++j) a.k[j] = kout[j];
+    a.u_new = u_new;
+    const hipStream_t st = (hipStream_t)stream;
+    const hipError_t e =
+        h->spec.dtype == KANODE_F64
+            ? kan::launch_kd_chain_step<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P, batch, a,
+                                                (double*)h->slab, kSlabBlocks, err_out, st)
+            : kan::launch_kd_chain_step<float>(h->hlc, h->n_layers, h->dlc, (const float*)p, h->P, batch, a,
+                                               (double*)h->slab, kSlabBlocks, err_out, st);
+    if (e == hipErrorNotSupported) return KANODE_OK;
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_step: ") + hipGetErrorString(e));
+    launched = true;
+    return KANODE_OK;
+}
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
                                               double* err_out, int64_t batch, void* stream, bool& launched) {
     launched = false;

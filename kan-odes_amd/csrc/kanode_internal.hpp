@@ -52,6 +52,11 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
                                       int64_t batch, void* stream, bool& launched);
+// a whole Tsit5 step of a small chain per column (kd_chain_step_kernel); K-form dense output
+kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
+                                         void* const* kout, void* u_new, const double* a6x6, const double* e7,
+                                         double abstol, double reltol, double* err_out, int64_t batch, void* stream,
+                                         bool& launched);
 // one InterpolatingAdjoint step on the Fisher-KPP table path (fk_vjp_step_pp_wave_kernel) plus
 // its reductions: kμ of the six stages -> km[0..5] (assigned), the λ error -> err_out
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,

@@ -345,6 +345,14 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
                                               o.adaptive ? e7 : nullptr, q47, o.abstol, o.reltol,
                                               o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
             if (!fused_step) return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5: fused step not launched");
+        } else {   // a small chain: the six stages per column in one launch
+            double a66[36] = {}, e7[7];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j <= i; ++j) a66[6 * i + j] = dt * TA[i][j];
+            for (int j = 0; j < 7; ++j) e7[j] = dt * BT[j];
+            SOLVE_TRY(kanode_internal_chain_step(h, p, s->u(step), ks[0], ks + 1, s->u(step + 1), a66,
+                                                 o.adaptive ? e7 : nullptr, o.abstol, o.reltol,
+                                                 o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double c[6];
