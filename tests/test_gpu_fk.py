@@ -161,3 +161,24 @@ def test_fk_graph_capture():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("nx,dx", [(21, 0.05), (256, 1.0 / 255)])
+def test_allen_cahn_source_rhs(nx, dx):
+    """The Allen-Cahn twin of the source-term KAN-ODE (PDE examples/Allen-Cahn_Source.jl:36-40,
+    90-93; dx = 0.05 there): du = -1e-4·lap·u + KAN(u) is the Fisher-KPP handle with D = -1e-4;
+    RHS and VJP against the oracle."""
+    rng = np.random.default_rng(nx)
+    D = -1e-4
+    p = rng.uniform(-1, 1, 11)
+    u = rng.uniform(-1.2, 1.2, (3, nx))
+    rhs = make_rhs(nx, dx, D=D)
+    du = rhs.rhs(t(u), t(p))
+    assert_close(du, O.fk_rhs(SPEC, p, D, dx, u), fk_scale(p, D, dx, u), RTOL[torch.float64], "du")
+    lam = rng.normal(size=u.shape)
+    lamJ, dp = rhs.vjp(t(u), t(p), t(lam))
+    rJ, rdp = O.fk_vjp(SPEC, p, D, dx, u, lam)
+    scJ = fk_scale(np.abs(p) * 10, D, dx, np.abs(lam)) * (1 + np.abs(u))
+    assert_close(lamJ, rJ, scJ, RTOL[torch.float64], "lamJ")
+    _, dpa = O.fk_vjp(SPEC, p, D, dx, u, np.abs(lam))
+    assert_close(dp, rdp, np.abs(dpa) + 1e-300, 1e-12, "dp")
