@@ -24,6 +24,10 @@
 
 #include <cstdlib>
 
+#ifndef KAN_VJP_PACKED
+#define KAN_VJP_PACKED 1
+#endif
+
 namespace kan {
 
 constexpr int kPPPerBlock = 4;                       // intervals built per block (13·4·4 = 208 lanes)
@@ -564,14 +568,29 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
     double v = l * E0;
     float v32 = (float)v, R32 = (float)R;
     const float t32 = (float)taup, t2 = t32 * t32;
+#if KAN_VJP_PACKED
+    // fp32 correction moments two knots at a time: (v_j, v_j+1) advanced by R² with one packed
+    // multiply (their weight in dC is <= 1.1e-6, so the fp32 rounding of R² does not show)
+    typedef float kf2 __attribute__((ext_vector_type(2)));
+    kf2 vp = {v32, v32 * R32};
+    const float R2 = R32 * R32;
+    const kf2 R2v = {R2, R2};
+#endif
 #pragma unroll
     for (int j = 0; j < GT; ++j) {
         S0[j] = S0[j] + v;
         v = v * R;
         if constexpr (PATH == PATH_REC_CORR) {
+#if KAN_VJP_PACKED
+            const float vj = (j & 1) ? vp.y : vp.x;
+            S1[j] = fmaf(vj, t32, S1[j]);
+            S2[j] = fmaf(vj, t2, S2[j]);
+            if (j & 1) vp = vp * R2v;
+#else
             S1[j] = fmaf(v32, t32, S1[j]);
             S2[j] = fmaf(v32, t2, S2[j]);
             v32 = v32 * R32;
+#endif
         }
     }
     return l * dphi;
