@@ -800,7 +800,10 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
     const int64_t rstride = (int64_t)gridDim.x * (kVjpBlock / kWave);
     const int P = GT + (lc.use_base ? 1 : 0);
     double eacc = 0.0;
-#pragma unroll 1
+#ifndef KAN_VSTEP_UNROLL
+#define KAN_VSTEP_UNROLL 6   // unrolled: static stage offsets and coefficients (132 -> 32 B/lane scratch, epoch -12%)
+#endif
+#pragma unroll KAN_VSTEP_UNROLL
     for (int s = 0; s < 6; ++s) {
         double S0[GT];
         float S1[GT], S2[GT];
