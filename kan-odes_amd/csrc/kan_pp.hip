@@ -333,6 +333,21 @@ __device__ __forceinline__ kd2 ld_stream(const double* p) {
 #endif
 }
 
+// Adjoint step kernel: u_i, λ, Q_m and kλ_j are re-read by later stages of the same launch.
+// They are read and written with the default cache policy, so the re-reads can hit in L2
+// (KAN_VSTEP_KEEP=0: nontemporal, as the streaming kernels; FK256 epoch at 4096 trajectories
+// 7.6 -> 6.6 ms, profiles/r01/epoch/vstep_keep_ab.txt)
+#ifndef KAN_VSTEP_KEEP
+#define KAN_VSTEP_KEEP 1
+#endif
+__device__ __forceinline__ kd2 ld_vstep(const double* p) {
+#if KAN_VSTEP_KEEP
+    return *reinterpret_cast<const kd2*>(p);
+#else
+    return ld_stream(p);
+#endif
+}
+
 // a[k] += Σ_{j<N} (sc·c_j)·K_j[k], e[k] += Σ_{j<N} (sc·ec_j)·K_j[k] (E) over the NP pairs of one
 // row at offset off: all N·NP loads are issued before the first FMA.  (An unrolled loop over
 // j < kMaxStages guarded by j < nk compiles to one branch per array, and the loads, which
@@ -384,6 +399,32 @@ __device__ __forceinline__ void st_stream(double* p, kd2 v) {
     __builtin_nontemporal_store(v, reinterpret_cast<kd2*>(p));
 #else
     *reinterpret_cast<kd2*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void st_vstep(double* p, kd2 v) {   // see ld_vstep
+#if KAN_VSTEP_KEEP
+    *reinterpret_cast<kd2*>(p) = v;
+#else
+    st_stream(p, v);
+#endif
+}
+// Forward step kernel: u_new and k_7 are read by the next step (KAN_FSTEP_KEEP=1: default
+// cache policy for those loads and stores; measured no faster, profiles/r01/epoch/fstep_keep_ab.txt)
+#ifndef KAN_FSTEP_KEEP
+#define KAN_FSTEP_KEEP 0
+#endif
+__device__ __forceinline__ kd2 ld_fstep(const double* p) {
+#if KAN_FSTEP_KEEP
+    return *reinterpret_cast<const kd2*>(p);
+#else
+    return ld_stream(p);
+#endif
+}
+__device__ __forceinline__ void st_fstep(double* p, kd2 v) {
+#if KAN_FSTEP_KEEP
+    *reinterpret_cast<kd2*>(p) = v;
+#else
+    st_stream(p, v);
 #endif
 }
 
@@ -821,8 +862,8 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
             kd2 uv[NP], lv[NP], l0[NP], ev[NP];
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
-                uv[k] = ld_stream(uu + rb + 128 * k);
-                lv[k] = ld_stream(a.lam + rb + 128 * k);
+                uv[k] = ld_vstep(uu + rb + 128 * k);
+                lv[k] = ld_vstep(a.lam + rb + 128 * k);
                 l0[k] = lv[k];
             }
             {   // u(t_s) = u_i + Σ_m θ^m Q_m (stage_sum order: Σ first, then added)
@@ -830,7 +871,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
 #pragma unroll
-                    for (int k = 0; k < NP; ++k) q[m][k] = ld_stream(a.su_q[s][m] + rb + 128 * k);
+                    for (int k = 0; k < NP; ++k) q[m][k] = ld_vstep(a.su_q[s][m] + rb + 128 * k);
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
                     kd2 t{0.0, 0.0};
@@ -856,7 +897,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
                         const double c = a.a[s][j], ce = a.ec[j];
 #pragma unroll
                         for (int k = 0; k < NP; ++k) {
-                            const kd2 kj = ld_stream(a.kl[j] + rb + 128 * k);
+                            const kd2 kj = ld_vstep(a.kl[j] + rb + 128 * k);
                             t[k].x = ::fma(c, kj.x, t[k].x);
                             t[k].y = ::fma(c, kj.y, t[k].y);
                             if (want_err) {
@@ -873,9 +914,9 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
                     ev[k] = e[k];
                 }
             }
-            if (last && a.lam_out) {
+            if (last && a.lam_out) {   // (read by the next adjoint step)
 #pragma unroll
-                for (int k = 0; k < NP; ++k) st_stream(a.lam_out + rb + 128 * k, lv[k]);
+                for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + 128 * k, lv[k]);
             }
             double rr[NP], rl[NP];
 #pragma unroll
@@ -914,7 +955,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
                 kd2 o;
                 o.x = a0 + x0b;
                 o.y = a1 + x1b;
-                st_stream(out + rb + 128 * k, o);
+                st_vstep(out + rb + 128 * k, o);
                 if (want_err) {
                     const double en = a.ec[6];
                     const double ex = ::fma(en, o.x, ek.x), ey = ::fma(en, o.y, ek.y);
@@ -1077,8 +1118,8 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
         kd2 uv[NP], kk[7][NP], y[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            uv[k] = ld_stream(u + rb + 128 * k);
-            kk[0][k] = ld_stream(k1 + rb + 128 * k);
+            uv[k] = ld_fstep(u + rb + 128 * k);
+            kk[0][k] = ld_fstep(k1 + rb + 128 * k);
         }
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
@@ -1112,11 +1153,11 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                 }
             }
 #pragma unroll
-            for (int k = 0; k < NP; ++k) st_stream(so.k[5] + rb + 128 * k, kk[6][k]);
+            for (int k = 0; k < NP; ++k) st_fstep(so.k[5] + rb + 128 * k, kk[6][k]);
         }
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            st_stream(so.u_new + rb + 128 * k, y[k]);
+            st_fstep(so.u_new + rb + 128 * k, y[k]);
             if (want_err) {
                 kd2 e{0.0, 0.0};
 #pragma unroll
@@ -1476,7 +1517,9 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>, lds, kVjpBlock);             \
-        grid = grid_for(B, kVjpBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        const char* ovs = getenv("KANODE_VSTEP_GRID");   /* experiments: grid override */         \
+        const int gcap = ovs && atoi(ovs) > 0 ? atoi(ovs) : cap;                                                 \
+        grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                                \
         if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                           \
         hipLaunchKernelGGL((fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>), dim3(grid), dim3(kVjpBlock), lds, st,  \
