@@ -239,6 +239,8 @@ def main() -> None:
                     help="nccl (= RCCL) for one rank per GPU; gloo only to rehearse the multi-rank path")
     ap.add_argument("--no-table", action="store_true",
                     help="per-point basis recurrence instead of the piecewise-polynomial table (kan_pp.hip)")
+    ap.add_argument("--grid-rhs", type=int, default=0,
+                    help="tuning: persistent grid of the table RHS kernel (KANODE_OPT_GRID_RHS; 0 = default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -267,6 +269,8 @@ def main() -> None:
     rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev,
                               table=False if args.no_table else None)
     table = rhs.hd.pointwise_table
+    if args.grid_rhs:
+        rhs.hd.set_option("grid_rhs", args.grid_rhs)
     p_np = kan1.setup(np.random.default_rng(0))[0].astype(np.float64)
     p = torch.as_tensor(p_np, device=dev)
     u = fk_ics(B, nx, dx, seed=1000 + rank, device=dev)

@@ -125,7 +125,9 @@ int64_t kanode_state_length(const kanode_handle* h);     /* N of the [N, B] stat
 kanode_status kanode_knots(const kanode_handle* h, int32_t layer, float* grid_out /* [G] host */);
 
 /* Pre-size handle workspaces for batches up to max_batch (no allocation in later
- * device calls with batch <= max_batch; required before hipGraph capture). */
+ * device calls with batch <= max_batch; required before hipGraph capture).  A device
+ * call that would still need to allocate while its stream is capturing returns
+ * KANODE_ERR_CAPTURE instead. */
 kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
 
 /* Evaluation-strategy switches (no reference counterpart: they select between
@@ -134,8 +136,30 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     through the per-launch piecewise-polynomial table (default where admissible:
  *     rbf/rswaf basis, even nx), 0 = the per-point basis recurrence.  Setting 1
  *     where inadmissible returns KANODE_ERR_UNSUPPORTED.
- * kanode_get_option returns the current value, or -1 for an unknown option. */
-typedef enum { KANODE_OPT_POINTWISE_TABLE = 1 } kanode_option;
+ *   KANODE_OPT_FUSED_STEP (default 1): the integrator issues one launch per Tsit5 /
+ *     adjoint step where a fused step kernel covers the RHS (Fisher-KPP table path,
+ *     small chains); 0 = one kanode_rhs_stage / kanode_vjp_stage launch per stage with
+ *     the K-form dense output.
+ *   KANODE_OPT_FUSED_SOLVE (default 1): control = auto may run a small-chain solve as
+ *     one workgroup; 0 = always the host loop.
+ *   KANODE_OPT_FUSED_SOLVE_CAP (default 0): dense-output slots of that one-workgroup
+ *     solve (0 = its own block; small values exercise the host-loop fallback).
+ *   KANODE_OPT_GRID_RHS / _GRID_VJP / _GRID_ADJ_STEP (default 0): persistent grid of
+ *     the Fisher-KPP table kernels: RHS, RK stage and one-launch Tsit5 step / VJP and
+ *     adjoint stage / one-launch adjoint step (0 = occupancy-derived).
+ *     Tuning only: the grid fixes the order of the dp reduction, so gradients are
+ *     bitwise reproducible for a given grid, not across grids.
+ * Options are read when a call is issued (never from the environment).  kanode_get_option
+ * returns the current value, or -1 for an unknown option. */
+typedef enum {
+    KANODE_OPT_POINTWISE_TABLE = 1,
+    KANODE_OPT_FUSED_STEP = 2,
+    KANODE_OPT_FUSED_SOLVE = 3,
+    KANODE_OPT_FUSED_SOLVE_CAP = 4,
+    KANODE_OPT_GRID_RHS = 5,
+    KANODE_OPT_GRID_VJP = 6,
+    KANODE_OPT_GRID_ADJ_STEP = 7
+} kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);
 

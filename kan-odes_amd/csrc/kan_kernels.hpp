@@ -55,18 +55,24 @@ hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, h
 // tables of an earlier launch with the same p (the integrator holds them per solve).  `tables` holds
 // kPPMaxFns slots of kPPCoef·ni doubles (slot = PPFn id); the build fills the listed
 // functions from p, the RHS then reads slot PP_PHI (fp64, Nx even).
+// Persistent-grid overrides of the table kernels (kanode_set_option KANODE_OPT_GRID_*; 0 = the
+// occupancy-derived default).  Tuning sweeps only: the grid fixes the dp reduction order.
+struct GridOverride {
+    int rhs = 0, vjp = 0, vstep = 0;
+};
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
                               double* tables, const int* fns, int nfn, hipStream_t st);
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
-                            hipStream_t st, bool build = true);
+                            hipStream_t st, bool build = true, int grid_ovr = 0);
 bool fk_vjp_pp_supported(const LayerConst& hlc, int Nx);
 bool fk_stage_pp_supported(const PPConst& hpc, int Nx);
 // fused stage: du = f(u + Σ c_j k_j), optional y_out, optional error total into err_out[0]
 hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                               const double* p, double* table, double cd, double co, int Nx, const double* u,
                               const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
-                              double* err_out, double* du, int64_t B, hipStream_t st, bool build = true);
+                              double* err_out, double* du, int64_t B, hipStream_t st, bool build = true,
+                              int grid_ovr = 0);
 // A whole Tsit5 step of the Fisher-KPP table RHS per trajectory row (fk_step_pp_wave_kernel):
 // a6x6[6s + j] = dt·a_sj, e7 = dt·btilde (error with err_out), k_2..k_7 -> kout[0..5]; with
 // q4x7[7m + i] = dt·RI[i][m] the dense output is Q_1..Q_4 -> kout[0..3] and k_7 -> kout[5]
@@ -74,11 +80,12 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
                              const double* p, double* table, double cd, double co, int Nx, const double* u,
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
                              const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
-                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build);
+                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build,
+                             int grid_ovr = 0);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
-                            hipStream_t st, bool build = true);
+                            hipStream_t st, bool build = true, int grid_ovr = 0);
 // adjoint stage, fused (kanode_vjp_stage): y = u + Σ su.c_j su.k_j, λs = lam + Σ sl.c_j sl.k_j
 // in registers (λs -> lam_out if non-null), λᵀJ at y, dp (= if dp_assign, else +=), the λ
 // error total -> err_out[0] when non-null (sl.ec / abstol / reltol)
@@ -87,7 +94,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
                                   const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
                                   double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
                                   double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build = true,
-                                  int* deferred_grid = nullptr);
+                                  int* deferred_grid = nullptr, int grid_ovr = 0);
 // The reductions of several adjoint stages launched with deferred_grid (their slabs in
 // separate regions) in one launch: job j sums slab_j rows into dp_j (= or +=) and err_slab_j
 // into err_out_j, each in the fixed order of vjp_finish_kernel.
@@ -110,7 +117,7 @@ struct AdjStepArgs {
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
-                                 hipStream_t st, bool build);
+                                 hipStream_t st, bool build, int grid_ovr = 0);
 constexpr int kMaxFinishJobs = 8;
 struct FinishJob {
     const double* slab;

@@ -676,7 +676,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     if (STG && stage_skip(sl.skip)) return;
     const int tsz = (kPPCoef / 2) * ni;   // double2 per table
-    for (int i = threadIdx.x; i < tsz; i += kBlock) {
+    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
         tl[tsz + i] = tables[PP_SWISH * tsz + i];
     }
@@ -827,7 +827,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     const int tsz = (kPPCoef / 2) * ni;
-    for (int i = threadIdx.x; i < tsz; i += kBlock) {
+    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
         tl[tsz + i] = tables[PP_SWISH * tsz + i];
     }
@@ -1245,7 +1245,7 @@ fk_stage_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 // Persistent grid: min(resident blocks per CU, 4) x CUs, each block stages the table
 // once.  4 blocks (16 waves) per CU streamed fastest in the grid sweep (tools/pp_grid.sh:
 // 98.7 us at 1024 blocks vs 101.4 us at the 6-block occupancy limit); the nontemporal
-// copy microbenchmark peaks at the same shape.  KANODE_PP_GRID overrides (tuning only).
+// copy microbenchmark peaks at the same shape.  KANODE_OPT_GRID_RHS overrides (tuning only).
 template <typename K>
 static int pp_grid_cap(K kernel, size_t lds, int bs = kBlock) {
     int dev = 0, cus = 256, nb = 0;
@@ -1267,7 +1267,7 @@ hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PP
 
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
-                            hipStream_t st, bool build) {
+                            hipStream_t st, bool build, int grid_ovr) {
     if (Nx < 2 || (Nx & 1)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
     if (build) {
@@ -1282,9 +1282,7 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
-        const char* ovs = getenv("KANODE_PP_GRID");   /* experiments: grid override */             \
-        const int ovr = ovs ? atoi(ovs) : 0;                                                                     \
-        const int grid = grid_for(B, kBlock / kWave, ovr > 0 ? ovr : cap);                                       \
+        const int grid = grid_for(B, kBlock / kWave, grid_ovr > 0 ? grid_ovr : cap);                             \
         hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B);                  \
     } while (0)
@@ -1318,7 +1316,7 @@ bool fk_stage_pp_supported(const PPConst& hpc, int Nx) { return hpc.enabled && (
 hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                               const double* p, double* table, double cd, double co, int Nx, const double* u,
                               const StageArgs<double>& sa, double* y_out, double* err_slab, int slab_blocks,
-                              double* err_out, double* du, int64_t B, hipStream_t st, bool build) {
+                              double* err_out, double* du, int64_t B, hipStream_t st, bool build, int grid_ovr) {
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
     hipError_t e = hipSuccess;
@@ -1330,7 +1328,8 @@ hipError_t launch_fk_stage_pp(const PPConst& hpc, const LayerConst& hlc, const L
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_stage_pp_wave_kernel<NORM, BASIS, NP>, lds);                             \
-        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
+        grid = grid_for(B, kBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_stage_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p, \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, sa, y_out, slab, du, B);  \
     } while (0)
@@ -1354,7 +1353,7 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
                              const double* p, double* table, double cd, double co, int Nx, const double* u,
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
                              const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
-                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build) {
+                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build, int grid_ovr) {
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
     hipError_t e = hipSuccess;
@@ -1379,7 +1378,8 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_step_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
-        grid = grid_for(B, kBlock / kWave, cap < slab_blocks ? cap : slab_blocks);                              \
+        const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
+        grid = grid_for(B, kBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,  \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, k1, so, sc, slab, B);    \
     } while (0)
@@ -1412,15 +1412,14 @@ template <int NORM, int PATH, int GT, bool STG>
 static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const double* p, const double* tables,
                                double cd, double co, int Nx, const double* u, const double* lam, double* lamJ,
                                double* slab, int slab_blocks, int64_t B, int& grid, const StageArgs<double>& su,
-                               const StageArgs<double>& sl, double* lam_out, double* err_slab, hipStream_t st) {
+                               const StageArgs<double>& sl, double* lam_out, double* err_slab, hipStream_t st,
+                               int grid_ovr) {
     const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
 #define KAN_VJP_WAVE(NP)                                                                                          \
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds, kVjpBlock);            \
-        const char* ovs = getenv("KANODE_VJP_GRID");   /* experiments: grid override */           \
-        const int ovr = ovs ? atoi(ovs) : 0;                                                                     \
-        const int gcap = ovr > 0 ? ovr : cap;                                                                    \
+        const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
         grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kVjpBlock), lds, st,  \
                            lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
@@ -1438,10 +1437,10 @@ static hipError_t fk_vjp_pp_dispatch(const PPConst& hpc, const LayerConst& hlc, 
                                      const double* tables, double cd, double co, int Nx, const double* u,
                                      const double* lam, double* lamJ, double* slab, int slab_blocks, int64_t B,
                                      int& grid, const StageArgs<double>& su, const StageArgs<double>& sl,
-                                     double* lam_out, double* err_slab, hipStream_t st) {
+                                     double* lam_out, double* err_slab, hipStream_t st, int grid_ovr) {
 #define KAN_VJP_GO(NORM, PATH, GT)                                                                               \
     return fk_vjp_pp_go<NORM, PATH, GT, STG>(hpc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, slab_blocks, B, \
-                                             grid, su, sl, lam_out, err_slab, st)
+                                             grid, su, sl, lam_out, err_slab, st, grid_ovr)
     if (hlc.path == PATH_REC_CORR) {
         if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_VJP_GO(NORM_SOFTSIGN, PATH_REC_CORR, 10);
         else if (hlc.G == 10) KAN_VJP_GO(NORM_TANH_FAST, PATH_REC_CORR, 10);
@@ -1459,7 +1458,7 @@ static hipError_t fk_vjp_pp_dispatch(const PPConst& hpc, const LayerConst& hlc, 
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
-                            hipStream_t st, bool build) {
+                            hipStream_t st, bool build, int grid_ovr) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1467,7 +1466,7 @@ hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
     int grid = 0;
     const StageArgs<double> none{};
     e = fk_vjp_pp_dispatch<false>(hpc, hlc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, slab_blocks, B, grid, none,
-                                  none, nullptr, nullptr, st);
+                                  none, nullptr, nullptr, st, grid_ovr);
     if (e != hipSuccess || !dp) return e;
     return launch_slab_reduce<double>(slab, grid, hlc.G + (hlc.use_base ? 1 : 0), dp, st);
 }
@@ -1477,7 +1476,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
                                   const StageArgs<double>& su, const double* lam, const StageArgs<double>& sl,
                                   double* lam_out, double* lamJ, double* dp, bool dp_assign, double* err_out,
                                   double* slab, int slab_blocks, int64_t B, hipStream_t st, bool build,
-                                  int* deferred_grid) {
+                                  int* deferred_grid, int grid_ovr) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1487,7 +1486,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
     // with deferred_grid the reduction is left to launch_vjp_finish_jobs
     const int cap = slab_blocks / 2;
     e = fk_vjp_pp_dispatch<true>(hpc, hlc, lc, p, tables, cd, co, Nx, u, lam, lamJ, slab, cap, B, grid, su, sl,
-                                 lam_out, err_out ? slab : nullptr, st);
+                                 lam_out, err_out ? slab : nullptr, st, grid_ovr);
     if (e != hipSuccess) return e;
     const int P = hlc.G + (hlc.use_base ? 1 : 0);
     if (deferred_grid) {
@@ -1504,7 +1503,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
-                                 int* grid_out, hipStream_t st, bool build) {
+                                 int* grid_out, hipStream_t st, bool build, int grid_ovr) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1517,8 +1516,7 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>, lds, kVjpBlock);             \
-        const char* ovs = getenv("KANODE_VSTEP_GRID");   /* experiments: grid override */         \
-        const int gcap = ovs && atoi(ovs) > 0 ? atoi(ovs) : cap;                                                 \
+        const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
         grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                                \
         if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                           \

@@ -56,6 +56,11 @@ struct kanode_handle {
     kan::PPConst* dpc = nullptr;
     double* dtable = nullptr;
     bool pp_on = false;
+    // evaluation-strategy options (kanode_set_option; read here, never from the environment per launch)
+    bool fused_step = true;           // KANODE_OPT_FUSED_STEP
+    bool fused_solve = true;          // KANODE_OPT_FUSED_SOLVE
+    int fused_solve_cap = 0;          // KANODE_OPT_FUSED_SOLVE_CAP (0 = the kernel's block)
+    kan::GridOverride grid_ovr{};     // KANODE_OPT_GRID_{RHS,VJP,ADJ_STEP} (0 = default)
     // the integrator's storage for solves without a dense output (kanode_solve.cpp)
     kanode_solution* solve_cache = nullptr;
     // table reuse inside one integrator solve (p constant): build each table set once
@@ -333,7 +338,7 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
         if constexpr (std::is_same<T, double>::value) {
             if (h->pp_on) {
                 HIP_TRY(h, kan::launch_fk_rhs_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co, (int)h->spec.nx, u, du,
-                                                 B, st, table_build(h, h->built_phi)));
+                                                 B, st, table_build(h, h->built_phi), h->grid_ovr.rhs));
                 return KANODE_OK;
             }
         }
@@ -385,7 +390,7 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
             if (h->pp_on && kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx)) {
                 HIP_TRY(h, kan::launch_fk_vjp_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                  (int)h->spec.nx, u, lam, out, dp, (double*)h->slab, kSlabBlocks, B,
-                                                 st, table_build(h, h->built_vjp)));
+                                                 st, table_build(h, h->built_vjp), h->grid_ovr.vjp));
                 return KANODE_OK;
             }
         }
@@ -463,7 +468,8 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
             const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
             HIP_TRY(h, kan::launch_fk_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                (int)h->spec.nx, u, sa, (double*)sg->y_out, (double*)h->slab,
-                                               kSlabBlocks, err_out, du, B, st, table_build(h, h->built_phi)));
+                                               kSlabBlocks, err_out, du, B, st, table_build(h, h->built_phi),
+                                               h->grid_ovr.rhs));
             return KANODE_OK;
         }
     }
@@ -527,6 +533,23 @@ kanode_status stage_args(kanode_handle* h, const kanode_stage* sg, kan::StageArg
 // one region of the deferred reduction slab: [grid][G+1] partials + [grid] error partials, grid <= kSlabBlocks/2
 constexpr size_t kDeferRegion = (size_t)(kSlabBlocks / 2) * (kan::kMaxGrid + 2);
 
+// The fixed-size reduction slabs of the Fisher-KPP table adjoint (deferred stage reductions and the
+// one-launch adjoint step).  kanode_create allocates them for handles that can take that path; this
+// covers a handle whose table path was switched on later, and refuses to allocate under capture.
+kanode_status ensure_adjoint_slabs(kanode_handle* h, hipStream_t st, bool at_create = false) {
+    if (h->defer_slab && h->step_slab) return KANODE_OK;
+    if (!at_create && is_capturing(st))
+        return fail(h, KANODE_ERR_CAPTURE, "adjoint reduction slabs would be allocated during capture");
+    const size_t defer = kDeferRegion * sizeof(double) * kan::kMaxFinishJobs;
+    const size_t step = (size_t)(kSlabBlocks / 2) * (6 * (kan::kMaxGrid + 1) + 1) * sizeof(double);
+    if ((!h->defer_slab && hipMalloc(&h->defer_slab, defer) != hipSuccess) ||
+        (!h->step_slab && hipMalloc(&h->step_slab, step) != hipSuccess)) {
+        (void)hipGetLastError();
+        return fail(h, KANODE_ERR_ALLOC, "adjoint reduction slabs");
+    }
+    return KANODE_OK;
+}
+
 kanode_status vjp_flush(kanode_handle* h, hipStream_t st) {
     if (h->njobs == 0) return KANODE_OK;
     const int n = h->njobs;
@@ -558,18 +581,13 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
             double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
             if (defer && (dp || err_out)) {
                 if (h->njobs == kan::kMaxFinishJobs && (s = vjp_flush(h, st)) != KANODE_OK) return s;
-                if (!h->defer_slab && hipMalloc(&h->defer_slab, kDeferRegion * sizeof(double) * kan::kMaxFinishJobs) !=
-                                          hipSuccess) {
-                    (void)hipGetLastError();
-                    h->defer_slab = nullptr;
-                    return fail(h, KANODE_ERR_ALLOC, "adjoint stage reduction slab");
-                }
+                if ((s = ensure_adjoint_slabs(h, st)) != KANODE_OK) return s;
                 double* region = (double*)h->defer_slab + (size_t)h->njobs * kDeferRegion;
                 int grid = 0;
                 HIP_TRY(h, kan::launch_fk_vjp_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                        (int)h->spec.nx, u, su, lam, sl, (double*)adj->y_out, lamJ,
                                                        dp, dp_assign, err_out, region, kSlabBlocks, B, st,
-                                                       table_build(h, h->built_vjp), &grid));
+                                                       table_build(h, h->built_vjp), &grid, h->grid_ovr.vjp));
                 kan::FinishJob& jb = h->jobs.j[h->njobs++];
                 jb.slab = region;
                 jb.err_slab = region + (int64_t)grid * (h->hlc[0].G + 1);
@@ -582,7 +600,7 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
             HIP_TRY(h, kan::launch_fk_vjp_stage_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, p, h->dtable, cd, co,
                                                    (int)h->spec.nx, u, su, lam, sl, (double*)adj->y_out, lamJ, dp,
                                                    dp_assign, err_out, (double*)h->slab, kSlabBlocks, B, st,
-                                                   table_build(h, h->built_vjp)));
+                                                   table_build(h, h->built_vjp), nullptr, h->grid_ovr.vjp));
             return KANODE_OK;
         }
     }
@@ -709,6 +727,10 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
                 (e = hipMalloc(&h->dtable, sizeof(double) * kan::kPPMaxFns * kan::kPPCoef * h->hpc.ni)) != hipSuccess)
                 return bail(fail(h, KANODE_ERR_HIP, std::string("pp table: ") + hipGetErrorString(e)));
             h->pp_on = true;
+            if (kan::fk_vjp_pp_supported(h->hlc[0], (int)spec->nx)) {
+                kanode_status s = ensure_adjoint_slabs(h, nullptr, true);
+                if (s != KANODE_OK) return bail(s);
+            }
         }
     }
     h->slab_bytes = (size_t)kSlabBlocks * (size_t)std::max(h->max_layer_P, 1) * h->esize;
@@ -768,6 +790,17 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch) {
 
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value) {
     if (!h) return KANODE_ERR_INVALID_ARG;
+    auto flag = [&](bool& dst, const char* name) {
+        if (value != 0 && value != 1) return fail(h, KANODE_ERR_INVALID_ARG, std::string(name) + " takes 0 or 1");
+        dst = value == 1;
+        return KANODE_OK;
+    };
+    auto count = [&](int& dst, const char* name, int64_t hi) {
+        if (value < 0 || value > hi)
+            return fail(h, KANODE_ERR_INVALID_ARG, std::string(name) + " takes 0.." + std::to_string(hi));
+        dst = (int)value;
+        return KANODE_OK;
+    };
     switch (option) {
     case KANODE_OPT_POINTWISE_TABLE:
         if (value != 0 && value != 1) return fail(h, KANODE_ERR_INVALID_ARG, "POINTWISE_TABLE takes 0 or 1");
@@ -776,6 +809,12 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
                         "POINTWISE_TABLE needs a pointwise f64 RHS with rbf/rswaf basis and even nx");
         h->pp_on = value == 1;
         return KANODE_OK;
+    case KANODE_OPT_FUSED_STEP: return flag(h->fused_step, "FUSED_STEP");
+    case KANODE_OPT_FUSED_SOLVE: return flag(h->fused_solve, "FUSED_SOLVE");
+    case KANODE_OPT_FUSED_SOLVE_CAP: return count(h->fused_solve_cap, "FUSED_SOLVE_CAP", 1 << 20);
+    case KANODE_OPT_GRID_RHS: return count(h->grid_ovr.rhs, "GRID_RHS", 1 << 16);
+    case KANODE_OPT_GRID_VJP: return count(h->grid_ovr.vjp, "GRID_VJP", kSlabBlocks / 2);
+    case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -784,6 +823,12 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     if (!h) return -1;
     switch (option) {
     case KANODE_OPT_POINTWISE_TABLE: return h->pp_on ? 1 : 0;
+    case KANODE_OPT_FUSED_STEP: return h->fused_step ? 1 : 0;
+    case KANODE_OPT_FUSED_SOLVE: return h->fused_solve ? 1 : 0;
+    case KANODE_OPT_FUSED_SOLVE_CAP: return h->fused_solve_cap;
+    case KANODE_OPT_GRID_RHS: return h->grid_ovr.rhs;
+    case KANODE_OPT_GRID_VJP: return h->grid_ovr.vjp;
+    case KANODE_OPT_GRID_ADJ_STEP: return h->grid_ovr.vstep;
     }
     return -1;
 }
@@ -970,14 +1015,15 @@ kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream) {
 void kanode_internal_vjp_discard(kanode_handle* h) { h->njobs = 0; }
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
     if (h->spec.rhs_kind != KANODE_RHS_CHAIN || batch < 1 || batch > kan::kChainSolveMaxBatch) return false;
-    if (std::getenv("KANODE_NO_FUSED_SOLVE")) return false;   // experiments: force the host loop
+    if (!h->fused_solve) return false;
     for (int l = 0; l < h->n_layers; ++l)
         if (h->kind[l] != KIND_COL) return false;
     return true;
 }
+int kanode_internal_fused_solve_cap(const kanode_handle* h) { return h->fused_solve_cap; }
 bool kanode_internal_fk_step_ok(const kanode_handle* h) {
     return h->spec.dtype == KANODE_F64 && h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on &&
-           kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) && !std::getenv("KANODE_NO_FUSED_STEP");
+           kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) && h->fused_step;
 }
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
@@ -990,7 +1036,8 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
     HIP_TRY(h, kan::launch_fk_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                       (int)h->spec.nx, (const double*)u, (const double*)k1, (double* const*)kout,
                                       (double*)u_new, a6x6, e7, q4x7, abstol, reltol, (double*)h->slab, kSlabBlocks,
-                                      err_out, batch, (hipStream_t)stream, table_build(h, h->built_phi)));
+                                      err_out, batch, (hipStream_t)stream, table_build(h, h->built_phi),
+                                      h->grid_ovr.rhs));
     launched = true;
     return KANODE_OK;
 }
@@ -999,7 +1046,7 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
                                          double abstol, double reltol, double* err_out, int64_t batch, void* stream,
                                          bool& launched) {
     launched = false;
-    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || std::getenv("KANODE_NO_FUSED_STEP")) return KANODE_OK;
+    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || !h->fused_step) return KANODE_OK;
     for (int l = 0; l < h->n_layers; ++l)
         if (h->kind[l] != KIND_COL) return KANODE_OK;
     kan::ChainStepArgs a{};
@@ -1028,25 +1075,18 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
                                               double* err_out, int64_t batch, void* stream, bool& launched) {
     launched = false;
     if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
-        !kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx) || std::getenv("KANODE_NO_FUSED_STEP"))
+        !kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx) || !h->fused_step)
         return KANODE_OK;
     const hipStream_t st = (hipStream_t)stream;
     const int P = h->hlc[0].G + (h->hlc[0].use_base ? 1 : 0);
-    const size_t need = (size_t)(kSlabBlocks / 2) * (6 * P + 1);
-    if (!h->step_slab) {
-        if (hipMalloc(&h->step_slab, need * sizeof(double)) != hipSuccess) {
-            (void)hipGetLastError();
-            h->step_slab = nullptr;
-            return fail(h, KANODE_ERR_ALLOC, "adjoint step reduction slab");
-        }
-    }
+    if (kanode_status s = ensure_adjoint_slabs(h, st); s != KANODE_OK) return s;
     const double dx2 = h->spec.dx * h->spec.dx;
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     a->err_slab = err_out ? (double*)h->step_slab : nullptr;   // relocated by the launcher
     int grid = 0;
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                           (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
-                                          table_build(h, h->built_vjp)));
+                                          table_build(h, h->built_vjp), h->grid_ovr.vstep));
     kan::FinishJobs jobs{};
     double* base = (double*)h->step_slab;
     for (int s = 0; s < 6; ++s) {

@@ -42,6 +42,8 @@ void kanode_internal_vjp_discard(kanode_handle* h);
 // the one-workgroup small-chain solve (kd_chain_tsit5_kernel): whether this handle's RHS and a
 // batch qualify, and the launch (launched = false when the kernel does not cover the shape)
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch);
+// KANODE_OPT_FUSED_SOLVE_CAP: dense-output slots of the one-workgroup solve (0 = its default)
+int kanode_internal_fused_solve_cap(const kanode_handle* h);
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched);
 // a whole Tsit5 step per row on the Fisher-KPP table path (fk_step_pp_wave_kernel); launched =

@@ -445,7 +445,7 @@ kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, dou
             }
         } else {
             cap = std::min<int64_t>(o.maxiters, 4096);
-            if (const char* e = std::getenv("KANODE_FUSED_CAP")) cap = std::max(1, std::atoi(e));   // tests only
+            if (const int c = kanode_internal_fused_solve_cap(h)) cap = c;   // KANODE_OPT_FUSED_SOLVE_CAP
         }
         cap = std::max<int64_t>(cap, 1);
         if (f.cap < cap) {

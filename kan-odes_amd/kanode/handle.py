@@ -7,6 +7,7 @@ cross the boundary.  The flat parameter vector is the ComponentArray order
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from dataclasses import dataclass, field
 
@@ -152,6 +153,30 @@ class KanodeHandle:
     def pointwise_table(self, on: bool) -> None:
         L.check(L.lib().kanode_set_option(self._h, L.OPT_POINTWISE_TABLE, 1 if on else 0), self._h,
                 "kanode_set_option")
+
+    def set_option(self, name: str, value: int) -> None:
+        """kanode_set_option by name (see include/kanode.h: pointwise_table, fused_step, fused_solve,
+        fused_solve_cap, grid_rhs, grid_vjp, grid_adj_step)."""
+        if name not in L.OPTIONS:
+            raise KeyError(f"unknown option {name!r}; known: {sorted(L.OPTIONS)}")
+        L.check(L.lib().kanode_set_option(self._h, L.OPTIONS[name], int(value)), self._h, "kanode_set_option")
+
+    def get_option(self, name: str) -> int:
+        if name not in L.OPTIONS:
+            raise KeyError(f"unknown option {name!r}; known: {sorted(L.OPTIONS)}")
+        return int(L.lib().kanode_get_option(self._h, L.OPTIONS[name]))
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Temporarily set options: `with hd.options(fused_step=0): ...`."""
+        old = {k: self.get_option(k) for k in kw}
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     # -- RHS -----------------------------------------------------------------
     def rhs(self, p: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

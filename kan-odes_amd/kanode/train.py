@@ -56,6 +56,26 @@ def reg_loss(p: torch.Tensor, act_reg: float = 1.0, entropy_reg: float = 1.0) ->
     return a * act_reg + (-torch.sum(e * torch.log(e))) * entropy_reg
 
 
+def _group_ranks(group) -> set[int]:
+    import torch.distributed as dist
+    if group is None or group is dist.group.WORLD:
+        return set(range(dist.get_world_size()))
+    return set(dist.get_process_group_ranks(group))
+
+
+def _check_orthogonal(dp_group, tp_group) -> None:
+    """The data-parallel gradient group of a grid-sharded trainer may share only this rank with the
+    grid-shard group: every other member of dp_group must own the same parameter slice."""
+    import torch.distributed as dist
+    if tp_group is None or not dist.is_initialized():
+        return
+    shared = (_group_ranks(dp_group) & _group_ranks(tp_group)) - {dist.get_rank()}
+    if dp_group is tp_group or shared:
+        raise ValueError("Trainer(tp=True): `group` must be the data-parallel group orthogonal to the rhs's "
+                         f"grid-shard group (it shares ranks {sorted(shared)}); all-reducing over it would add "
+                         "gradients of different parameter slices")
+
+
 class Trainer:
     """KAN-ODE training on a shard of trajectories.
 
@@ -66,7 +86,12 @@ class Trainer:
     def __init__(self, rhs, u0, tspan, saveat, target, p0, eta: float = 5e-4, solver: Tsit5Options | None = None,
                  sparse_reg: float = 0.0, group=None, sensealg: str | None = None, tp: bool = False):
         """tp=True: `rhs` is grid-sharded (kanode.tp.GridShardedChainRHS); u0/target/p0 are this rank's
-        slices, the loss is this shard's part of the global mean, gradients are shard-local."""
+        slices, the loss is this shard's part of the global mean, gradients are shard-local.  `group`
+        is then the ORTHOGONAL data-parallel group (ranks holding the same parameter slice for other
+        trajectories); passing the grid-shard group would sum slices of different parameters, so a
+        group sharing any rank with rhs.group other than this one is rejected."""
+        if tp and group is not None:
+            _check_orthogonal(group, getattr(rhs, "group", None))
         self.rhs, self.u0, self.tspan, self.saveat, self.target = rhs, u0, tspan, saveat, target
         self.tp = tp
         self.p = p0.detach().clone()

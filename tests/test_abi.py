@@ -40,6 +40,21 @@ def test_library_exports_every_declared_symbol():
     assert sorted(n for n, _, _ in L.SIGNATURES) == declared_functions()
 
 
+def test_option_ids_match_the_header():
+    """kanode_option enum values == the Python binding's OPTIONS table (names lower-cased)."""
+    src = open(HEADER).read()
+    body = re.search(r"typedef enum \{([^}]*)\} kanode_option;", src, flags=re.S).group(1)
+    ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"KANODE_OPT_(\w+)\s*=\s*(\d+)", body)}
+    assert ids == L.OPTIONS
+
+
+def test_library_has_no_environment_knobs():
+    """Launch-time behaviour comes from kanode_set_option, never from getenv in the hot path."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", kanode.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert not re.search(r"\bgetenv\b", out)
+
+
 def test_library_loads_and_reports_version():
     lib = kanode.lib()
     assert lib.kanode_abi_version() == 1

@@ -369,8 +369,8 @@ def test_fused_chain_adjoint_saveat_edges(ts):
     assert (ua - uh).abs().max().item() <= 1e-9 * max(1e-300, uh.abs().max().item())
 
 
-def test_fused_chain_solve_falls_back_when_dense_output_fills(monkeypatch):
-    """A dense output larger than the fused block (KANODE_FUSED_CAP, tests only) falls back to the
+def test_fused_chain_solve_falls_back_when_dense_output_fills():
+    """A dense output larger than the fused block (KANODE_OPT_FUSED_SOLVE_CAP) falls back to the
     host loop: same steps, same values, a usable dense output."""
     rhs = lv()
     u0 = t(_lv_u0(2))
@@ -382,39 +382,106 @@ def test_fused_chain_solve_falls_back_when_dense_output_fills(monkeypatch):
     ref = kanode.solve(rhs, u0, (0.0, 3.5), ref_p, ts, dataclasses.replace(opt, control="host"),
                        sensealg="interpolating_adjoint")
     (gr,) = torch.autograd.grad((ref.u * w).sum(), [ref_p])
-    monkeypatch.setenv("KANODE_FUSED_CAP", "3")
     p = p0.clone().requires_grad_(True)
-    sol = kanode.solve(rhs, u0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
-    (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+    with rhs.hd.options(fused_solve_cap=3):
+        sol = kanode.solve(rhs, u0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
+        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
     assert sol.stats["naccept"] == ref.stats["naccept"] > 3
     assert (sol.u - ref.u).abs().max().item() <= 1e-12 * max(1.0, ref.u.abs().max().item())
     assert (g - gr).abs().max().item() <= 1e-12 * gr.abs().max().item()
 
 
-@pytest.mark.parametrize("adaptive", [True, False])
-def test_fused_fk_step_matches_stage_launches(monkeypatch, adaptive):
-    """The one-launch Tsit5 step (fk_step_pp_wave_kernel, Q-form dense output) and adjoint step
-    (fk_vjp_step_pp_wave_kernel) against the per-stage launches with the K-form dense output
-    (KANODE_NO_FUSED_STEP): same steps, saveat values and gradients."""
-    rhs, u0, p0, tspan, ts = _setup("fk256")
-    if not adaptive:
-        tspan, dt = FIXED["fk256"]
-        ts = [x for x in ts if x <= tspan[1]] + [tspan[1]]
-    opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else 5e-4, abstol=1e-8, reltol=1e-7)
+def _fk_cfg(nx, G, norm, basis="rbf"):
+    kan1 = kanode.Chain(kanode.KDense(1, 1, G, normalizer=norm, basis_func=basis))
+    return kanode.FisherKPPRHS(kan1, nx=nx, dx=1.0 / (nx - 1), D=0.01, device=device())
+
+
+def _fused_vs_staged(rhs, u0, p0, tspan, ts, opt, grids=None):
+    """Solve + InterpolatingAdjoint with the one-launch step kernels (KANODE_OPT_FUSED_STEP = 1) and
+    with per-stage launches (0); returns ((sol, dp, du0) fused, (sol, dp, du0) staged)."""
     w = t(np.random.default_rng(12).normal(size=(len(ts),) + tuple(u0.shape)))
     out = {}
-    for fused in (True, False):
-        if fused:
-            monkeypatch.delenv("KANODE_NO_FUSED_STEP", raising=False)
-        else:
-            monkeypatch.setenv("KANODE_NO_FUSED_STEP", "1")
-        p = p0.clone().requires_grad_(True)
-        sol = kanode.solve(rhs, u0, tspan, p, ts, opt, sensealg="interpolating_adjoint")
-        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
-        out[fused] = (sol, g)
-    (sf, gf), (ss, gs) = out[True], out[False]
+    for fused in (1, 0):
+        with rhs.hd.options(fused_step=fused, **(grids or {})):
+            p = p0.clone().requires_grad_(True)
+            x0 = u0.clone().requires_grad_(True)
+            sol = kanode.solve(rhs, x0, tspan, p, ts, opt, sensealg="interpolating_adjoint")
+            g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+        out[fused] = (sol, g, gu)
+    return out[1], out[0]
+
+
+def _check_fused_vs_staged(fused, staged, adaptive):
+    (sf, gf, guf), (ss, gs, gus) = fused, staged
     assert sf.stats["naccept"] == ss.stats["naccept"] and sf.stats["nreject"] == ss.stats["nreject"]
-    assert abs(sf.stats["adjoint"]["naccept"] - ss.stats["adjoint"]["naccept"]) <= 1
+    assert abs(sf.stats["adjoint"]["naccept"] - ss.stats["adjoint"]["naccept"]) <= (1 if adaptive else 0)
     scale = max(1.0, ss.u.abs().max().item())
     assert (sf.u - ss.u).abs().max().item() <= 1e-12 * scale
     assert (gf - gs).abs().max().item() <= 1e-9 * gs.abs().max().item()
+    assert (guf - gus).abs().max().item() <= 1e-9 * gus.abs().max().item()
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+@pytest.mark.parametrize("nx", [128, 256, 512])
+@pytest.mark.parametrize("G,norm", [(10, "softsign"), (5, "tanh_fast")])
+def test_fused_fk_step_matches_stage_launches(adaptive, nx, G, norm):
+    """The one-launch Tsit5 step (fk_step_pp_wave_kernel, Q-form dense output) and adjoint step
+    (fk_vjp_step_pp_wave_kernel) against the per-stage launches with the K-form dense output
+    (KANODE_OPT_FUSED_STEP = 0): same steps, saveat values, dL/dp and dL/du0.  Nx = 128/256/512 are
+    the NP = 1/2/4 instantiations (the periodic wrap crosses pairs for NP > 1)."""
+    rhs = _fk_cfg(nx, G, norm)
+    u0 = t(fk_u0(nx, 4))
+    p0 = t(np.random.default_rng(7).uniform(-1.0, 1.0, G + 1))
+    if adaptive:
+        tspan, ts = (0.0, 1.0), [0.25 * i for i in range(5)]
+    else:
+        tspan, ts = (0.0, 0.1), [0.0, 0.05, 0.1]
+    opt = kanode.Tsit5Options(adaptive=adaptive, dt=None if adaptive else 5e-4, abstol=1e-8, reltol=1e-7)
+    _check_fused_vs_staged(*_fused_vs_staged(rhs, u0, p0, tspan, ts, opt), adaptive)
+
+
+@pytest.mark.parametrize("nx", [128, 256, 512])
+def test_fused_fk_step_several_rows_per_wave(nx):
+    """Persistent grids of ONE block (KANODE_OPT_GRID_*=1): each of its 4 waves runs 3 trajectory rows
+    through the forward step, the adjoint step and the per-stage kernels, so the row loops, the
+    per-row register reuse and the block-level moment sums over several rows are exercised."""
+    rhs = _fk_cfg(nx, 10, "softsign")
+    u0 = t(fk_u0(nx, 12, 3))
+    p0 = t(np.random.default_rng(8).uniform(-1.0, 1.0, 11))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7)
+    ts = [0.0, 0.2, 0.5]
+    one = dict(grid_rhs=1, grid_vjp=1, grid_adj_step=1)
+    fused, staged = _fused_vs_staged(rhs, u0, p0, (0.0, 0.5), ts, opt, one)
+    _check_fused_vs_staged(fused, staged, True)
+    # and the single-block grid against the default grid (only the dp reduction order differs)
+    dflt, _ = _fused_vs_staged(rhs, u0, p0, (0.0, 0.5), ts, opt)
+    _check_fused_vs_staged(fused, dflt, True)
+
+
+@pytest.mark.parametrize("norm,basis", [("sigmoid", "rbf"), ("softsign", "rswaf")])
+def test_qform_forward_with_per_stage_adjoint(norm, basis):
+    """Table-path configurations the fused adjoint step does not cover (fk_vjp_pp_supported false:
+    sigmoid normalizer, rswaf basis): the forward runs the one-launch step with the Q-form dense
+    output and the adjoint feeds the 4-array Q-form interpolant into the per-stage VJP.  Checked
+    against the all-per-stage run (K-form dense output) on dL/dp and dL/du0."""
+    rhs = _fk_cfg(256, 10, norm, basis)
+    assert rhs.hd.pointwise_table
+    u0 = t(fk_u0(256, 3, 4))
+    p0 = t(np.random.default_rng(9).uniform(-1.0, 1.0, 11))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7)
+    _check_fused_vs_staged(*_fused_vs_staged(rhs, u0, p0, (0.0, 0.5), [0.0, 0.25, 0.5], opt), True)
+
+
+def test_options_round_trip_and_reject_bad_values():
+    rhs = fk(256)
+    hd = rhs.hd
+    assert hd.get_option("fused_step") == 1 and hd.get_option("fused_solve") == 1
+    assert hd.get_option("grid_rhs") == hd.get_option("grid_vjp") == hd.get_option("grid_adj_step") == 0
+    with hd.options(fused_step=0, grid_vjp=7):
+        assert hd.get_option("fused_step") == 0 and hd.get_option("grid_vjp") == 7
+    assert hd.get_option("fused_step") == 1 and hd.get_option("grid_vjp") == 0
+    for name, bad in (("fused_step", 2), ("grid_rhs", -1), ("grid_vjp", 1 << 20), ("fused_solve_cap", -3)):
+        with pytest.raises(L.KanodeError):
+            hd.set_option(name, bad)
+    with pytest.raises(KeyError):
+        hd.set_option("no_such_option", 1)

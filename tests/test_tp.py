@@ -106,6 +106,15 @@ def _worker(rank, world, port, q):
                             solver=kanode.Tsit5Options(adaptive=False, dt=0.01), tp=True)
         out["losses"] = [tr.step() for _ in range(2)]
         out["p_trained"] = tp.gather_params(tr.p).numpy()
+        # the grid-shard group as the gradient group would sum different parameter slices: rejected
+        try:
+            kanode.Trainer(tp, u0[:, a:b].contiguous(), (0.0, 0.5), TS, target, pl, group=tp.group, tp=True)
+            out["overlap_rejected"] = False
+        except ValueError:
+            out["overlap_rejected"] = True
+        # a one-rank data-parallel group (this rank only) is orthogonal: accepted
+        solo = [dist.new_group([r]) for r in range(world)][rank]
+        kanode.Trainer(tp, u0[:, a:b].contiguous(), (0.0, 0.5), TS, target, pl, group=solo, tp=True)
         q.put(out)
     finally:
         dist.destroy_process_group()
@@ -168,3 +177,9 @@ def test_sharded_training_matches_unsharded(sharded):
         # Adam normalises each gradient entry (Δ = η m̂/(√v̂ + ϵ)): entries with |g| ~ ϵ turn the
         # rounding-level gradient differences of the sharded sums into ~1e-8 parameter differences
         assert np.max(np.abs(r["p_trained"] - tr.p.numpy())) <= 1e-7
+
+
+def test_trainer_rejects_the_grid_shard_group_as_gradient_group(sharded):
+    """Trainer(tp=True, group=<the rhs's own grid-shard group>) raises instead of averaging
+    gradients of different parameter slices."""
+    assert all(r["overlap_rejected"] for r in sharded)

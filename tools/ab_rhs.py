@@ -79,7 +79,7 @@ def main():
         cells.setdefault(("torch_copy", 0), []).append(e0.elapsed_time(e1) / a.reps)
         for n, lib in libs:
             for g in grids:
-                os.environ["KANODE_PP_GRID"] = str(g)
+                assert lib.kanode_set_option(hs[n], 6 if a.op == "vjp" else 5, g) == 0   # KANODE_OPT_GRID_VJP / _RHS
                 if a.op == "rhs":
                     call = lambda: lib.kanode_rhs(hs[n], C.c_void_p(p.data_ptr()), C.c_void_p(u.data_ptr()),  # noqa: E731
                                                   C.c_void_p(du.data_ptr()), a.batch, st)

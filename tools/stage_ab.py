@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Device time of one Fisher-KPP adjoint stage (kanode_vjp_stage: forward dense-output
 interpolation + adjoint stage input + VJP + reductions) against the plain VJP, by batch,
-number of interpolated arrays and grid (KANODE_VJP_GRID), from hipGraphs of back-to-back calls.
+number of interpolated arrays and grid (KANODE_OPT_GRID_VJP), from hipGraphs of back-to-back calls.
 
     python3 tools/stage_ab.py [--batch 4096]
 """
@@ -61,10 +61,7 @@ def main():
         fk.hd.reserve(B)
         mb = B * 256 * 8 / 1e6
         for grid in args.grids:
-            if grid:
-                os.environ["KANODE_VJP_GRID"] = str(grid)
-            else:
-                os.environ.pop("KANODE_VJP_GRID", None)
+            fk.hd.set_option("grid_vjp", grid or 0)
             t_vjp = graph_time(lambda: fk.hd.vjp(p, u, lam, dp=dp))
             row = [f"B={B:6d} grid={grid or 'auto':>5}  vjp {t_vjp:7.2f} us ({3 * mb / t_vjp:5.2f} TB/s)"]
             for nu, nl, err in ((0, 0, False), (7, 0, False), (7, 3, True), (7, 6, True)):

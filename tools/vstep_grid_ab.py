@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of the adjoint-step kernel's grid (KANODE_VSTEP_GRID, read at every launch)
+"""Interleaved A/B of the adjoint-step kernel's grid (KANODE_OPT_GRID_ADJ_STEP)
 on bench.py's epoch leg (FK256 fp64, fixed-step Tsit5 + InterpolatingAdjoint + Adam).
 
     python3 tools/vstep_grid_ab.py --batch 4096 --grids 0,512,640,1024 --rounds 5
@@ -44,7 +44,7 @@ def main():
     first = {}
     for r in range(a.rounds):
         for g in grids:
-            os.environ["KANODE_VSTEP_GRID"] = str(g)
+            rhs.hd.set_option("grid_adj_step", g)
             tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, target, p0, eta=1e-3, solver=solver)
             tr.step()
             torch.cuda.synchronize()
