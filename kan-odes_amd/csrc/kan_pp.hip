@@ -325,6 +325,9 @@ typedef double kd2 __attribute__((ext_vector_type(2)));
 #ifndef KAN_PP_ROWS
 #define KAN_PP_ROWS 1
 #endif
+#ifndef KAN_PP_COLD_GLOBAL_EXP
+#define KAN_PP_COLD_GLOBAL_EXP 1
+#endif
 __device__ __forceinline__ kd2 ld_stream(const double* p) {
 #if KAN_PP_NT
     return __builtin_nontemporal_load(reinterpret_cast<const kd2*>(p));
@@ -433,17 +436,26 @@ __device__ __forceinline__ void st_fstep(double* p, kd2 v) {
 // neighbours u[128k + 2l - 1] and u[128k + 2l + 2] are the neighbouring lanes'
 // values (wave rotations), the periodic wrap included: u is read from HBM once, by
 // streaming (nontemporal) loads, and du written once by streaming stores.
+// Row mapping (chunk = rows per wave): chunk > 0 gives block k the contiguous rows
+// [k·4·chunk, (k+1)·4·chunk), wave j taking rows j, j+4, ... of it, and the grid covers the batch
+// (ceil(B / (4 chunk)) blocks, dispatched as the hardware frees slots); chunk = 0 is the persistent
+// grid-stride form.  At 1M trajectories the contiguous chunks stream faster than a persistent grid
+// (the table staging is amortised over 4·chunk rows; profiles/r02/ab/).
 template <int NORM, int BASIS, int NP>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
 fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                       const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
-                      const double* __restrict__ u, double* __restrict__ du, int64_t B) {
+                      const double* __restrict__ u, double* __restrict__ du, int64_t B, int chunk) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     constexpr int R = KAN_PP_ROWS;   // rows per wave per pipeline step
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
-    int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int64_t rstride = chunk > 0 ? (int64_t)(kBlock / kWave) : (int64_t)gridDim.x * (kBlock / kWave);
+    int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) * (chunk > 0 ? chunk : 1) + (threadIdx.x >> 6);
+    if (chunk > 0) {
+        const int64_t end = ((int64_t)blockIdx.x + 1) * (kBlock / kWave) * chunk;
+        B = end < B ? end : B;
+    }
     // the first rows' loads are in flight while the block stages its table
     kd2 v[R][NP];
 #pragma unroll
@@ -455,8 +467,15 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         }
     }
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+#if KAN_PP_COLD_GLOBAL_EXP
+    // only the cold direct-formula branch takes exponentials: it reads the 2 KB 2^(j/256) table from
+    // global memory instead of every block staging it in LDS
+    __syncthreads();
+    const Math<double> M{kExp2Tab256};
+#else
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
+#endif
     const LayerConst& lc = *lcp;
     for (; b < B; b += R * rstride) {
         // software pipeline: the next R rows' loads are issued before these rows' math
@@ -1265,6 +1284,11 @@ hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PP
     return hipGetLastError();
 }
 
+#ifndef KAN_PP_CHUNK
+#define KAN_PP_CHUNK 4
+#endif
+constexpr int kPPChunk = KAN_PP_CHUNK;   // rows per wave of the table RHS kernel (0 = persistent grid)
+
 hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc, const double* p,
                             double* table, double cd, double co, int Nx, const double* u, double* du, int64_t B,
                             hipStream_t st, bool build, int grid_ovr) {
@@ -1282,9 +1306,11 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
-        const int grid = grid_for(B, kBlock / kWave, grid_ovr > 0 ? grid_ovr : cap);                             \
+        const int chunk = grid_ovr > 0 ? 0 : kPPChunk;                                                          \
+        const int grid = chunk > 0 ? grid_for(B, (kBlock / kWave) * chunk, 1 << 30)                               \
+                                   : grid_for(B, kBlock / kWave, grid_ovr > 0 ? grid_ovr : cap);                \
         hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
-                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B);                  \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B, chunk);           \
     } while (0)
 #define KAN_PP_PAIR(NORM, BASIS, SHORT)                                                                          \
     do {                                                                                                         \

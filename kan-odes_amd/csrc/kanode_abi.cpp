@@ -812,7 +812,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_FUSED_STEP: return flag(h->fused_step, "FUSED_STEP");
     case KANODE_OPT_FUSED_SOLVE: return flag(h->fused_solve, "FUSED_SOLVE");
     case KANODE_OPT_FUSED_SOLVE_CAP: return count(h->fused_solve_cap, "FUSED_SOLVE_CAP", 1 << 20);
-    case KANODE_OPT_GRID_RHS: return count(h->grid_ovr.rhs, "GRID_RHS", 1 << 16);
+    case KANODE_OPT_GRID_RHS: return count(h->grid_ovr.rhs, "GRID_RHS", 1 << 24);
     case KANODE_OPT_GRID_VJP: return count(h->grid_ovr.vjp, "GRID_VJP", kSlabBlocks / 2);
     case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
     }
