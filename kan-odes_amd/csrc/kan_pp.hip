@@ -77,9 +77,46 @@ struct PPFns {
     int fn[kPPMaxFns];
 };
 
+__device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
+                               const double* __restrict__ p, double* __restrict__ tables, PPFns fns);
+
 __global__ void __launch_bounds__(kBlock)
 fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
                    const double* __restrict__ p, double* __restrict__ tables, PPFns fns) {
+    // Parameter stamp (pp_stamp_region): the table of slot fn was last built from the parameters in
+    // its stamp.  When p matches it bit for bit, the blocks skip the build; the last block to finish
+    // (all blocks have compared by then) writes the stamp of this launch.
+    {
+        const PPConst& pc0 = *pcp;
+        const int G0 = lcp->G, fn0 = fns.fn[blockIdx.y];
+        double* __restrict__ stamp = pp_stamp(tables, pc0.ni, fn0);
+        __shared__ int same;
+        if (threadIdx.x < kWave) {
+            const int j = threadIdx.x;
+            const double pj = j <= G0 && (j < G0 || lcp->use_base) ? p[j] : 0.0;
+            const bool ne = j <= G0 && __double_as_longlong(stamp[j]) != __double_as_longlong(pj);
+            const bool valid = stamp[kPPStampValid] == 1.0;
+            if (j == 0) same = 0;
+            const bool any_ne = __any(ne);
+            if (j == 0) same = valid && !any_ne;
+        }
+        __syncthreads();
+        if (!same) pp_build_block(lcp, pcp, p, tables, fns);
+        __syncthreads();   // every thread of this block has written its coefficients
+        if (threadIdx.x == 0) {
+            __threadfence();
+            unsigned* cnt = reinterpret_cast<unsigned*>(stamp + kPPStampCount);
+            if (atomicAdd(cnt, 1u) == gridDim.x - 1) {
+                for (int j = 0; j <= G0; ++j) stamp[j] = j < G0 || lcp->use_base ? p[j] : 0.0;
+                stamp[kPPStampValid] = 1.0;
+                *cnt = 0u;
+            }
+        }
+    }
+}
+
+__device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
+                               const double* __restrict__ p, double* __restrict__ tables, PPFns fns) {
     __shared__ double sQ[kPPCoef * kPPCoef];
     __shared__ double sT[kPPEvals];              // nodes, then check points
     __shared__ double sC[kMaxGrid + 1];          // C_0..C_{G-1}, W

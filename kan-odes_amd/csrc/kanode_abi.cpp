@@ -724,7 +724,8 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
         if (h->hpc.enabled) {
             if ((e = hipMalloc(&h->dpc, sizeof(kan::PPConst))) != hipSuccess ||
                 (e = hipMemcpy(h->dpc, &h->hpc, sizeof(kan::PPConst), hipMemcpyHostToDevice)) != hipSuccess ||
-                (e = hipMalloc(&h->dtable, sizeof(double) * kan::kPPMaxFns * kan::kPPCoef * h->hpc.ni)) != hipSuccess)
+                (e = hipMalloc(&h->dtable, sizeof(double) * kan::pp_tables_doubles(h->hpc.ni))) != hipSuccess ||
+                (e = hipMemset(h->dtable, 0, sizeof(double) * kan::pp_tables_doubles(h->hpc.ni))) != hipSuccess)
                 return bail(fail(h, KANODE_ERR_HIP, std::string("pp table: ") + hipGetErrorString(e)));
             h->pp_on = true;
             if (kan::fk_vjp_pp_supported(h->hlc[0], (int)spec->nx)) {

@@ -182,3 +182,37 @@ def test_table_vjp_nonfinite_and_reproducible():
     rJ, _ = O.fk_vjp(O.LayerSpec(1, 1, 10, "softsign"), p, D, dx, u, lam)
     assert np.array_equal(np.isnan(lamJ.cpu().numpy()), np.isnan(rJ))
     assert torch.isnan(dp).all()
+
+
+def test_table_stamp_tracks_parameter_changes_in_place():
+    """The table build skips itself when p matches the stamp of the last build (bitwise): an
+    in-place change of p, a change of one bit, and a return to earlier values must all be seen
+    by the RHS and the VJP; a repeated call with unchanged p is bitwise identical."""
+    rhs = rhs_for(256, D=0.01, dx=1.0 / 255)
+    spec = O.LayerSpec(1, 1, 10, "softsign")
+    rng = np.random.default_rng(5)
+    u = rng.uniform(-1.5, 1.5, (6, 256))
+    lam = rng.normal(size=u.shape)
+    ut, lt = t(u), t(lam)
+    p = t(rng.uniform(-1, 1, 11))
+    p1 = p.clone()
+    p_bit = p1.clone()
+    p_bit[3] = float(np.nextafter(p_bit[3].item(), np.inf))
+    for pv in (p1, p1 * 2.0, p_bit, p1):
+        p.copy_(pv)                      # same device buffer, new contents
+        du = rhs.rhs(ut, p)
+        lamJ, dp = rhs.vjp(ut, p, lt)
+        pn = pv.cpu().numpy()
+        ref = O.fk_rhs(spec, pn, 0.01, 1.0 / 255, u)
+        rJ, rdp = O.fk_vjp(spec, pn, 0.01, 1.0 / 255, u, lam)
+        scale = np.max(np.abs(ref)) + 4 * 0.01 * 255 ** 2
+        assert np.max(np.abs(du.cpu().numpy() - ref)) <= 1e-13 * scale
+        assert np.max(np.abs(lamJ.cpu().numpy() - rJ)) <= 1e-12 * (np.max(np.abs(rJ)) + 4 * 0.01 * 255 ** 2)
+        assert np.max(np.abs(dp.cpu().numpy() - rdp)) <= 1e-11 * np.max(np.abs(rdp))
+        assert torch.equal(rhs.rhs(ut, p), du)
+    # the one-ulp change must rebuild: its table differs from p1's in at least one coefficient
+    p.copy_(p1)
+    d1 = rhs.rhs(ut, p).clone()
+    p.copy_(p_bit)
+    d2 = rhs.rhs(ut, p)
+    assert not torch.equal(d1, d2)
