@@ -270,12 +270,16 @@ constexpr int kWideOMax = 16;    // max out_dims of a wide-in layer
 template <typename T>
 hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
                                 int64_t K, hipStream_t st);
+// xslab (nullable): the layer input is the nblk chunk partials of the wide-in layer before it
+// (launch_kd_fwd_widein with y == nullptr), summed in the reduce kernel's order by the consumer
 template <typename T>
 hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
-                                 hipStream_t st);
+                                 hipStream_t st, const T* xslab = nullptr, int xnblk = 0);
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
-                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st);
+                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab = nullptr,
+                                 int xnblk = 0);
+inline int widein_chunks(const LayerConst& h) { return (h.I + 63) / 64; }
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
                                 T* pbar, int64_t K, hipStream_t st);

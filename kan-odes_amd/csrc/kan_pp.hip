@@ -711,6 +711,10 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 #endif
 
 constexpr int kVjpBlock = KAN_VJP_BLOCK;
+#ifndef KAN_VJP_CHUNK
+#define KAN_VJP_CHUNK 8
+#endif
+constexpr int kVjpChunk = KAN_VJP_CHUNK;   // rows per wave of the standalone table VJP (0 = persistent grid)
 // Nx = 128·NP, one wave per trajectory row (as fk_rhs_pp_wave_kernel): u and λ by
 // nontemporal 16-B loads, λ's stencil neighbours by wave rotation, λᵀJ by
 // nontemporal stores; per-thread dC/dW registers, block-summed into the slab row
@@ -726,7 +730,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                       const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
                       double* __restrict__ slab, int64_t B, StageArgs<double> su, StageArgs<double> sl,
-                      double* __restrict__ lam_out, double* __restrict__ err_slab) {
+                      double* __restrict__ lam_out, double* __restrict__ err_slab, int chunk) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
@@ -754,8 +758,14 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     const double suc = STG ? stage_scale(su.cscale) : 1.0, slc = STG ? stage_scale(sl.cscale) : 1.0;
     double eacc = 0.0;
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rstride = (int64_t)gridDim.x * (kVjpBlock / kWave);
-    for (int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+    // row mapping as fk_rhs_pp_wave_kernel: chunk > 0 = contiguous rows per block (grid covers B)
+    const int64_t rstride = chunk > 0 ? (int64_t)(kVjpBlock / kWave) : (int64_t)gridDim.x * (kVjpBlock / kWave);
+    if (chunk > 0) {
+        const int64_t end = ((int64_t)blockIdx.x + 1) * (kVjpBlock / kWave) * chunk;
+        B = end < B ? end : B;
+    }
+    for (int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) * (chunk > 0 ? chunk : 1) + (threadIdx.x >> 6); b < B;
+         b += rstride) {
         const int64_t rb = b * Nx + 2 * lane;
         kd2 uv[NP], lv[NP], l0[NP], ev[NP];
 #pragma unroll
@@ -1483,10 +1493,21 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds, kVjpBlock);            \
         const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
-        grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
+        /* the standalone VJP (not a stage): contiguous chunks over a batch-covering grid, chunk */             \
+        /* grown until the grid fits the slab */                                                                 \
+        int chunk = 0;                                                                                           \
+        if (!STG && grid_ovr == 0 && kVjpChunk > 0) {                                                            \
+            chunk = kVjpChunk;                                                                                   \
+            while ((B + (int64_t)(kVjpBlock / kWave) * chunk - 1) / ((int64_t)(kVjpBlock / kWave) * chunk) >     \
+                   slab_blocks)                                                                                  \
+                chunk *= 2;                                                                                      \
+            grid = grid_for(B, (kVjpBlock / kWave) * chunk, slab_blocks);                                        \
+        } else {                                                                                                 \
+            grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                      \
+        }                                                                                                        \
         hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kVjpBlock), lds, st,  \
                            lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
-                           su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr);               \
+                           su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr, chunk);        \
     } while (0)
     if (Nx == 256) KAN_VJP_WAVE(2);
     else if (Nx == 128) KAN_VJP_WAVE(1);

@@ -18,6 +18,10 @@
 // thread per (i, k) turns the G + 1 sums into x̄[i, k];
 // wide-in -- lane i owns dC[:, g + G i], dW[:, i] (accumulated in its own LDS slots over
 // the columns) and x̄[i, :].  Every reduction runs in a fixed order (bitwise reproducible).
+// Surrogate chain [wide-in, wide-out]: the wide-out kernels can take their input as the
+// wide-in layer's chunk partials (`xslab`), each block summing what it needs in the order of
+// kd_widein_reduce_kernel, so the chain RHS is two launches and its VJP four, bitwise equal to
+// the layer-by-layer path.
 #include "kan_common.hpp"
 #include "kan_kernels.hpp"
 
@@ -117,6 +121,30 @@ kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p
     }
 }
 
+// Element x[i, k] of a layer input [I, K]: from x, or (xslab != nullptr) the ordered sum over the
+// nblk chunk partials of the wide-in layer that produced it, xslab[(b*K + k)*I + i] -- the order
+// of kd_widein_reduce_kernel.
+template <typename T>
+__device__ __forceinline__ T layer_in(const T* __restrict__ x, const T* __restrict__ xslab, int nblk, int I, int64_t K,
+                                      int i, int64_t k) {
+    if (!xslab) return x[(int64_t)I * k + i];
+    // 16 partials in flight per round (a plain loop would wait for each load before the next
+    // add); the additions keep the reduce kernel's order
+    constexpr int kR = 16;
+    const T* __restrict__ src = xslab + k * I + i;
+    const int64_t stride = K * I;
+    T s = T(0);
+    for (int b0 = 0; b0 < nblk; b0 += kR) {
+        T v[kR];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) v[j] = b0 + j < nblk ? src[(int64_t)(b0 + j) * stride] : T(0);
+#pragma unroll
+        for (int j = 0; j < kR; ++j)
+            if (b0 + j < nblk) s += v[j];
+    }
+    return s;
+}
+
 // y[o + O*k] = Σ_b slab[(b*K + k)*O + o]   (ordered over b)
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
@@ -125,21 +153,20 @@ kd_widein_reduce_kernel(const T* __restrict__ slab, int nblk, int O, int64_t K, 
     if (idx >= (int64_t)O * K) return;
     const int64_t k = idx / O;
     const int o = (int)(idx - k * O);
-    T s = T(0);
-    for (int b = 0; b < nblk; ++b) s += slab[((int64_t)b * K + k) * O + o];
-    y[(int64_t)O * k + o] = s;
+    y[(int64_t)O * k + o] = layer_in<T>(nullptr, slab, nblk, O, K, o, k);
 }
 
 // Basis values of a column tile of the (short) input, staged in LDS:
 // phiL[(g + G i)*kKT + kk], swL[i*kKT + kk] (zero outside the tile).
 template <typename T, int PATH>
 __device__ __forceinline__ void stage_tile_basis(const Math<T>& M, const LayerConst& lc, const T* __restrict__ x,
-                                                 int64_t k0, int kt, T* phiL, T* swL) {
+                                                 const T* __restrict__ xslab, int nblk, int64_t K, int64_t k0, int kt,
+                                                 T* phiL, T* swL) {
     const int I = lc.I, G = lc.G;
     for (int t = threadIdx.x; t < I * kKT; t += blockDim.x) {
         const int i = t / kKT, kk = t - i * kKT;
         if (kk < kt) {
-            const T xi = x[(int64_t)I * (k0 + kk) + i];
+            const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k0 + kk);
             Basis1<T, PATH> bs;
             bs.init(M, lc, xi);
             for (int g = 0; g < G; ++g) {
@@ -163,7 +190,7 @@ constexpr int kWOB = 64;
 template <typename T, int PATH>
 __global__ void __launch_bounds__(kWOB * kSW)
 kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                      T* __restrict__ y, int64_t K) {
+                      const T* __restrict__ xslab, int nblk, T* __restrict__ y, int64_t K) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     __shared__ T red[kSW][kKT][kWOB];
     KAN_EXP_TABLE_LDS(tab);
@@ -180,7 +207,7 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
     for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
         const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
         __syncthreads();
-        stage_tile_basis<T, PATH>(M, lc, x, k0, kt, phiL, swL);
+        stage_tile_basis<T, PATH>(M, lc, x, xslab, nblk, K, k0, kt, phiL, swL);
         __syncthreads();
         T acc[kKT];
 #pragma unroll
@@ -225,18 +252,16 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
 // (coalesced over o).  The basis of input i is staged in LDS kWOPK columns at a time.
 constexpr int kWOPK = 128;
 template <typename T, int PATH>
-__global__ void __launch_bounds__(kWOB * kSW)
-kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ ybar,
-                            T* __restrict__ pbar, int64_t K) {
+__device__ __forceinline__ void wideout_param_body(const Math<T>& M, const LayerConst* __restrict__ lcp,
+                                                   const T* __restrict__ x, const T* __restrict__ xslab, int nblk,
+                                                   const T* __restrict__ ybar, T* __restrict__ pbar, int64_t K,
+                                                   int bx, int i) {
     __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
     __shared__ T red[kSW][kWOB];
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
-    const int i = blockIdx.y;
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const int o = blockIdx.x * kWOB + lane;
+    const int o = bx * kWOB + lane;
     const bool base = lc.use_base != 0;
     T acc[kMaxGrid + 1];
 #pragma unroll
@@ -245,7 +270,7 @@ kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restr
         const int kt = (int)((K - k0) < kWOPK ? (K - k0) : kWOPK);
         __syncthreads();
         for (int kk = threadIdx.x; kk < kt; kk += blockDim.x) {
-            const T xi = x[(int64_t)I * (k0 + kk) + i];
+            const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k0 + kk);
             Basis1<T, PATH> bs;
             bs.init(M, lc, xi);
             for (int g = 0; g < G; ++g) {
@@ -291,18 +316,19 @@ kd_vjp_wideout_param_kernel(const LayerConst* __restrict__ lcp, const T* __restr
 //   fin:  thread (i, k): x̄[i, k] from S through the basis / normalizer / swish rrules
 //         (utils.jl:15-21, NNlib).
 constexpr int kWOX = 256;
+static_assert(kWOX == kWOB * kSW, "the dot and parameter bodies share one launch");
 template <typename T>
-__global__ void __launch_bounds__(kWOX)
-kd_vjp_wideout_dot_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ ybar,
-                          T* __restrict__ S, int64_t K) {
+__device__ __forceinline__ void wideout_dot_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
+                                                 const T* __restrict__ ybar, T* __restrict__ S, int64_t K, int bx,
+                                                 int by, int gy) {
     __shared__ T red[kWOX / kWave][kKT];
     const LayerConst& lc = *lcp;
     const int O = lc.O, G = lc.G;
     const int R = G + (lc.use_base ? 1 : 0);
-    const int i = blockIdx.x / R, r = blockIdx.x - i * R;
+    const int i = bx / R, r = bx - i * R;
     const T* __restrict__ row = r < G ? p + lc.p_off + (int64_t)O * (r + (int64_t)G * i) : p + lc.w_off + (int64_t)O * i;
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    for (int64_t k0 = (int64_t)blockIdx.y * kKT; k0 < K; k0 += (int64_t)gridDim.y * kKT) {
+    for (int64_t k0 = (int64_t)by * kKT; k0 < K; k0 += (int64_t)gy * kKT) {
         const int kt = (int)((K - k0) < kKT ? (K - k0) : kKT);
         T acc[kKT];
 #pragma unroll
@@ -324,16 +350,36 @@ kd_vjp_wideout_dot_kernel(const LayerConst* __restrict__ lcp, const T* __restric
             T s = red[0][threadIdx.x];
 #pragma unroll
             for (int w = 1; w < kWOX / kWave; ++w) s += red[w][threadIdx.x];
-            S[((int64_t)blockIdx.x * K) + k0 + threadIdx.x] = s;
+            S[((int64_t)bx * K) + k0 + threadIdx.x] = s;
         }
         __syncthreads();
     }
 }
 
+// One launch for both independent parts of the wide-out pullback's first pass: blocks
+// [0, nd) are the dot products (nd = I·R·tiles, laid out (i·R + r) + I·R·tile), the rest the
+// parameter cotangents ((row chunk, input i) = (b % nrc, b / nrc)).
+template <typename T, int PATH>
+__global__ void __launch_bounds__(kWOX)
+kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                               const T* __restrict__ xslab, int nblk, const T* __restrict__ ybar, T* __restrict__ S,
+                               T* __restrict__ pbar, int64_t K, int nd, int tiles, int nrc) {
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const int b = blockIdx.x;
+    if (b < nd) {
+        const int ir = lcp->I * (lcp->G + (lcp->use_base ? 1 : 0));
+        wideout_dot_body<T>(lcp, p, ybar, S, K, b % ir, b / ir, tiles);
+    } else {
+        const int q = b - nd;
+        wideout_param_body<T, PATH>(M, lcp, x, xslab, nblk, ybar, pbar, K, q % nrc, q / nrc);
+    }
+}
+
 template <typename T, int PATH>
 __global__ void __launch_bounds__(kBlock)
-kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ S,
-                           T* __restrict__ xbar, int64_t K) {
+kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ xslab,
+                           int nblk, const T* __restrict__ S, T* __restrict__ xbar, int64_t K) {
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
@@ -345,7 +391,7 @@ kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restri
         const int64_t k = idx / I;
         const int i = (int)(idx - k * I);
         const T* __restrict__ Si = S + (int64_t)i * R * K + k;
-        const T xi = x[idx];
+        const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k);
         Basis1<T, PATH> bs;
         bs.init(M, lc, xi);
         T nbar = T(0);
@@ -482,7 +528,7 @@ hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const
     }
 #undef KAN_WI
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !y) return e;   // y == nullptr: the consumer sums the slab itself
     const int64_t n = (int64_t)h.O * K;
     hipLaunchKernelGGL((kd_widein_reduce_kernel<T>), dim3(grid_for(n, kBlock, 1 << 30)), dim3(kBlock), 0, st, slab,
                        nblk, h.O, K, y);
@@ -491,10 +537,11 @@ hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const
 
 template <typename T>
 hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
-                                 hipStream_t st) {
+                                 hipStream_t st, const T* xslab, int xnblk) {
     const dim3 grid((h.O + kWOB - 1) / kWOB, col_tiles(K));
     const size_t lds = wideout_lds(h, sizeof(T));
-#define KAN_WO(PATH) hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH>), grid, dim3(kWOB * kSW), lds, st, lc, p, x, y, K)
+#define KAN_WO(PATH)                                                                                               \
+    hipLaunchKernelGGL((kd_fwd_wideout_kernel<T, PATH>), grid, dim3(kWOB * kSW), lds, st, lc, p, x, xslab, xnblk, y, K)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WO(PATH_REC_CORR); break;
     case PATH_REC: KAN_WO(PATH_REC); break;
@@ -506,17 +553,18 @@ hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, cons
 
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
-                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st) {
+                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab, int xnblk) {
     const int R = h.G + (h.use_base ? 1 : 0);
-    const dim3 gp((h.O + kWOB - 1) / kWOB, h.I), gd(h.I * R, col_tiles(K));
+    const int tiles = (int)col_tiles(K), nrc = (h.O + kWOB - 1) / kWOB;
+    const int nd = xb ? h.I * R * tiles : 0, np = pbar ? nrc * h.I : 0;
     const unsigned gf = grid_for((int64_t)h.I * K, kBlock, kGridCap);
-    if (xb) hipLaunchKernelGGL((kd_vjp_wideout_dot_kernel<T>), gd, dim3(kWOX), 0, st, lc, p, yb, slab, K);
 #define KAN_WOV(PATH)                                                                                              \
     do {                                                                                                           \
-        if (pbar) hipLaunchKernelGGL((kd_vjp_wideout_param_kernel<T, PATH>), gp, dim3(kWOB * kSW), 0, st, lc, x, yb, pbar, \
-                                     K);                                                                          \
-        if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xfin_kernel<T, PATH>), dim3(gf), dim3(kBlock), 0, st, lc, x, slab, \
-                                   xb, K);                                                                        \
+        if (nd + np > 0)                                                                                           \
+            hipLaunchKernelGGL((kd_vjp_wideout_dotparam_kernel<T, PATH>), dim3(nd + np), dim3(kWOX), 0, st, lc, p, x, \
+                               xslab, xnblk, yb, slab, pbar, K, nd, tiles, nrc);                                  \
+        if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xfin_kernel<T, PATH>), dim3(gf), dim3(kBlock), 0, st, lc, x, xslab, \
+                                   xnblk, slab, xb, K);                                                           \
     } while (0)
     switch (h.path) {
     case PATH_REC_CORR: KAN_WOV(PATH_REC_CORR); break;
@@ -551,9 +599,9 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
     template hipError_t launch_kd_fwd_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*, T*, \
                                                 int64_t, hipStream_t);                                          \
     template hipError_t launch_kd_fwd_wideout<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,   \
-                                                 int64_t, hipStream_t);                                         \
+                                                 int64_t, hipStream_t, const T*, int);                          \
     template hipError_t launch_kd_vjp_wideout<T>(const LayerConst&, const LayerConst*, const T*, const T*,       \
-                                                 const T*, T*, T*, T*, int64_t, hipStream_t);                   \
+                                                 const T*, T*, T*, T*, int64_t, hipStream_t, const T*, int);    \
     template hipError_t launch_kd_vjp_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*,        \
                                                 const T*, T*, T*, int64_t, hipStream_t);
 KAN_WIDE_INST(double)

@@ -26,7 +26,10 @@ using kan::LayerConst;
 
 namespace {
 
-constexpr int kSlabBlocks = 4096;   // grid cap of the VJP kernels = slab rows
+#ifndef KAN_SLAB_BLOCKS
+#define KAN_SLAB_BLOCKS 4096
+#endif
+constexpr int kSlabBlocks = KAN_SLAB_BLOCKS;   // grid cap of the VJP kernels = slab rows
 
 // column: thread per batch column (small I·G, O <= 16; e.g. LV [2,10,2]);
 // wide-in / wide-out: the surrogate shapes (kan_wide.hip)
@@ -251,10 +254,18 @@ int64_t wide_slab_elems(const kanode_handle* h, int64_t B) {
     return m;
 }
 
+// The full-field surrogate shape KAN [N, H, N] (Burgers_Surrogate.jl:85-88,
+// Schrodinger_Surrogate.jl:93-96): a wide-in layer feeding a wide-out layer.  Its RHS and VJP
+// hand the hidden layer over as the wide-in chunk partials (no reduce launch).
+bool surrogate_pair(const kanode_handle* h) {
+    return h->n_layers == 2 && h->kind[0] == KIND_WIDE_IN && h->kind[1] == KIND_WIDE_OUT;
+}
+
 // Chain workspace layout (elements of the dtype), for a batch of B columns:
 //   [hidden activations: Σ_{l>=1} I_l·B][grad ping: max_dim·B][grad pong: max_dim·B][wide slab]
+//   [surrogate pair: the wide-in layer's chunk partials, chunks·B·H]
 struct WsLayout {
-    int64_t acts, g0, g1, wslab, total;
+    int64_t acts, g0, g1, wslab, pslab, total;
 };
 WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     WsLayout w{};
@@ -267,6 +278,8 @@ WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     e += (int64_t)h->max_dim * B;
     w.wslab = e;
     e += wide_slab_elems(h, B);
+    w.pslab = e;
+    if (surrogate_pair(h)) e += (int64_t)kan::widein_chunks(h->hlc[0]) * B * h->hlc[0].O;
     w.total = e;
     return w;
 }
@@ -356,6 +369,13 @@ kanode_status rhs_t(kanode_handle* h, const T* p, const T* u, T* du, int64_t B, 
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;
     const WsLayout wl = ws_layout(h, B);
+    if (surrogate_pair(h)) {   // two launches: wide-in partials -> wide-out summing them itself
+        T* ps = ws + wl.pslab;
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st));
+        HIP_TRY(h, kan::launch_kd_fwd_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, du, B, st, ps,
+                                                  kan::widein_chunks(h->hlc[0])));
+        return KANODE_OK;
+    }
     const T* cur = u;
     for (int l = 0; l < h->n_layers; ++l) {
         T* out = (l == h->n_layers - 1) ? du : ws + ((l % 2) ? wl.g1 : wl.g0);
@@ -415,6 +435,18 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
     if (s != KANODE_OK) return s;
     T* ws = (T*)h->ws;
     const WsLayout wl = ws_layout(h, B);
+    if (surrogate_pair(h)) {
+        // four launches: wide-in partials; the wide-out pullback's dot products and parameter
+        // cotangents in one launch; its input cotangent; the wide-in pullback
+        T* ps = ws + wl.pslab;
+        T* hbar = ws + wl.g0;
+        const int nb = kan::widein_chunks(h->hlc[0]);
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st));
+        HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, lam, hbar, dp,
+                                                  ws + wl.wslab, B, st, ps, nb));
+        if (lamJ || dp) HIP_TRY(h, kan::launch_kd_vjp_widein<T>(h->hlc[0], h->dlc, p, u, hbar, lamJ, dp, B, st));
+        return KANODE_OK;
+    }
     // forward recompute, keeping every hidden layer's input
     const T* acts[KANODE_MAX_LAYERS];
     acts[0] = u;
@@ -734,7 +766,20 @@ kanode_status kanode_create(const kanode_spec* spec, kanode_handle** out) {
             }
         }
     }
-    h->slab_bytes = (size_t)kSlabBlocks * (size_t)std::max(h->max_layer_P, 1) * h->esize;
+    // per-block partial rows: the column-kernel VJPs need a layer's (an all-column chain's) P per row;
+    // the wide kernels keep their partials in the chain workspace; stage / error / table-VJP rows
+    // need at most kMaxGrid + 2 doubles
+    {
+        bool all_col = true;
+        int64_t col_P = 0;
+        for (int l = 0; l < h->n_layers; ++l) {
+            if (h->kind[l] == KIND_COL) col_P = std::max<int64_t>(col_P, layer_P(h->hlc[l]));
+            else all_col = false;
+        }
+        if (all_col) col_P = std::max<int64_t>(col_P, h->P);
+        const size_t row = std::max<size_t>((size_t)col_P * h->esize, (size_t)(kan::kMaxGrid + 2) * sizeof(double));
+        h->slab_bytes = (size_t)kSlabBlocks * row;
+    }
     if ((e = hipMalloc(&h->slab, h->slab_bytes)) != hipSuccess)
         return bail(fail(h, KANODE_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e)));
     *out = h;

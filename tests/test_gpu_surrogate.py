@@ -92,3 +92,31 @@ def test_surrogate_f32():
     y = hd.rhs(t(p, torch.float32), t(u, torch.float32))
     sc = chain_scale(specs, p.astype(np.float64), u.astype(np.float64))
     assert_close(y, O.chain_fwd(specs, p, u), sc, RTOL[torch.float32], "y f32")
+
+
+@pytest.mark.parametrize("N,G,B", [(512, 5, 1), (2048, 10, 8), (300, 7, 11)])
+def test_surrogate_pair_launches_equal_layer_by_layer(N, G, B):
+    """KAN [N, 10, N]: the fused chain path (wide-out reading the wide-in chunk partials; merged
+    dot + parameter launch) is bitwise equal to the layer-by-layer calls through
+    kanode_layer_forward / kanode_layer_vjp, which materialise the hidden layer."""
+    rng = np.random.default_rng(N * G + B)
+    specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+    p = t(_glorot_params(rng, specs))
+    u = t(rng.uniform(-1, 1, (B, N)))
+    lam = t(rng.normal(size=(B, N)))
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=torch.float64, rhs_kind="chain", device=device())
+    P0 = hd.layers[0].param_length
+    p0, p1 = p[:P0].contiguous(), p[P0:].contiguous()
+    h = hd.layer_forward(0, p0, u)
+    y_ref = hd.layer_forward(1, p1, h)
+    assert torch.equal(hd.rhs(p, u), y_ref)
+    hbar, pb1 = hd.layer_vjp(1, p1, h, lam)
+    xbar, pb0 = hd.layer_vjp(0, p0, u, hbar)
+    lamJ, dp = hd.vjp(p, u, lam)
+    assert torch.equal(lamJ, xbar)
+    assert torch.equal(dp, torch.cat([pb0, pb1]))
+    # the VJP without λᵀJ (dp only) and without dp (λᵀJ only)
+    lamJ2, _ = hd.vjp(p, u, lam, accumulate_dp=False)
+    assert torch.equal(lamJ2, xbar)
+    _, dp2 = hd.vjp(p, u, lam, want_lamJ=False)
+    assert torch.equal(dp2, dp)
