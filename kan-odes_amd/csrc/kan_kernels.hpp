@@ -279,7 +279,22 @@ template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
                                  T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab = nullptr,
                                  int xnblk = 0);
-inline int widein_chunks(const LayerConst& h) { return (h.I + 63) / 64; }
+// inputs per block of the wide-in forward (kd_fwd_widein_co_kernel: at most kWIMaxV C and kWIMaxW W
+// entries per thread of 256) and its chunk count
+constexpr int kWideInMaxInputs = 64;
+constexpr int kWIMaxV = 32;
+constexpr int kWIMaxW = 8;
+__host__ __device__ inline int widein_cw(int O, int G) {
+    const int tn = (256 / O) * O;
+    int cw = (kWIMaxV * tn) / (O * G);
+    if (cw > kWideInMaxInputs) cw = kWideInMaxInputs;
+    if (cw * O > kWIMaxW * tn) cw = (kWIMaxW * tn) / O;
+    return cw < 1 ? 1 : cw;
+}
+inline int widein_chunks(const LayerConst& h) {
+    const int cw = widein_cw(h.O, h.G);
+    return (h.I + cw - 1) / cw;
+}
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
                                 T* pbar, int64_t K, hipStream_t st);

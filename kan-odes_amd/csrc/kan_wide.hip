@@ -7,17 +7,18 @@
 //
 // The batch is a handful of trajectories, so the kernels spread each column over many
 // workgroups instead of looping over the columns in a few:
-//   wide-in  (I·G large, O <= 16): grid (input chunk of 64, column); lane i evaluates the
-//            basis of its input and its partial y[o]; a wave sum per o gives the chunk's
-//            partial (slab), then an ordered reduction over the chunks.
+//   wide-in  (I·G large, O <= 16): grid (input chunk, column); the chunk's C and W blocks are
+//            contiguous and read with coalesced loads (thread t meets output t mod O), the
+//            chunk's basis values staged in LDS meanwhile; per-output partials (slab), then an
+//            ordered reduction over the chunks.
 //   wide-out (O large): grid (row chunk of 256, column tile of 8); the block stages the
 //            small basis of its tile in LDS; C[o + O*c] reads are coalesced over o.
 // Pullbacks: wide-out parameters -- thread o owns dC[o, :], dW[o, :] (no reduction);
 // wide-out input cotangent -- one workgroup per (input i, basis row r, column tile) forms
 // Σ_o C[o, r + G i] ȳ[o, k] (coalesced over o, ordered block sum) into a slab, then one
 // thread per (i, k) turns the G + 1 sums into x̄[i, k];
-// wide-in -- lane i owns dC[:, g + G i], dW[:, i] (accumulated in its own LDS slots over
-// the columns) and x̄[i, :].  Every reduction runs in a fixed order (bitwise reproducible).
+// wide-in -- one block per input chunk owns the chunk's dC, dW entries (coalesced, columns summed
+// in order), other blocks form x̄ per column (one thread per basis slot, then per input).  Every reduction runs in a fixed order (bitwise reproducible).
 // Surrogate chain [wide-in, wide-out]: the wide-out kernels can take their input as the
 // wide-in layer's chunk partials (`xslab`), each block summing what it needs in the order of
 // kd_widein_reduce_kernel, so the chain RHS is two launches and its VJP four, bitwise equal to
@@ -60,66 +61,7 @@ struct Basis1 {
 };
 
 // ---------------------------------------------------------------------------
-// wide-in forward: grid (ceil(I/64), columns); slab[(chunk*K + k)*O + o] = Σ_{i in chunk} (C φ + W sw)
-constexpr int kWIB = 64;   // inputs per wide-in workgroup (one per lane)
-constexpr int kSW = 4;     // waves per workgroup splitting the inner loop (latency: more loads in flight)
-template <typename T, int PATH>
-__global__ void __launch_bounds__(kWIB * kSW)
-kd_fwd_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                     T* __restrict__ slab, int64_t K) {
-    __shared__ T red[kSW][kOWide];
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
-    const LayerConst& lc = *lcp;
-    const int I = lc.I, O = lc.O, G = lc.G;
-    const T* __restrict__ C = p + lc.p_off;
-    const T* __restrict__ W = p + lc.w_off;
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const int i = blockIdx.x * kWIB + lane;
-    const bool valid = i < I;
-    for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
-        // wave w takes the knots g ≡ w (mod kSW); the base term goes to wave G mod kSW
-        T acc[kOWide];
-#pragma unroll
-        for (int o = 0; o < kOWide; ++o) acc[o] = T(0);
-        if (valid) {
-            const T xi = x[(int64_t)I * k + i];
-            Basis1<T, PATH> bs;
-            bs.init(M, lc, xi);
-            for (int g = 0; g < G; ++g) {
-                T z, aux;
-                const T phi = bs.next(M, lc, g, z, aux);
-                if ((g % kSW) != w) continue;
-                const T* Cc = C + (int64_t)O * (g + (int64_t)G * i);
-#pragma unroll
-                for (int o = 0; o < kOWide; ++o)
-                    if (o < O) acc[o] = kfma<T>(Cc[o], phi, acc[o]);
-            }
-            if (lc.use_base && w == G % kSW) {
-                const T sw = swish<T>(M, xi);
-                const T* Wi = W + (int64_t)O * i;
-#pragma unroll
-                for (int o = 0; o < kOWide; ++o)
-                    if (o < O) acc[o] = kfma<T>(Wi[o], sw, acc[o]);
-            }
-        }
-#pragma unroll
-        for (int o = 0; o < kOWide; ++o) {
-            if (o < O) {
-                const T sum = wave_sum(acc[o]);
-                if (lane == 0) red[w][o] = sum;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < O) {
-            T sum = red[0][threadIdx.x];
-#pragma unroll
-            for (int v = 1; v < kSW; ++v) sum += red[v][threadIdx.x];
-            slab[((int64_t)blockIdx.x * K + k) * O + threadIdx.x] = sum;
-        }
-        __syncthreads();
-    }
-}
+constexpr int kSW = 4;     // waves per wide-out workgroup splitting the inner loop (latency: more loads in flight)
 
 // Element x[i, k] of a layer input [I, K]: from x, or (xslab != nullptr) the ordered sum over the
 // nblk chunk partials of the wide-in layer that produced it, xslab[(b*K + k)*I + i] -- the order
@@ -143,6 +85,75 @@ __device__ __forceinline__ T layer_in(const T* __restrict__ x, const T* __restri
             if (b0 + j < nblk) s += v[j];
     }
     return s;
+}
+
+// wide-in forward, coalesced: grid (chunks of cw inputs, columns), 256 threads.  The chunk's C
+// block (O·G·cw doubles) and W block (O·cw) are contiguous in the ComponentArray vector
+// (C[o + O(g + G i)], W[o + O i]); thread t takes the entries t + m·Tn, Tn = ⌊256/O⌋·O, so every
+// load instruction reads a contiguous run and thread t always meets output o = t mod O.  The C
+// and W loads are issued before the chunk's basis values are staged in LDS (by the first cw
+// threads), so their latency overlaps the exponentials.  Per-thread partials are summed per
+// output in thread order: slab[(chunk*K + k)*O + o].
+template <typename T>
+__global__ void __launch_bounds__(256)
+kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                        T* __restrict__ slab, int64_t K) {
+    __shared__ T phiL[kWideInMaxInputs * kMaxGrid];
+    __shared__ T swL[kWideInMaxInputs];
+    __shared__ T red[256];
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<T> M{tab};
+    const LayerConst& lc = *lcp;
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const int cw = widein_cw(O, G);
+    const int i0 = blockIdx.x * cw;
+    const int ni = I - i0 < cw ? I - i0 : cw;
+    const int tn = (256 / O) * O, t = threadIdx.x;
+    const int nf = O * G * ni, nw = lc.use_base ? O * ni : 0;
+    const T* __restrict__ Cb = p + lc.p_off + (int64_t)O * G * i0;
+    const T* __restrict__ Wb = p + lc.w_off + (int64_t)O * i0;
+    const int c0 = t / O, cs = tn / O;   // entry t + m·tn belongs to basis slot c0 + m·cs
+    for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+        T cv[kWIMaxV], wv[kWIMaxW];
+#pragma unroll
+        for (int m = 0; m < kWIMaxV; ++m) {
+            const int f = t + m * tn;
+            cv[m] = t < tn && f < nf ? Cb[f] : T(0);
+        }
+#pragma unroll
+        for (int m = 0; m < kWIMaxW; ++m) {
+            const int f = t + m * tn;
+            wv[m] = t < tn && f < nw ? Wb[f] : T(0);
+        }
+        // one thread per basis slot c = g + G i (direct formula: no per-input knot chain)
+        for (int c = t; c < ni * G; c += blockDim.x) {
+            const int i = c / G, g = c - i * G;
+            const T xi = x[(int64_t)I * k + i0 + i];
+            const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
+            T aux = T(0);
+            phiL[c] = basis_direct<T>(M, lc.basis, (n - T(lc.grid[g])) * T(lc.invh), aux);
+            if (g == 0) swL[i] = lc.use_base ? swish<T>(M, xi) : T(0);
+        }
+        __syncthreads();
+        T acc = T(0);
+        if (t < tn) {
+#pragma unroll
+            for (int m = 0; m < kWIMaxV; ++m)
+                if (t + m * tn < nf) acc = kfma<T>(cv[m], phiL[c0 + m * cs], acc);
+#pragma unroll
+            for (int m = 0; m < kWIMaxW; ++m)
+                if (t + m * tn < nw) acc = kfma<T>(wv[m], swL[c0 + m * cs], acc);
+        }
+        red[t] = acc;
+        __syncthreads();
+        if (t < O) {
+            T sum = red[t];
+#pragma unroll 8
+            for (int q = 1; q < cs; ++q) sum += red[t + q * O];
+            slab[((int64_t)blockIdx.x * K + k) * O + t] = sum;
+        }
+        __syncthreads();
+    }
 }
 
 // y[o + O*k] = Σ_b slab[(b*K + k)*O + o]   (ordered over b)
@@ -411,99 +422,142 @@ kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restri
 }
 
 // ---------------------------------------------------------------------------
-// wide-in pullback, grid (ceil(I/64), np + nx), lane = input i:
-//   blockIdx.y <  np (= O when pbar): row o = blockIdx.y; lane i owns dC[o, g + G i] (g < G)
-//                  and dW[o, i] in registers, the kSW waves taking every kSW-th column; the
-//                  wave partials are summed in order through LDS and added to pbar once;
-//   blockIdx.y >= np: wave w forms x̄[i, k] for the columns k = (y - np)·kSW + w (stride
-//                  nx·kSW): the G + 1 dot products Σ_o C[o, g + G i] ȳ[o, k] (O <= 16,
-//                  registers) then the basis / normalizer / swish rrules.
-template <typename T, int PATH>
-__global__ void __launch_bounds__(kWIB * kSW)
-kd_vjp_widein_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                     const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
-                     int nx) {
-    __shared__ T red[kSW][kWIB];
+// wide-in pullback, grid (chunks of cw inputs as the forward, np + nxg), 256 threads:
+//   blockIdx.y <  np (np = O with pbar): output o = y's parameter cotangents of the chunk over all
+//          columns, dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k), dW[o, i] += Σ_k ȳ[o, k] swish(x_ik), one
+//          thread per basis slot (direct formula), columns summed in order, pbar written once;
+//   blockIdx.y >= np: x̄ of the columns k ≡ y - np (mod nxg): the chunk's basis values in LDS,
+//          one thread per basis slot c = g + G i forms Σ_o C[o, c] ȳ[o, k] and its rrule term,
+//          then one thread per input sums them over g (the order of the reference pullback).
+template <typename T>
+__global__ void __launch_bounds__(256)
+kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                        const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
+                        int nxg, int cw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wv_raw[];
+    T* L = reinterpret_cast<T*>(wv_raw);
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
-    const T* __restrict__ C = p + lc.p_off;
-    const T* __restrict__ W = p + lc.w_off;
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    const int i = blockIdx.x * kWIB + lane;
-    const bool valid = i < I;
+    
+    const int i0 = blockIdx.x * cw;
+    const int ni = I - i0 < cw ? I - i0 : cw;
+    const int t = threadIdx.x;
     const bool base = lc.use_base != 0;
+    const T invh = T(lc.invh);
     if ((int)blockIdx.y < np) {
+        // output o = blockIdx.y: dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k) for the chunk's basis slots c, basis
+        // by the direct formula; dW[o, i] += Σ_k ȳ[o, k] swish(x_ik).  With cw·G <= 128 the block's
+        // threads are nq = 256 / (cw·G) column lanes per slot (columns k ≡ q mod nq), summed over the
+        // lanes in order through LDS; otherwise one lane, slots t, t + 256, ...
         const int o = blockIdx.y;
-        T acc[kMaxGrid + 1];
+        const int nc = ni * G, ncp = cw * G;
+        const int nq = ncp <= 128 ? 256 / ncp : 1;
+        constexpr int kS = (kWideInMaxInputs * kMaxGrid + 255) / 256;
+        const int q = nq > 1 ? t / ncp : 0;
+        const int cb = nq > 1 ? t - q * ncp : t;
+        T dcv[kS], dwv[kS];
 #pragma unroll
-        for (int g = 0; g <= kMaxGrid; ++g) acc[g] = T(0);
-        if (valid) {
-            for (int64_t k = w; k < K; k += kSW) {
-                const T xi = x[(int64_t)I * k + i];
+        for (int m = 0; m < kS; ++m) dcv[m] = dwv[m] = T(0);
+        if (q < nq) {
+            for (int64_t k = q; k < K; k += nq) {
                 const T yb = ybar[(int64_t)O * k + o];
-                Basis1<T, PATH> bs;
-                bs.init(M, lc, xi);
 #pragma unroll
-                for (int g = 0; g < kMaxGrid; ++g) {
-                    if (g < G) {
-                        T z, aux;
-                        acc[g] = kfma<T>(yb, bs.next(M, lc, g, z, aux), acc[g]);
+                for (int m = 0; m < kS; ++m) {
+                    const int c = cb + 256 * m;
+                    if ((nq == 1 || m == 0) && c < nc) {
+                        const int i = c / G, g = c - i * G;
+                        const T xi = x[(int64_t)I * k + i0 + i];
+                        const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
+                        T aux = T(0);
+                        dcv[m] = kfma<T>(yb, basis_direct<T>(M, lc.basis, (n - T(lc.grid[g])) * invh, aux), dcv[m]);
+                        if (base && g == 0) dwv[m] = kfma<T>(yb, swish<T>(M, xi), dwv[m]);
                     }
                 }
-                if (base) acc[kMaxGrid] = kfma<T>(yb, swish<T>(M, xi), acc[kMaxGrid]);
             }
         }
-        T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
+        T* __restrict__ dC = pbar + lc.p_off + (int64_t)O * G * i0 + o;
+        if (nq == 1) {
 #pragma unroll
-        for (int g = 0; g <= kMaxGrid; ++g) {
-            if (g < G || (g == kMaxGrid && base)) {
-                __syncthreads();
-                red[w][lane] = acc[g];
-                __syncthreads();
-                if (w == 0 && valid) {
-                    T sum = red[0][lane];
-#pragma unroll
-                    for (int v = 1; v < kSW; ++v) sum += red[v][lane];
-                    if (g < G) dC[(int64_t)O * g] += sum;
-                    else pbar[lc.w_off + o + (int64_t)O * i] += sum;
+            for (int m = 0; m < kS; ++m) {
+                const int c = t + 256 * m;
+                if (c < nc) {
+                    dC[(int64_t)O * c] += dcv[m];
+                    if (base && c % G == 0) pbar[lc.w_off + (int64_t)O * (i0 + c / G) + o] += dwv[m];
+                }
+            }
+        } else {
+            T* red = L;           // [nq][ncp] slot partials, then [nq][cw] swish partials
+            T* redw = L + nq * ncp;
+            if (q < nq) {
+                red[t] = dcv[0];
+                if (cb < nc && cb % G == 0) redw[q * cw + cb / G] = dwv[0];
+            }
+            __syncthreads();
+            if (t < nc) {
+                T sum = red[t];
+                for (int r = 1; r < nq; ++r) sum += red[r * ncp + t];
+                dC[(int64_t)O * t] += sum;
+                if (base && t % G == 0) {
+                    T sw = redw[t / G];
+                    for (int r = 1; r < nq; ++r) sw += redw[r * cw + t / G];
+                    pbar[lc.w_off + (int64_t)O * (i0 + t / G) + o] += sw;
                 }
             }
         }
         return;
     }
-    if (!valid) return;
-    const T invh = T(lc.invh);
-    for (int64_t k = (int64_t)((int)blockIdx.y - np) * kSW + w; k < K; k += (int64_t)nx * kSW) {
-        T yb[kOWide];
-#pragma unroll
-        for (int o = 0; o < kOWide; ++o) yb[o] = o < O ? ybar[(int64_t)O * k + o] : T(0);
-        const T xi = x[(int64_t)I * k + i];
-        Basis1<T, PATH> bs;
-        bs.init(M, lc, xi);
-        T nbar = T(0);
-        for (int g = 0; g < G; ++g) {
-            T z, aux;
-            const T phi = bs.next(M, lc, g, z, aux);
-            const T* __restrict__ Cc = C + (int64_t)O * (g + (int64_t)G * i);
+    const int nc = ni * G;
+    T* phL = L;                  // [cw·G] basis values, arguments, aux, rrule terms
+    T* zL = phL + cw * G;
+    T* auL = zL + cw * G;
+    T* puL = auL + cw * G;
+    T* ybL = puL + cw * G;       // [O]
+    T* dnL = ybL + kOWide;       // [cw] N'(x_i)
+    T* dsL = dnL + cw;           // [cw] swish'(x_i)
+    const T* __restrict__ C = p + lc.p_off + (int64_t)O * G * i0;
+    const T* __restrict__ W = p + lc.w_off + (int64_t)O * i0;
+    for (int64_t k = (int64_t)blockIdx.y - np; k < K; k += nxg) {
+        __syncthreads();
+        for (int c = t; c < nc; c += blockDim.x) {
+            const int i = c / G, g = c - i * G;
+            const T xi = x[(int64_t)I * k + i0 + i];
+            const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
+            const T z = (n - T(lc.grid[g])) * invh;
+            T aux = T(0);
+            phL[c] = basis_direct<T>(M, lc.basis, z, aux);
+            zL[c] = z;
+            auL[c] = aux;
+            if (g == 0) {
+                dnL[i] = dnormalize<NORM_RUNTIME, T>(lc.norm, n);
+                if (base) {
+                    T sw, dsw;
+                    swish_and_grad<T>(M, xi, sw, dsw);
+                    dsL[i] = dsw;
+                }
+            }
+        }
+        if (t < O) ybL[t] = ybar[(int64_t)O * k + t];
+        __syncthreads();
+        for (int c = t; c < nc; c += blockDim.x) {
+            const T* __restrict__ Cc = C + (int64_t)O * c;
             T bb = T(0);
-#pragma unroll
-            for (int o = 0; o < kOWide; ++o)
-                if (o < O) bb = kfma<T>(Cc[o], yb[o], bb);
-            nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, bb) * invh;
+            for (int o = 0; o < O; ++o) bb = kfma<T>(Cc[o], ybL[o], bb);
+            puL[c] = basis_pull<T>(lc.basis, lc.iqf_quirk, zL[c], phL[c], auL[c], bb) * invh;
         }
-        T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
-        if (base) {
-            T sw, dsw;
-            swish_and_grad<T>(M, xi, sw, dsw);
-            T sb = T(0);
-#pragma unroll
-            for (int o = 0; o < kOWide; ++o)
-                if (o < O) sb = kfma<T>(W[(int64_t)O * i + o], yb[o], sb);
-            xb = xb + sb * dsw;
+        __syncthreads();
+        if (t < ni) {
+            T nbar = T(0);
+            for (int g = 0; g < G; ++g) nbar = nbar + puL[t * G + g];
+            T xb = nbar * dnL[t];
+            if (base) {
+                T sb = T(0);
+                for (int o = 0; o < O; ++o) sb = kfma<T>(W[(int64_t)O * t + o], ybL[o], sb);
+                xb = xb + sb * dsL[t];
+            }
+            xbar[(int64_t)I * k + i0 + t] = xb;
         }
-        xbar[(int64_t)I * k + i] = xb;
     }
 }
 
@@ -518,15 +572,9 @@ static inline unsigned col_tiles(int64_t K) {
 template <typename T>
 hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
                                 int64_t K, hipStream_t st) {
-    const int nblk = (h.I + kWIB - 1) / kWIB;
+    const int nblk = widein_chunks(h);
     const dim3 grid(nblk, (unsigned)(K < 65535 ? K : 65535));
-#define KAN_WI(PATH) hipLaunchKernelGGL((kd_fwd_widein_kernel<T, PATH>), grid, dim3(kWIB * kSW), 0, st, lc, p, x, slab, K)
-    switch (h.path) {
-    case PATH_REC_CORR: KAN_WI(PATH_REC_CORR); break;
-    case PATH_REC: KAN_WI(PATH_REC); break;
-    default: KAN_WI(PATH_DIRECT);
-    }
-#undef KAN_WI
+    hipLaunchKernelGGL((kd_fwd_widein_co_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !y) return e;   // y == nullptr: the consumer sums the slab itself
     const int64_t n = (int64_t)h.O * K;
@@ -578,20 +626,18 @@ hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, cons
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
                                 T* pbar, int64_t K, hipStream_t st) {
-    const int nblk = (h.I + kWIB - 1) / kWIB;
+    // few columns: the forward's chunks; many: chunks of <= 64 basis slots, so the parameter blocks
+    // spread the columns over 256 / (cw·G) >= 4 lanes per slot
+    const int cw = K > 8 ? (64 / h.G > 1 ? 64 / h.G : 1) : widein_cw(h.O, h.G);
+    const int nblk = (h.I + cw - 1) / cw;
     const int np = pbar ? h.O : 0;
-    const int64_t kc = K < 4096 ? K : 4096;
-    const int nx = xb ? (int)((kc + kSW - 1) / kSW) : 0;
-    if (np + nx == 0) return hipSuccess;
-    const dim3 grid(nblk, np + nx);
-#define KAN_WIV(PATH)                                                                                              \
-    hipLaunchKernelGGL((kd_vjp_widein_kernel<T, PATH>), grid, dim3(kWIB * kSW), 0, st, lc, p, x, yb, xb, pbar, K, np, nx)
-    switch (h.path) {
-    case PATH_REC_CORR: KAN_WIV(PATH_REC_CORR); break;
-    case PATH_REC: KAN_WIV(PATH_REC); break;
-    default: KAN_WIV(PATH_DIRECT);
-    }
-#undef KAN_WIV
+    const int nxg = xb ? (int)(K < 4096 ? K : 4096) : 0;
+    if (np + nxg == 0) return hipSuccess;
+    const dim3 grid(nblk, np + nxg);
+    size_t lds = (size_t)4 * cw * h.G + kOWide + 2 * (size_t)cw;   // x̄ blocks
+    lds = sizeof(T) * (lds > 512 ? lds : 512);                         // parameter blocks' lane sums
+    hipLaunchKernelGGL((kd_vjp_widein_co_kernel<T>), grid, dim3(256), lds, st, lc, p, x, yb, xb, pbar, K, np, nxg,
+                       cw);
     return hipGetLastError();
 }
 

@@ -248,7 +248,7 @@ int64_t wide_slab_elems(const kanode_handle* h, int64_t B) {
     int64_t m = 0;
     for (int l = 0; l < h->n_layers; ++l) {
         const LayerConst& c = h->hlc[l];
-        if (h->kind[l] == KIND_WIDE_IN) m = std::max<int64_t>(m, (int64_t)((c.I + 63) / 64) * B * c.O);
+        if (h->kind[l] == KIND_WIDE_IN) m = std::max<int64_t>(m, (int64_t)kan::widein_chunks(c) * B * c.O);
         if (h->kind[l] == KIND_WIDE_OUT) m = std::max<int64_t>(m, (int64_t)c.I * (c.G + 1) * B);
     }
     return m;
