@@ -149,6 +149,10 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     adjoint stage / one-launch adjoint step (0 = occupancy-derived).
  *     Tuning only: the grid fixes the order of the dp reduction, so gradients are
  *     bitwise reproducible for a given grid, not across grids.
+ *   KANODE_OPT_ADJ_STEP_ROWS (default 1): the one-launch Fisher-KPP adjoint step keeps each
+ *     trajectory row's stage values in the registers of one wave (batches up to 8192 rows
+ *     of <= 256 points, GRID_ADJ_STEP unset); 0 = the persistent-grid step kernel, whose
+ *     stages pass kλ through memory.  Same λᵀJ and λ bitwise; dp to the reduction order.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -158,7 +162,8 @@ typedef enum {
     KANODE_OPT_FUSED_SOLVE_CAP = 4,
     KANODE_OPT_GRID_RHS = 5,
     KANODE_OPT_GRID_VJP = 6,
-    KANODE_OPT_GRID_ADJ_STEP = 7
+    KANODE_OPT_GRID_ADJ_STEP = 7,
+    KANODE_OPT_ADJ_STEP_ROWS = 8
 } kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);

@@ -59,6 +59,7 @@ hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, h
 // occupancy-derived default).  Tuning sweeps only: the grid fixes the dp reduction order.
 struct GridOverride {
     int rhs = 0, vjp = 0, vstep = 0;
+    bool vstep_rows = true;   // KANODE_OPT_ADJ_STEP_ROWS
 };
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
                               double* tables, const int* fns, int nfn, hipStream_t st);
@@ -113,11 +114,12 @@ struct AdjStepArgs {
     double* lam_out;
     double* slab[6];           // per stage: [grid][P] moment rows
     double* err_slab;          // [grid] (null: no error)
+    int32_t reload[6];         // (set by the launcher) stage s reads u_i, Q_m other than stage s-1's
 };
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
-                                 hipStream_t st, bool build, int grid_ovr = 0);
+                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true);
 constexpr int kMaxFinishJobs = 8;
 struct FinishJob {
     const double* slab;

@@ -1055,6 +1055,188 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
     }
 }
 
+// The same adjoint step with one trajectory row per wave and the row's stage values in registers
+// (batches up to 4 rows x the slab's blocks; fk_vjp_step_pp_wave_kernel beyond).  The wave keeps
+// λ, kλ_1..kλ_6 and the dense-output arrays u_i, Q_1..Q_4 of its row across the six stages, so a
+// step reads λ, kλ_1 and the dense output once (again only when a stage falls in another forward
+// step: a.reload) and writes λ_new and kλ_7: 7 to 12 state passes per step instead of ~58.  The
+// per-point arithmetic is fk_vjp_step_pp_wave_kernel's, statement for statement (λᵀJ, λ_new and
+// kλ_7 bitwise equal); the moment partials are block-summed per stage into the same slab rows
+// (the grid differs, so dp differs from that kernel in the last bits of the reduction order).
+#ifndef KAN_VROWS_WPE
+#define KAN_VROWS_WPE 2
+#endif
+#ifndef KAN_VROWS_SB
+#define KAN_VROWS_SB 1
+#endif
+#ifndef KAN_VROWS_NORED
+#define KAN_VROWS_NORED 0
+#endif
+template <int NORM, int PATH, int GT, int NP>
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
+fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                        const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
+                        int64_t B, AdjStepArgs a) {
+    constexpr int Nx = 128 * NP;
+    extern __shared__ double2 tl[];
+    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6);
+    const bool live = b < B;
+    const int64_t rb = (live ? b : 0) * Nx + 2 * lane;
+    // the row's loads are in flight while the block stages its tables
+    kd2 lam0[NP], kl[6][NP], ui[NP], qi[4][NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        lam0[k] = kd2{0.0, 0.0};
+        kl[0][k] = kd2{0.0, 0.0};
+        ui[k] = kd2{0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) qi[m][k] = kd2{0.0, 0.0};
+    }
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            lam0[k] = ld_vstep(a.lam + rb + 128 * k);
+            kl[0][k] = ld_vstep(a.kl[0] + rb + 128 * k);
+            ui[k] = ld_vstep(a.su_u[0] + rb + 128 * k);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[0][m] + rb + 128 * k);
+        }
+    }
+    const int tsz = (kPPCoef / 2) * ni;
+    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
+        tl[i] = tables[PP_DPHI * tsz + i];
+        tl[tsz + i] = tables[PP_SWISH * tsz + i];
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<double> M{tab};
+    const double2* __restrict__ td = tl;
+    const double2* __restrict__ ts = tl + tsz;
+    const LayerConst& lc = *lcp;
+    const RecScalars<double> rc(lc);
+    const int P = GT + (lc.use_base ? 1 : 0);
+    double eacc = 0.0;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        double S0[GT];
+        float S1[GT], S2[GT];
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            S0[j] = 0.0;
+            S1[j] = S2[j] = 0.0f;
+        }
+        double dW = 0.0;
+        const bool last = s == 5;
+        const bool want_err = last && a.err_slab != nullptr;
+        if (live) {
+            if (s > 0 && a.reload[s]) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    ui[k] = ld_vstep(a.su_u[s] + rb + 128 * k);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[s][m] + rb + 128 * k);
+                }
+            }
+            kd2 uv[NP], lv[NP], ev[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {   // u(t_s) = u_i + Σ_m θ^m Q_m
+                kd2 t{0.0, 0.0};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    t.x = ::fma(a.su_c[s][m], qi[m][k].x, t.x);
+                    t.y = ::fma(a.su_c[s][m], qi[m][k].y, t.y);
+                }
+                uv[k].x = ::fma(1.0, t.x, ui[k].x);
+                uv[k].y = ::fma(1.0, t.y, ui[k].y);
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {   // λs = λ + Σ_{j<=s} h a_sj kλ_j (and the error sum)
+                kd2 t{0.0, 0.0}, e{0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j <= s; ++j) {
+                    const double c = a.a[s][j], ce = a.ec[j];
+                    t.x = ::fma(c, kl[j][k].x, t.x);
+                    t.y = ::fma(c, kl[j][k].y, t.y);
+                    if (want_err) {
+                        e.x = ::fma(ce, kl[j][k].x, e.x);
+                        e.y = ::fma(ce, kl[j][k].y, e.y);
+                    }
+                }
+                lv[k].x = ::fma(1.0, t.x, lam0[k].x);
+                lv[k].y = ::fma(1.0, t.y, lam0[k].y);
+                ev[k] = e;
+            }
+            if (last && a.lam_out) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + 128 * k, lv[k]);
+            }
+            double rr[NP], rl[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                rr[k] = wave_ror1(lv[k].y);
+                rl[k] = wave_rol1(lv[k].x);
+            }
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+                const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+                double a0, a1;
+                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, a0, a1);
+#if KAN_VROWS_SB
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].x, lv[k].x,
+                                                               S0, S1, S2, dW);
+#if KAN_VROWS_SB
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].y, lv[k].y,
+                                                               S0, S1, S2, dW);
+                kd2 o;
+                o.x = a0 + x0b;
+                o.y = a1 + x1b;
+                if (!last) {
+                    kl[s + 1 < 6 ? s + 1 : 5][k] = o;
+                } else {
+                    st_vstep(a.kl[6] + rb + 128 * k, o);
+                    if (want_err) {
+                        const double en = a.ec[6];
+                        const double ex = ::fma(en, o.x, ev[k].x), ey = ::fma(en, o.y, ev[k].y);
+                        const double sx = ::fma(a.reltol, fmax(kabs(lam0[k].x), kabs(lv[k].x)), a.abstol);
+                        const double sy = ::fma(a.reltol, fmax(kabs(lam0[k].y), kabs(lv[k].y)), a.abstol);
+                        const double rx = ex / sx, ry = ey / sy;
+                        eacc = ::fma(rx, rx, eacc);
+                        eacc = ::fma(ry, ry, eacc);
+                    }
+                }
+            }
+        }
+        double acc[GT + 1];
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            const double e = lc.e[j];
+            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+                                           : lc.K[j] * S0[j];
+        }
+        acc[GT] = dW;
+#if KAN_VROWS_NORED   // timing experiment only: no moment reduction (wrong dp)
+        {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j <= GT; ++j) t += acc[j];
+            if (threadIdx.x == 0) a.slab[s][(int64_t)blockIdx.x * P] = t;
+        }
+#else
+        block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+#endif
+    }
+    if (a.err_slab) {
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, a.err_slab + blockIdx.x);
+    }
+}
+
 // dp[q] (= or +=) Σ_b slab[b·P + q] for q < P (block q), and err_out[0] = Σ_b err_slab[b]
 // (block P): the adjoint stage's reductions in one launch, fixed order.
 __global__ void __launch_bounds__(kBlock)
@@ -1587,7 +1769,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
-                                 int* grid_out, hipStream_t st, bool build, int grid_ovr) {
+                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1596,8 +1778,24 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     const int P = hlc.G + (hlc.use_base ? 1 : 0);
     AdjStepArgs a = a_in;
     int grid = 0;
+    // one row per wave, the row's stages in registers, where the grid of one row per wave fits the slab
+    const bool use_rows = rows && grid_ovr == 0 && Nx <= 256 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks;
+    a.reload[0] = 1;
+    for (int s = 1; s < 6; ++s) {
+        bool same = a.su_u[s] == a.su_u[s - 1];
+        for (int m = 0; m < 4; ++m) same = same && a.su_q[s][m] == a.su_q[s - 1][m];
+        a.reload[s] = same ? 0 : 1;
+    }
 #define KAN_VSTEP(NORM, PATH, GT, NP)                                                                              \
     do {                                                                                                         \
+        if (use_rows) {                                                                                          \
+            grid = grid_for(B, kVjpBlock / kWave, slab_blocks);                                                  \
+            for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
+            if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
+            hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2)>), dim3(grid), dim3(kVjpBlock), lds, st, \
+                               lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, B, a);          \
+            break;                                                                                               \
+        }                                                                                                        \
         static int cap = 0;                                                                                      \
         if (!cap) cap = pp_grid_cap(fk_vjp_step_pp_wave_kernel<NORM, PATH, GT, NP>, lds, kVjpBlock);             \
         const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \

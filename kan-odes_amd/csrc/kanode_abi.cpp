@@ -861,6 +861,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_GRID_RHS: return count(h->grid_ovr.rhs, "GRID_RHS", 1 << 24);
     case KANODE_OPT_GRID_VJP: return count(h->grid_ovr.vjp, "GRID_VJP", kSlabBlocks / 2);
     case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
+    case KANODE_OPT_ADJ_STEP_ROWS: return flag(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -875,6 +876,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_GRID_RHS: return h->grid_ovr.rhs;
     case KANODE_OPT_GRID_VJP: return h->grid_ovr.vjp;
     case KANODE_OPT_GRID_ADJ_STEP: return h->grid_ovr.vstep;
+    case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows ? 1 : 0;
     }
     return -1;
 }
@@ -1132,7 +1134,8 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
     int grid = 0;
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                           (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
-                                          table_build(h, h->built_vjp), h->grid_ovr.vstep));
+                                          table_build(h, h->built_vjp), h->grid_ovr.vstep,
+                                          h->grid_ovr.vstep_rows));
     kan::FinishJobs jobs{};
     double* base = (double*)h->step_slab;
     for (int s = 0; s < 6; ++s) {

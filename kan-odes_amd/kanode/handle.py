@@ -156,7 +156,7 @@ class KanodeHandle:
 
     def set_option(self, name: str, value: int) -> None:
         """kanode_set_option by name (see include/kanode.h: pointwise_table, fused_step, fused_solve,
-        fused_solve_cap, grid_rhs, grid_vjp, grid_adj_step)."""
+        fused_solve_cap, grid_rhs, grid_vjp, grid_adj_step, adj_step_rows)."""
         if name not in L.OPTIONS:
             raise KeyError(f"unknown option {name!r}; known: {sorted(L.OPTIONS)}")
         L.check(L.lib().kanode_set_option(self._h, L.OPTIONS[name], int(value)), self._h, "kanode_set_option")

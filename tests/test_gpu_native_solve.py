@@ -468,6 +468,57 @@ def test_fused_fk_step_several_rows_per_wave(nx):
     assert (gu1 - gud).abs().max().item() <= 1e-13 * gud.abs().max().item()
 
 
+def _solve_grad(rhs, u0, p0, tspan, ts, opt, **opts):
+    w = t(np.random.default_rng(13).normal(size=(len(ts),) + tuple(u0.shape)))
+    with rhs.hd.options(**opts):
+        p = p0.clone().requires_grad_(True)
+        x0 = u0.clone().requires_grad_(True)
+        sol = kanode.solve(rhs, x0, tspan, p, ts, opt, sensealg="interpolating_adjoint")
+        g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+    return sol, g, gu
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+@pytest.mark.parametrize("nx,B", [(128, 6), (256, 6), (256, 37)])
+def test_adjoint_step_rows_kernel_matches_persistent_grid(nx, B, adaptive):
+    """The adjoint step with one row per wave and the row's stage values in registers
+    (fk_vjp_step_rows_kernel, the default up to 8192 rows of <= 256 points) against the
+    persistent-grid step kernel that passes kλ through memory (KANODE_OPT_ADJ_STEP_ROWS = 0).
+    B = 6 and 37 leave idle waves in the last block.  At a fixed step λ (dL/du0) is bitwise equal
+    (the stage arithmetic is the same, statement for statement) and dL/dp equal to the reduction
+    order.  Adaptive runs put adjoint stages in other forward steps than their step's first stage
+    (the dense-output reload) and take their step sizes from the [λ; μ] error norm."""
+    rhs = _fk_cfg(nx, 10, "softsign")
+    u0 = t(fk_u0(nx, B, 5))
+    p0 = t(np.random.default_rng(11).uniform(-1.0, 1.0, 11))
+    if adaptive:
+        tspan, ts, opt = (0.0, 0.6), [0.0, 0.2, 0.45, 0.6], kanode.Tsit5Options(abstol=1e-10, reltol=1e-9)
+    else:
+        tspan, ts = (0.0, 0.1), [0.0, 0.05, 0.1]
+        opt = kanode.Tsit5Options(adaptive=False, dt=5e-4 * (256 / nx) ** 2)
+    s1, g1, gu1 = _solve_grad(rhs, u0, p0, tspan, ts, opt)
+    s0, g0, gu0 = _solve_grad(rhs, u0, p0, tspan, ts, opt, adj_step_rows=0)
+    assert torch.equal(s1.u, s0.u)
+    assert abs(s1.stats["adjoint"]["naccept"] - s0.stats["adjoint"]["naccept"]) <= (1 if adaptive else 0)
+    assert (g1 - g0).abs().max().item() <= 1e-12 * g0.abs().max().item()
+    if adaptive:
+        assert (gu1 - gu0).abs().max().item() <= 1e-10 * gu0.abs().max().item()
+    else:
+        assert torch.equal(gu1, gu0)
+
+
+def test_adjoint_step_rows_kernel_batch_cap():
+    """Above 8192 rows (4 rows x the 2048 slab blocks) the adjoint step falls back to the
+    persistent-grid kernel: both settings of KANODE_OPT_ADJ_STEP_ROWS then run the same kernel."""
+    rhs = _fk_cfg(128, 10, "softsign")
+    u0 = t(np.tile(fk_u0(128, 16, 6), (513, 1)))    # 8208 rows
+    p0 = t(np.random.default_rng(12).uniform(-1.0, 1.0, 11))
+    opt = kanode.Tsit5Options(adaptive=False, dt=2e-3)
+    s1, g1, gu1 = _solve_grad(rhs, u0, p0, (0.0, 0.006), [0.0, 0.006], opt)
+    s0, g0, gu0 = _solve_grad(rhs, u0, p0, (0.0, 0.006), [0.0, 0.006], opt, adj_step_rows=0)
+    assert torch.equal(s1.u, s0.u) and torch.equal(g1, g0) and torch.equal(gu1, gu0)
+
+
 @pytest.mark.parametrize("norm,basis", [("sigmoid", "rbf"), ("softsign", "rswaf")])
 def test_qform_forward_with_per_stage_adjoint(norm, basis):
     """Table-path configurations the fused adjoint step does not cover (fk_vjp_pp_supported false:
@@ -487,6 +538,7 @@ def test_options_round_trip_and_reject_bad_values():
     hd = rhs.hd
     assert hd.get_option("fused_step") == 1 and hd.get_option("fused_solve") == 1
     assert hd.get_option("grid_rhs") == hd.get_option("grid_vjp") == hd.get_option("grid_adj_step") == 0
+    assert hd.get_option("adj_step_rows") == 1
     with hd.options(fused_step=0, grid_vjp=7):
         assert hd.get_option("fused_step") == 0 and hd.get_option("grid_vjp") == 7
     assert hd.get_option("fused_step") == 1 and hd.get_option("grid_vjp") == 0
