@@ -61,19 +61,101 @@ template <typename T> __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-// Sum `n` (<= N) per-thread values across the block into out[0..n): wave
-// shuffles, then the wave partials summed in wave order (fixed order, so the
-// result is bitwise reproducible).  `red` is LDS of >= (blockDim/64)*N elements.
+// Wave reduce-scatter of M values per lane (recursive halving): at lane offset OFF the lanes with
+// that bit set keep the upper half of their slots and the others the lower half, each adding its
+// partner's copy, so the exchange count halves with every step (N = 11: 14 exchanges instead of
+// 6 x 11 shuffles).  Lane-local (base, cnt): the lane's slots hold the global values
+// [base, base + cnt).  Once one slot is left, the remaining offsets are a plain butterfly (a + b and
+// b + a: the same bits on both lanes).  No LDS: OFF = 32 / 16 exchange halves / rows with
+// v_permlane32_swap / v_permlane16_swap (gfx950), which also do the keep/send selection; OFF = 8, 4,
+// 2, 1 pair lanes inside a 16-lane row with DPP row_mirror, row_half_mirror and quad perms (each an
+// involution that pairs lanes differing in bit OFF).
+__device__ __forceinline__ void perm_swap32(double& x, double& y) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
+    x = __hiloint2double((int)hi[0], (int)lo[0]);
+    y = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void perm_swap16(double& x, double& y) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
+    x = __hiloint2double((int)hi[0], (int)lo[0]);
+    y = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void perm_swap32(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(y), false, false);
+    x = __int_as_float((int)r[0]);
+    y = __int_as_float((int)r[1]);
+}
+__device__ __forceinline__ void perm_swap16(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(y), false, false);
+    x = __int_as_float((int)r[0]);
+    y = __int_as_float((int)r[1]);
+}
+template <int OFF, typename T> __device__ __forceinline__ T row_partner(T v) {
+    static_assert(OFF == 8 || OFF == 4 || OFF == 2 || OFF == 1, "row-local partner");
+    return dpp_mov<OFF == 8 ? 0x140 : OFF == 4 ? 0x141 : OFF == 2 ? 0x4E : 0xB1>(v);
+}
+template <typename T, int M, int OFF>
+__device__ __forceinline__ void rs_step(T (&w)[16], int lane, int& base, int& cnt) {
+    if constexpr (OFF > 0) {
+        if constexpr (M == 1) {
+            static_assert(OFF <= 8, "N >= 3 keeps two slots past the cross-row steps");
+            w[0] = w[0] + row_partner<OFF>(w[0]);
+            rs_step<T, 1, OFF / 2>(w, lane, base, cnt);
+        } else {
+            constexpr int H = (M + 1) / 2;
+            const bool hi = (lane & OFF) != 0;
+#pragma unroll
+            for (int i = 0; i < H; ++i) {
+                T a = w[i];
+                T b = i + H < M ? w[i + H] : T(0);
+                if constexpr (OFF >= 16) {
+                    // x = [own a | partner's b], y = [partner's a | own b] on the lower / upper lanes
+                    if constexpr (OFF == 32) perm_swap32(a, b);
+                    else perm_swap16(a, b);
+                    w[i] = hi ? b + a : a + b;   // own + partner on both sides
+                } else {
+                    const T keep = hi ? b : a, send = hi ? a : b;
+                    w[i] = keep + row_partner<OFF>(send);
+                }
+            }
+            if (hi) {
+                base += H;
+                cnt = cnt > H ? cnt - H : 0;
+            } else {
+                cnt = cnt < H ? cnt : H;
+            }
+            rs_step<T, H, OFF / 2>(w, lane, base, cnt);
+        }
+    }
+}
+
+#ifndef KAN_BLOCK_RS
+#define KAN_BLOCK_RS 1
+#endif
+// Sum `n` (<= N) per-thread values across the block into out[0..n): a wave reduce-scatter
+// (3 <= N <= 16; wave_sum per value otherwise), then the wave partials summed in wave order (fixed
+// order, so the result is bitwise reproducible).  `red` is LDS of >= (blockDim/64)*N elements.
 template <typename T, int N>
 __device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* out) {
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     const int nw = blockDim.x / kWave;
+    if constexpr (KAN_BLOCK_RS && N >= 3 && N <= 16) {
+        T w[16];
 #pragma unroll
-    for (int q = 0; q < N; ++q) {
-        if (q < n) {
-            const T s = wave_sum(v[q]);
-            if (lane == 0) red[wid * n + q] = s;
+        for (int q = 0; q < 16; ++q) w[q] = q < N ? v[q] : T(0);
+        int base = 0, cnt = N;
+        rs_step<T, N, 32>(w, lane, base, cnt);
+        if ((lane & 3) == 0 && cnt >= 1 && base < n) red[wid * n + base] = w[0];
+    } else {
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            if (q < n) {
+                const T s = wave_sum(v[q]);
+                if (lane == 0) red[wid * n + q] = s;
+            }
         }
     }
     __syncthreads();
