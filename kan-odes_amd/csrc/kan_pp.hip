@@ -703,6 +703,9 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 #ifndef KAN_VJP_SPLIT_HORNER
 #define KAN_VJP_SPLIT_HORNER 1
 #endif
+#ifndef KAN_VJP_UNROLL_PAIRS
+#define KAN_VJP_UNROLL_PAIRS 1
+#endif
 #ifndef KAN_VJP_WPE
 #define KAN_VJP_WPE 3
 #endif
@@ -724,14 +727,18 @@ constexpr int kVjpChunk = KAN_VJP_CHUNK;   // rows per wave of the standalone ta
 // and the adjoint stage input λs = lam + Σ sl.c_j sl.k_j are formed in registers (λs written
 // to lam_out when non-null); with err_slab the λ error Σ (e/sk)², e = Σ sl.ec_j sl.k_j +
 // sl.ec_nk λᵀJ, sk = abstol + reltol·max(|lam|,|λs|), is block-summed into err_slab[block].
-template <int NORM, int PATH, int GT, int NP, bool STG>
+// NI > 0: the table's interval count as a compile-time constant, so the LDS row offsets of the
+// Horner coefficients are instruction immediates instead of per-point address adds (with the
+// unrolled pairs: 1M trajectories 1557 -> 1460 us); 0: runtime ni.
+template <int NORM, int PATH, int GT, int NP, bool STG, int NI>
 __global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(STG ? KAN_VJP_STG_WPE : KAN_VJP_WPE)))
 fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
-                      const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
+                      const double2* __restrict__ tables, int ni_rt, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, const double* __restrict__ lam, double* __restrict__ lamJ,
                       double* __restrict__ slab, int64_t B, StageArgs<double> su, StageArgs<double> sl,
                       double* __restrict__ lam_out, double* __restrict__ err_slab, int chunk) {
     constexpr int Nx = 128 * NP;
+    const int ni = NI > 0 ? NI : ni_rt;
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     if (STG && stage_skip(sl.skip)) return;
@@ -820,9 +827,12 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
             lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, la[k][0], la[k][1]);
         }
-        // a real loop over the row's pairs (not unrolled): only one pair's table reads
-        // and exponentials are live next to the 40 accumulator VGPRs
-#pragma unroll 1
+        // the row's pairs of the standalone VJP (NP <= 2): unrolled, with a scheduling barrier between
+        // them so only one pair's table reads and exponentials are live next to the 40 accumulator
+        // VGPRs (1M trajectories 1557 -> 1460 us, profiles/r02/ab/vjp_unroll_ab.txt).  Elsewhere a real
+        // loop selecting the pair's registers (unrolled, the stage and NP = 4 forms spill).
+        constexpr int kPairUnroll = (KAN_VJP_UNROLL_PAIRS && !STG && NP <= 2) ? NP : 1;
+#pragma unroll kPairUnroll
         for (int k = 0; k < NP; ++k) {
             kd2 uk = uv[0], lk = lv[0], l0k = l0[0], ek = ev[0];
             double a0 = la[0][0], a1 = la[0][1];
@@ -839,6 +849,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                     }
                 }
             }
+            if constexpr (kPairUnroll > 1) __builtin_amdgcn_sched_barrier(0);
             const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0, S1,
                                                            S2, dW);
             __builtin_amdgcn_sched_barrier(0);
@@ -1670,10 +1681,10 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
                                const StageArgs<double>& sl, double* lam_out, double* err_slab, hipStream_t st,
                                int grid_ovr) {
     const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
-#define KAN_VJP_WAVE(NP)                                                                                          \
+#define KAN_VJP_WAVE(NP, NI)                                                                                      \
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
-        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>, lds, kVjpBlock);            \
+        if (!cap) cap = pp_grid_cap(fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG, NI>, lds, kVjpBlock);        \
         const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
         /* the standalone VJP (not a stage): contiguous chunks over a batch-covering grid, chunk */             \
         /* grown until the grid fits the slab */                                                                 \
@@ -1687,13 +1698,14 @@ static hipError_t fk_vjp_pp_go(const PPConst& hpc, const LayerConst* lc, const d
         } else {                                                                                                 \
             grid = grid_for(B, kVjpBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                      \
         }                                                                                                        \
-        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG>), dim3(grid), dim3(kVjpBlock), lds, st,  \
+        hipLaunchKernelGGL((fk_vjp_pp_wave_kernel<NORM, PATH, GT, NP, STG, NI>), dim3(grid), dim3(kVjpBlock), lds, st, \
                            lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, lam, lamJ, slab, B, \
                            su, sl, lam_out, err_slab ? slab + (int64_t)grid * (GT + 1) : nullptr, chunk);        \
     } while (0)
-    if (Nx == 256) KAN_VJP_WAVE(2);
-    else if (Nx == 128) KAN_VJP_WAVE(1);
-    else KAN_VJP_WAVE(4);
+    if (Nx == 256 && !STG && hpc.ni == 256) KAN_VJP_WAVE(2, 256);   // the FK256 tables (w = 1/32 on [-4, 4))
+    else if (Nx == 256) KAN_VJP_WAVE(2, 0);
+    else if (Nx == 128) KAN_VJP_WAVE(1, 0);
+    else KAN_VJP_WAVE(4, 0);
 #undef KAN_VJP_WAVE
     return hipGetLastError();
 }

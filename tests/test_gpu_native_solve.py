@@ -491,25 +491,34 @@ def test_adjoint_step_rows_kernel_matches_persistent_grid(nx, B, adaptive):
     rhs = _fk_cfg(nx, 10, "softsign")
     u0 = t(fk_u0(nx, B, 5))
     p0 = t(np.random.default_rng(11).uniform(-1.0, 1.0, 11))
-    if adaptive:
-        tspan, ts, opt = (0.0, 0.6), [0.0, 0.2, 0.45, 0.6], kanode.Tsit5Options(abstol=1e-10, reltol=1e-9)
+    if adaptive:   # tolerances at which accuracy, not the stability limit, picks the steps (see above)
+        tspan, ts, opt = (0.0, 0.5), [0.0, 0.2, 0.45, 0.5], kanode.Tsit5Options(abstol=1e-11, reltol=1e-10)
     else:
         tspan, ts = (0.0, 0.1), [0.0, 0.05, 0.1]
         opt = kanode.Tsit5Options(adaptive=False, dt=5e-4 * (256 / nx) ** 2)
     s1, g1, gu1 = _solve_grad(rhs, u0, p0, tspan, ts, opt)
     s0, g0, gu0 = _solve_grad(rhs, u0, p0, tspan, ts, opt, adj_step_rows=0)
     assert torch.equal(s1.u, s0.u)
-    assert abs(s1.stats["adjoint"]["naccept"] - s0.stats["adjoint"]["naccept"]) <= (1 if adaptive else 0)
-    assert (g1 - g0).abs().max().item() <= 1e-12 * g0.abs().max().item()
     if adaptive:
-        assert (gu1 - gu0).abs().max().item() <= 1e-10 * gu0.abs().max().item()
+        # μ starts at 0, so its error scale is abstol and the μ error estimate (a difference of
+        # reduced sums) carries the reductions' rounding: the two kernels' step sequences can part
+        # on last-bit differences (as in test_native_adjoint_matches_python_adjoint); both then
+        # solve the same adjoint to the tolerance
+        na, nb = s1.stats["adjoint"]["naccept"], s0.stats["adjoint"]["naccept"]
+        assert abs(na - nb) <= 0.01 * nb
+        tol = 1e-9 if na == nb else 50 * opt.reltol
+        assert (g1 - g0).abs().max().item() <= tol * g0.abs().max().item()
+        assert (gu1 - gu0).abs().max().item() <= tol * gu0.abs().max().item()
     else:
+        assert s1.stats["adjoint"]["naccept"] == s0.stats["adjoint"]["naccept"]
+        assert (g1 - g0).abs().max().item() <= 1e-12 * g0.abs().max().item()
         assert torch.equal(gu1, gu0)
 
 
 def test_adjoint_step_rows_kernel_batch_cap():
-    """Above 8192 rows (4 rows x the 2048 slab blocks) the adjoint step falls back to the
-    persistent-grid kernel: both settings of KANODE_OPT_ADJ_STEP_ROWS then run the same kernel."""
+    """Above 8192 rows (one row per wave: 4 rows x the 2048 slab blocks) the adjoint step falls back
+    to the persistent-grid kernel: both settings of KANODE_OPT_ADJ_STEP_ROWS then run the same
+    kernel."""
     rhs = _fk_cfg(128, 10, "softsign")
     u0 = t(np.tile(fk_u0(128, 16, 6), (513, 1)))    # 8208 rows
     p0 = t(np.random.default_rng(12).uniform(-1.0, 1.0, 11))
