@@ -31,6 +31,10 @@ for w in fk_rhs fk_rhs_rec fk_vjp; do
       python3 tools/prof_kernel.py --what $w --reps 5 --batch ${BATCH:-1048576} > $OUT/pmc_${w}_$n.log 2>&1 || { echo "pmc $w $n failed"; tail -5 $OUT/pmc_${w}_$n.log; exit 3; }
   done
 done
+echo "== epoch kernel trace"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/epoch -o run --output-format csv -- \
+  python3 tools/prof_epoch.py --batch 4096 --reps 3 > $OUT/epoch.log 2>&1 || { tail -5 $OUT/epoch.log; exit 3; }
+cp $OUT/epoch/run_kernel_stats.csv $OUT/epoch_kernel_stats.csv
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 BATCH=${BATCH:-1048576} python3 tools/traffic.py $OUT > $OUT/traffic.json
 cat $OUT/pmc_summary.txt $OUT/traffic.json
