@@ -93,31 +93,45 @@ def cpu_baseline(nx, dx, D, p_np, target_s: float):
     }
 
 
-def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: float, reps: int):
+def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: float, reps: int, group=None,
+                rank: int = 0, world: int = 1):
     """Wall-clock of one training epoch (BASELINE metric, second half): fixed-step Tsit5 forward
     solve with saveat (dense output kept), the InterpolatingAdjoint backward solve (the reference's
-    SciMLSensitivity default; one kanode_vjp_stage per adjoint stage), loss, Adam update
-    (kanode.Trainer.step; Fisher-KPP_Source.jl:102-109,167-201).  The CPU reference runs the
-    same epoch through the oracle (dense Nx x Nx Laplacian matvec, as the reference does) on a
-    bounded sample of B_cpu trajectories; per-trajectory times are reported for both."""
+    SciMLSensitivity default), loss, Adam update (kanode.Trainer.step; Fisher-KPP_Source.jl:102-109,
+    167-201).  With a process group every rank trains its own shard of B_gpu trajectories (data
+    parallel, weak scaling) and Trainer.step all-reduces [dL/dp ; L] once per epoch (RCCL with the
+    nccl backend); the epoch time is the max over ranks.  The CPU reference runs the same epoch
+    through the oracle (dense Nx x Nx Laplacian matvec, as the reference does) on a bounded sample
+    of B_cpu trajectories; per-trajectory times are reported for both."""
     T = steps * dt
     saveat = [T * i / 5 for i in range(6)]
     solver = kanode.Tsit5Options(adaptive=False, dt=dt)
     kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
     rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev)
-    u0 = fk_ics(B_gpu, nx, dx, seed=7, device=dev)
+    u0 = fk_ics(B_gpu, nx, dx, seed=7 + rank, device=dev)
     target = (0.9 * u0).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
     tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, target, torch.as_tensor(p_np, device=dev), eta=1e-3,
-                        solver=solver)
-    tr.step()                                   # warm-up (allocations, table builds)
+                        solver=solver, group=group)
+    tr.step()                                   # warm-up (allocations, table builds, the collective)
     torch.cuda.synchronize()
+    if group is not None:
+        import torch.distributed as tdist
+        tdist.barrier(group=group)
     t0 = time.perf_counter()
     for _ in range(reps):
         tr.step()
     torch.cuda.synchronize()
     gpu_s = (time.perf_counter() - t0) / reps
+    if group is not None:
+        tt = torch.tensor([gpu_s], dtype=torch.float64, device=dev if tdist.get_backend(group) == "nccl" else "cpu")
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX, group=group)
+        gpu_s = float(tt.item())
     out = {"unit": "s/epoch", "gpu": gpu_s, "gpu_batch": B_gpu, "steps": steps, "dt": dt, "stages_per_step": 6,
            "what": "fixed-step Tsit5 solve + InterpolatingAdjoint + Adam, FK256 fp64 (native kanode_solve_tsit5 + kanode_adjoint_tsit5)"}
+    if group is not None:
+        out.update({"ranks": world, "trajectories_total": B_gpu * world, "scaling": "weak",
+                    "trajectories_per_s": B_gpu * world / gpu_s,
+                    "collective": "one all_reduce(SUM) of [dL/dp ; L] (12 doubles) per epoch"})
     if B_cpu > 0:
         from oracle import oracle as O
         from oracle.oracle_rhs import OracleFKRHS
@@ -379,9 +393,12 @@ def main() -> None:
         out["lv4096"] = lv4096_bench(dev)
         out["lv1_train"] = lv1_train_bench(dev, world == 1 and not args.no_cpu_baseline)
 
-    if not args.no_epoch and rank == 0:
-        out["epoch"] = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch,
-                                   0 if (args.no_cpu_baseline or world > 1) else 8, args.epoch_steps, 1e-3, 3)
+    if not args.no_epoch:
+        ep = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch, 0 if (args.no_cpu_baseline or world > 1) else 8,
+                         args.epoch_steps, 1e-3, 3, group=tdist.group.WORLD if dist else None, rank=rank,
+                         world=world)
+        if rank == 0:
+            out["epoch"] = ep
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(nx, dx, D, p_np, args.cpu_seconds)
