@@ -234,6 +234,91 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     return out
 
 
+def _graph_us(fn, reps: int = 50) -> float:
+    """Device time per call from a hipGraph of `reps` back-to-back calls (launch-bound sizes)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(st):
+        fn()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(reps):
+                fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (3 * reps)
+
+
+def surrogate_bench(dev, with_cpu: bool, only: str | None = None, reps: int = 3):
+    """BASELINE configs[3] and [4]: the full-field KAN surrogates, per GPU.
+    burgers512: KAN [512, 10, 512] G=5 softsign (Burgers_Surrogate.jl:85-97 at 512 points), 4 ICs
+      u0 = -sin(pi x) + sum_k a_k sin(k pi x) on [-1, 1], tspan (0, 1), saveat every 0.005 (200 steps),
+      ADAM(1e-2) (:160).
+    schrodinger1024: KAN [2048, 10, 2048] G=10 softsign (Schrodinger_Surrogate.jl:93-104 at 1024 points,
+      state [Re; Im]), 8 ICs u0 = A 2 sech(x) (cos th, sin th) on [-5, 5], tspan (0, pi/2), saveat
+      0.1:0.2:1.5 (:73), ADAM(1e-3) (:170).
+    Reported: device time per RHS and per VJP at the batch (hipGraph of back-to-back calls) and one
+    training iteration (adaptive Tsit5 at the default tolerances, InterpolatingAdjoint, Adam;
+    kanode.Trainer.step).  CPU: the oracle chain (C restatement of kdense.jl:109-130, one core) per RHS
+    of the same batch."""
+    out = {}
+    cases = (("burgers512", 512, 5, 4, (-1.0, 1.0), (0.0, 1.0), [0.005 * i for i in range(201)], 1e-2),
+             ("schrodinger1024", 1024, 10, 8, (-5.0, 5.0), (0.0, np.pi / 2), [0.1 + 0.2 * i for i in range(8)], 1e-3))
+    for name, nx, G, B, xs, tspan, saveat, eta in cases:
+        if only and name != only:
+            continue
+        N = nx if name.startswith("burgers") else 2 * nx
+        chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
+        rhs = kanode.ChainRHS(chain, device=dev)
+        p_np = chain.setup(np.random.default_rng(0))[0].astype(np.float64)
+        p = torch.as_tensor(p_np, device=dev)
+        rng = np.random.default_rng(5)
+        x = np.linspace(xs[0], xs[1], nx)
+        if name.startswith("burgers"):
+            a = rng.normal(0.0, 0.1, (B, 3))
+            u0 = -np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3))
+        else:
+            amp, th = rng.uniform(0.8, 1.2, (B, 1)), rng.uniform(0.0, 2 * np.pi, (B, 1))
+            env = amp * 2.0 / np.cosh(x)[None, :]
+            u0 = np.concatenate([env * np.cos(th), env * np.sin(th)], axis=1)
+        u = torch.as_tensor(u0, device=dev)
+        lam = torch.randn_like(u)
+        du, dp = torch.empty_like(u), torch.zeros_like(p)
+        rhs.hd.reserve(B)
+        t_rhs = _graph_us(lambda: rhs.hd.rhs(p, u, du))
+        t_vjp = _graph_us(lambda: rhs.hd.vjp(p, u, lam, dp=dp))
+        target = (0.9 * u).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+        tr = kanode.Trainer(rhs, u, tspan, saveat, target, p, eta=eta)
+        tr.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tr.step()
+        torch.cuda.synchronize()
+        it_ms = (time.perf_counter() - t0) / reps * 1e3
+        _, _, sol = tr.loss_and_grad()
+        o = {"kan": f"[{N}, 10, {N}] G={G} softsign", "P": int(p.numel()), "batch": B, "dtype": "f64",
+             "rhs_us": t_rhs, "vjp_us": t_vjp, "rhs_evals_per_s": B / (t_rhs * 1e-6),
+             "param_GBps_rhs": 8.0 * p.numel() / (t_rhs * 1e-6) / 1e9,
+             "train_iteration_ms": it_ms, "forward_steps": sol.stats["naccept"],
+             "adjoint_steps": sol.stats["adjoint"]["naccept"] if "adjoint" in sol.stats else None}
+        if with_cpu:
+            from oracle import oracle as O
+            specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+            tc = O.bench_chain(specs, p_np, u0, 20, 1) / 20
+            o.update({"cpu_rhs_us": tc * 1e6, "cpu_cores": 1, "cpu_kind": "port (oracle chain, C)",
+                      "gpu_vs_cpu_rhs": tc * 1e6 / t_rhs})
+        out[name] = o
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -392,6 +477,7 @@ def main() -> None:
     if rank == 0 and not args.no_vjp:
         out["lv4096"] = lv4096_bench(dev)
         out["lv1_train"] = lv1_train_bench(dev, world == 1 and not args.no_cpu_baseline)
+        out["surrogates"] = surrogate_bench(dev, world == 1 and not args.no_cpu_baseline)
 
     if not args.no_epoch:
         ep = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch, 0 if (args.no_cpu_baseline or world > 1) else 8,

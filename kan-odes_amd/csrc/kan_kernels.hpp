@@ -269,18 +269,32 @@ hipError_t launch_kd_chain_tsit5(const LayerConst* hlcs, int nl, const LayerCons
 // surrogate shapes (kan_wide.hip)
 constexpr int kWideKT = 8;       // column tile of the wide-out kernels
 constexpr int kWideOMax = 16;    // max out_dims of a wide-in layer
+// Stage inputs formed by the wide-in forward of a surrogate pair (kanode_rhs_stage /
+// kanode_vjp_stage): block (chunk, column) forms its inputs y = x + Σ su.c·su.k (the order of
+// stage_lincomb_kernel) -> y_out, and, with lam, the adjoint stage input λs = lam + Σ sl.c·sl.k
+// over the same index range -> ls_out (N_in == N_out), so no separate combination launches.
+template <typename T>
+struct WideStageIn {
+    StageArgs<T> su;
+    T* y_out;
+    const T* lam;
+    StageArgs<T> sl;
+    T* ls_out;
+};
 template <typename T>
 hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
-                                int64_t K, hipStream_t st);
+                                int64_t K, hipStream_t st, const WideStageIn<T>* si = nullptr);
 // xslab (nullable): the layer input is the nblk chunk partials of the wide-in layer before it
 // (launch_kd_fwd_widein with y == nullptr), summed in the reduce kernel's order by the consumer
 template <typename T>
 hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                                  hipStream_t st, const T* xslab = nullptr, int xnblk = 0);
+// assign: the parameter cotangents are written (=) instead of accumulated (+=); every pbar entry of
+// the layer has exactly one writer
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
                                  T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab = nullptr,
-                                 int xnblk = 0);
+                                 int xnblk = 0, bool assign = false);
 // inputs per block of the wide-in forward (kd_fwd_widein_co_kernel: at most kWIMaxV C and kWIMaxW W
 // entries per thread of 256) and its chunk count
 constexpr int kWideInMaxInputs = 64;
@@ -299,6 +313,6 @@ inline int widein_chunks(const LayerConst& h) {
 }
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
-                                T* pbar, int64_t K, hipStream_t st);
+                                T* pbar, int64_t K, hipStream_t st, bool assign = false);
 
 }  // namespace kan

@@ -94,12 +94,24 @@ __device__ __forceinline__ T layer_in(const T* __restrict__ x, const T* __restri
 // and W loads are issued before the chunk's basis values are staged in LDS (by the first cw
 // threads), so their latency overlaps the exponentials.  Per-thread partials are summed per
 // output in thread order: slab[(chunk*K + k)*O + o].
+// With stage_on the chunk's inputs are the stage input y = x + Σ su.c·su.k, formed by the first ni
+// threads into LDS (and y_out), which also form λs over the same range (WideStageIn).
 template <typename T>
-__global__ void __launch_bounds__(256)
-kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                        T* __restrict__ slab, int64_t K) {
+__device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const StageArgs<T>& sa, int64_t idx) {
+    const double sc = stage_scale(sa.cscale);
+    T v = base[idx];
+#pragma unroll
+    for (int j = 0; j < kMaxStages; ++j)
+        if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), sa.k[j][idx], v);
+    return v;
+}
+template <typename T, bool STAGE>
+__device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
+                                                const T* __restrict__ x, T* __restrict__ slab, int64_t K,
+                                                const WideStageIn<T>* si) {
     __shared__ T phiL[kWideInMaxInputs * kMaxGrid];
     __shared__ T swL[kWideInMaxInputs];
+    __shared__ T xL[kWideInMaxInputs];
     __shared__ T red[256];
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
@@ -125,10 +137,20 @@ kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
             const int f = t + m * tn;
             wv[m] = t < tn && f < nw ? Wb[f] : T(0);
         }
+        if constexpr (STAGE) {
+            if (t < ni) {
+                const int64_t idx = (int64_t)I * k + i0 + t;
+                const T v = wide_stage_comb<T>(x, si->su, idx);
+                xL[t] = v;
+                if (si->y_out) si->y_out[idx] = v;
+                if (si->lam) si->ls_out[idx] = wide_stage_comb<T>(si->lam, si->sl, idx);
+            }
+            __syncthreads();
+        }
         // one thread per basis slot c = g + G i (direct formula: no per-input knot chain)
         for (int c = t; c < ni * G; c += blockDim.x) {
             const int i = c / G, g = c - i * G;
-            const T xi = x[(int64_t)I * k + i0 + i];
+            const T xi = STAGE ? xL[i] : x[(int64_t)I * k + i0 + i];
             const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
             T aux = T(0);
             phiL[c] = basis_direct<T>(M, lc.basis, (n - T(lc.grid[g])) * T(lc.invh), aux);
@@ -154,6 +176,19 @@ kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
         }
         __syncthreads();
     }
+}
+// (two kernels: the plain forward keeps a small argument block, the stage form carries StageArgs)
+template <typename T>
+__global__ void __launch_bounds__(256)
+kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                        T* __restrict__ slab, int64_t K) {
+    widein_fwd_body<T, false>(lcp, p, x, slab, K, nullptr);
+}
+template <typename T>
+__global__ void __launch_bounds__(256)
+kd_fwd_widein_stage_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                           T* __restrict__ slab, int64_t K, WideStageIn<T> si) {
+    widein_fwd_body<T, true>(lcp, p, x, slab, K, &si);
 }
 
 // y[o + O*k] = Σ_b slab[(b*K + k)*O + o]   (ordered over b)
@@ -266,7 +301,7 @@ template <typename T, int PATH>
 __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const LayerConst* __restrict__ lcp,
                                                    const T* __restrict__ x, const T* __restrict__ xslab, int nblk,
                                                    const T* __restrict__ ybar, T* __restrict__ pbar, int64_t K,
-                                                   int bx, int i) {
+                                                   int bx, int i, int assign) {
     __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
     __shared__ T red[kSW][kWOB];
     const LayerConst& lc = *lcp;
@@ -313,8 +348,8 @@ __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const Layer
                 T sum = red[0][lane];
 #pragma unroll
                 for (int v = 1; v < kSW; ++v) sum += red[v][lane];
-                if (r < G) dC[(int64_t)O * r] += sum;
-                else pbar[lc.w_off + o + (int64_t)O * i] += sum;
+                T* dst = r < G ? dC + (int64_t)O * r : pbar + lc.w_off + o + (int64_t)O * i;
+                *dst = assign ? sum : *dst + sum;
             }
         }
     }
@@ -374,7 +409,7 @@ template <typename T, int PATH>
 __global__ void __launch_bounds__(kWOX)
 kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                                const T* __restrict__ xslab, int nblk, const T* __restrict__ ybar, T* __restrict__ S,
-                               T* __restrict__ pbar, int64_t K, int nd, int tiles, int nrc) {
+                               T* __restrict__ pbar, int64_t K, int nd, int tiles, int nrc, int assign) {
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
     const int b = blockIdx.x;
@@ -383,7 +418,7 @@ kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __re
         wideout_dot_body<T>(lcp, p, ybar, S, K, b % ir, b / ir, tiles);
     } else {
         const int q = b - nd;
-        wideout_param_body<T, PATH>(M, lcp, x, xslab, nblk, ybar, pbar, K, q % nrc, q / nrc);
+        wideout_param_body<T, PATH>(M, lcp, x, xslab, nblk, ybar, pbar, K, q % nrc, q / nrc, assign);
     }
 }
 
@@ -433,7 +468,7 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                         const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
-                        int nxg, int cw) {
+                        int nxg, int cw, int assign) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wv_raw[];
     T* L = reinterpret_cast<T*>(wv_raw);
     KAN_EXP_TABLE_LDS(tab);
@@ -483,8 +518,12 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
             for (int m = 0; m < kS; ++m) {
                 const int c = t + 256 * m;
                 if (c < nc) {
-                    dC[(int64_t)O * c] += dcv[m];
-                    if (base && c % G == 0) pbar[lc.w_off + (int64_t)O * (i0 + c / G) + o] += dwv[m];
+                    T* d = dC + (int64_t)O * c;
+                    *d = assign ? dcv[m] : *d + dcv[m];
+                    if (base && c % G == 0) {
+                        T* dw = pbar + lc.w_off + (int64_t)O * (i0 + c / G) + o;
+                        *dw = assign ? dwv[m] : *dw + dwv[m];
+                    }
                 }
             }
         } else {
@@ -498,11 +537,13 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
             if (t < nc) {
                 T sum = red[t];
                 for (int r = 1; r < nq; ++r) sum += red[r * ncp + t];
-                dC[(int64_t)O * t] += sum;
+                T* d = dC + (int64_t)O * t;
+                *d = assign ? sum : *d + sum;
                 if (base && t % G == 0) {
                     T sw = redw[t / G];
                     for (int r = 1; r < nq; ++r) sw += redw[r * cw + t / G];
-                    pbar[lc.w_off + (int64_t)O * (i0 + t / G) + o] += sw;
+                    T* dw = pbar + lc.w_off + (int64_t)O * (i0 + t / G) + o;
+                    *dw = assign ? sw : *dw + sw;
                 }
             }
         }
@@ -571,10 +612,11 @@ static inline unsigned col_tiles(int64_t K) {
 
 template <typename T>
 hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, T* y, T* slab,
-                                int64_t K, hipStream_t st) {
+                                int64_t K, hipStream_t st, const WideStageIn<T>* si) {
     const int nblk = widein_chunks(h);
     const dim3 grid(nblk, (unsigned)(K < 65535 ? K : 65535));
-    hipLaunchKernelGGL((kd_fwd_widein_co_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K);
+    if (si) hipLaunchKernelGGL((kd_fwd_widein_stage_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K, *si);
+    else hipLaunchKernelGGL((kd_fwd_widein_co_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !y) return e;   // y == nullptr: the consumer sums the slab itself
     const int64_t n = (int64_t)h.O * K;
@@ -601,7 +643,8 @@ hipError_t launch_kd_fwd_wideout(const LayerConst& h, const LayerConst* lc, cons
 
 template <typename T>
 hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb,
-                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab, int xnblk) {
+                                 T* xb, T* pbar, T* slab, int64_t K, hipStream_t st, const T* xslab, int xnblk,
+                                 bool assign) {
     const int R = h.G + (h.use_base ? 1 : 0);
     const int tiles = (int)col_tiles(K), nrc = (h.O + kWOB - 1) / kWOB;
     const int nd = xb ? h.I * R * tiles : 0, np = pbar ? nrc * h.I : 0;
@@ -610,7 +653,7 @@ hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, cons
     do {                                                                                                           \
         if (nd + np > 0)                                                                                           \
             hipLaunchKernelGGL((kd_vjp_wideout_dotparam_kernel<T, PATH>), dim3(nd + np), dim3(kWOX), 0, st, lc, p, x, \
-                               xslab, xnblk, yb, slab, pbar, K, nd, tiles, nrc);                                  \
+                               xslab, xnblk, yb, slab, pbar, K, nd, tiles, nrc, assign ? 1 : 0);                  \
         if (xb) hipLaunchKernelGGL((kd_vjp_wideout_xfin_kernel<T, PATH>), dim3(gf), dim3(kBlock), 0, st, lc, x, xslab, \
                                    xnblk, slab, xb, K);                                                           \
     } while (0)
@@ -625,7 +668,7 @@ hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, cons
 
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
-                                T* pbar, int64_t K, hipStream_t st) {
+                                T* pbar, int64_t K, hipStream_t st, bool assign) {
     // few columns: the forward's chunks; many: chunks of <= 64 basis slots, so the parameter blocks
     // spread the columns over 256 / (cw·G) >= 4 lanes per slot
     const int cw = K > 8 ? (64 / h.G > 1 ? 64 / h.G : 1) : widein_cw(h.O, h.G);
@@ -637,19 +680,19 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
     size_t lds = (size_t)4 * cw * h.G + kOWide + 2 * (size_t)cw;   // x̄ blocks
     lds = sizeof(T) * (lds > 512 ? lds : 512);                         // parameter blocks' lane sums
     hipLaunchKernelGGL((kd_vjp_widein_co_kernel<T>), grid, dim3(256), lds, st, lc, p, x, yb, xb, pbar, K, np, nxg,
-                       cw);
+                       cw, assign ? 1 : 0);
     return hipGetLastError();
 }
 
 #define KAN_WIDE_INST(T)                                                                                       \
     template hipError_t launch_kd_fwd_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*, T*, \
-                                                int64_t, hipStream_t);                                          \
+                                                int64_t, hipStream_t, const WideStageIn<T>*);                   \
     template hipError_t launch_kd_fwd_wideout<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,   \
                                                  int64_t, hipStream_t, const T*, int);                          \
     template hipError_t launch_kd_vjp_wideout<T>(const LayerConst&, const LayerConst*, const T*, const T*,       \
-                                                 const T*, T*, T*, T*, int64_t, hipStream_t, const T*, int);    \
+                                                 const T*, T*, T*, T*, int64_t, hipStream_t, const T*, int, bool); \
     template hipError_t launch_kd_vjp_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*,        \
-                                                const T*, T*, T*, int64_t, hipStream_t);
+                                                const T*, T*, T*, int64_t, hipStream_t, bool);
 KAN_WIDE_INST(double)
 KAN_WIDE_INST(float)
 #undef KAN_WIDE_INST

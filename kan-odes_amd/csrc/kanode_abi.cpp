@@ -517,8 +517,27 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_col: ") + hipGetErrorString(e));
         }
     }
-    // unfused: y materialised (into y_out or the handle's stage workspace), RHS, error pass
     const int64_t n = h->n_in * B;
+    if (h->spec.rhs_kind == KANODE_RHS_CHAIN && surrogate_pair(h) && !skip) {
+        // surrogate pair: the wide-in forward forms y itself (kd_fwd_widein_co_kernel stage input)
+        kanode_status s = ensure_ws(h, B, st);
+        if (s != KANODE_OK) return s;
+        T* y = (T*)sg->y_out;
+        if (!y && err_out) {
+            if ((s = ensure_stage_ws(h, (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
+            y = (T*)h->stage_ws;
+        }
+        T* ps = (T*)h->ws + ws_layout(h, B).pslab;
+        kan::WideStageIn<T> si{};
+        si.su = sa;
+        si.y_out = y;
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st, &si));
+        HIP_TRY(h, kan::launch_kd_fwd_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, du, B, st, ps,
+                                                  kan::widein_chunks(h->hlc[0])));
+        if (err_out) HIP_TRY(h, kan::launch_stage_error<T>(u, y, du, sa, (double*)h->slab, kSlabBlocks, err_out, n, st));
+        return KANODE_OK;
+    }
+    // unfused: y materialised (into y_out or the handle's stage workspace), RHS, error pass
     T* y = (T*)sg->y_out;
     if (!y) {
         kanode_status s = ensure_stage_ws(h, (size_t)n * sizeof(T), st);
@@ -648,6 +667,33 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
             if (e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_vjp_stage: ") + hipGetErrorString(e));
         }
+    }
+    if (h->spec.rhs_kind == KANODE_RHS_CHAIN && surrogate_pair(h) && lamJ) {
+        // surrogate pair: y and λs formed by the wide-in forward (no combination launches), the
+        // parameter cotangents written with = when dp_assign (no memset): four launches per stage
+        if ((s = ensure_ws(h, B, st)) != KANODE_OK) return s;
+        if ((s = ensure_stage_ws(h, 2 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
+        T* y = (T*)h->stage_ws;
+        T* ls = adj->y_out ? (T*)adj->y_out : (T*)h->stage_ws + n;
+        const WsLayout wl = ws_layout(h, B);
+        T* ws = (T*)h->ws;
+        T* ps = ws + wl.pslab;
+        T* hbar = ws + wl.g0;
+        const int nb = kan::widein_chunks(h->hlc[0]);
+        kan::WideStageIn<T> si{};
+        si.su = su;
+        si.y_out = y;
+        si.lam = lam;
+        si.sl = sl;
+        si.ls_out = ls;
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st, &si));
+        HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, ls, hbar, dp,
+                                                  ws + wl.wslab, B, st, ps, nb, dp_assign));
+        HIP_TRY(h, kan::launch_kd_vjp_widein<T>(h->hlc[0], h->dlc, p, y, hbar, lamJ, dp, B, st, dp_assign));
+        if (adj->want_error)
+            HIP_TRY(h, kan::launch_stage_error<T>(lam, ls, lamJ, sl, (double*)h->slab, kSlabBlocks,
+                                                  (double*)adj->error_sumsq, n, st));
+        return KANODE_OK;
     }
     if (dp && dp_assign) HIP_TRY(h, hipMemsetAsync(dp, 0, (size_t)h->P * sizeof(T), st));
     if ((s = ensure_stage_ws(h, 2 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;

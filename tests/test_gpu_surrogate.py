@@ -120,3 +120,39 @@ def test_surrogate_pair_launches_equal_layer_by_layer(N, G, B):
     assert torch.equal(lamJ2, xbar)
     _, dp2 = hd.vjp(p, u, lam, want_lamJ=False)
     assert torch.equal(dp2, dp)
+
+
+@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (2048, 10, 8), (300, 7, 3)])
+def test_surrogate_pair_stages_form_their_inputs_in_the_wide_in_kernel(N, G, B):
+    """kanode_rhs_stage / kanode_vjp_stage on a KAN [N, 10, N]: the wide-in forward forms the stage
+    input y = u + Σ c_j k_j and the adjoint stage input λs = λ + Σ lc_j lk_j itself and the parameter
+    cotangents are written with = (no combination or memset launches).  Against the plain RHS / VJP
+    evaluated at the y and λs the stages wrote out: bitwise equal; y and λs against torch's
+    combination to rounding; dp accumulates onto a given vector."""
+    rng = np.random.default_rng(N + G + B)
+    specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+    p = t(_glorot_params(rng, specs))
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=torch.float64, rhs_kind="chain", device=device())
+    u = t(rng.uniform(-1, 1, (B, N)))
+    ks = [t(rng.normal(size=(B, N))) for _ in range(3)]
+    c = [0.1, -0.05, 0.02]
+    y = torch.empty_like(u)
+    sumsq = torch.zeros(1, dtype=torch.float64, device=device())
+    du = hd.rhs_stage(p, u, ks, c, y_out=y, error=([0.01, -0.02, 0.03, 0.04], 1e-6, 1e-3, sumsq))
+    y_ref = u + c[0] * ks[0] + c[1] * ks[1] + c[2] * ks[2]
+    assert (y - y_ref).abs().max().item() <= 1e-15 * max(1.0, y_ref.abs().max().item())
+    assert torch.equal(du, hd.rhs(p, y))
+    e = 0.01 * ks[0] - 0.02 * ks[1] + 0.03 * ks[2] + 0.04 * du
+    sk = 1e-6 + 1e-3 * torch.maximum(u.abs(), y.abs())
+    assert abs(sumsq.item() - ((e / sk) ** 2).sum().item()) <= 1e-12 * ((e / sk) ** 2).sum().item()
+    lam = t(rng.normal(size=(B, N)))
+    lks = [t(rng.normal(size=(B, N))) for _ in range(2)]
+    lc = [0.3, -0.2]
+    ls = torch.empty_like(u)
+    lamJ, dp = hd.vjp_stage(p, u, ks, c, lam, lks, lc, lam_out=ls)
+    assert (ls - (lam + lc[0] * lks[0] + lc[1] * lks[1])).abs().max().item() <= 1e-15 * ls.abs().max().item()
+    lamJ_ref, dp_ref = hd.vjp(p, y, ls)
+    assert torch.equal(lamJ, lamJ_ref) and torch.equal(dp, dp_ref)
+    dp0 = t(rng.normal(size=p.shape))
+    _, dp2 = hd.vjp_stage(p, u, ks, c, lam, lks, lc, dp=dp0.clone())
+    assert (dp2 - (dp0 + dp_ref)).abs().max().item() <= 1e-15 * (dp0.abs() + dp_ref.abs()).max().item()
