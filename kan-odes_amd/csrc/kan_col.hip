@@ -120,6 +120,9 @@ kd_fwd_col_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, c
 // compile time for the Lotka-Volterra KAN [2,10,2], G = 5 (LV_driver_KANODE.jl:139-142), where
 // the loops over outputs and knots then unroll to exactly the live iterations (the generic code
 // runs all 16 output slots per layer: ~3x the instructions on a latency-bound single wave).
+#ifndef KAN_CHAIN_OUTMAJOR
+#define KAN_CHAIN_OUTMAJOR 1
+#endif
 struct ChainShapeAny {
     static constexpr int NL = 0;
     static constexpr int dim(int) { return 0; }
@@ -161,11 +164,93 @@ __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* l
 
 constexpr int kChainBlock = 256;
 constexpr int kChainDim = 16;    // lanes per column = max layer width
+
+// Output-major evaluation of a fixed-shape layer with a few inputs and more outputs (the LV layer
+// [2 -> 10]): the I inputs are broadcast from lanes 0..I-1 of the row, every lane evaluates their
+// bases, and lane o < O forms output o itself -- no cross-lane sums (input-major, each of the O
+// outputs costs two 16-lane row sums: 20 of them for the LV layer).
+constexpr int kOutMajorMaxI = 4;
+template <class S> __device__ __forceinline__ constexpr bool out_major(int l) {
+    return S::NL > 0 && S::dim(l) <= kOutMajorMaxI && S::dim(l + 1) > 2 * S::dim(l);
+}
+template <typename T, int NORM, int PATH>
+__device__ __forceinline__ T layer_fwd_outmajor(const Math<T>& M, const LayerConst& lc, const T* ps, int I, int O,
+                                                int G, int j, T a) {
+    const T* __restrict__ C = ps + lc.p_off;
+    const T* __restrict__ W = ps + lc.w_off;
+    const int o = j < O ? j : 0;   // lanes >= O evaluate output 0 and discard it
+    T acc = T(0), bas = T(0);
+#pragma unroll
+    for (int i = 0; i < kOutMajorMaxI; ++i) {
+        if (i < I) {
+            const T xi = row16_bcast(a, i);
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, normalize<NORM, T>(M, lc.norm, xi));
+#pragma unroll
+            for (int g = 0; g < kMaxGrid; ++g) {
+                if (g < G) {
+                    T z, aux;
+                    const T phi = bs.next(M, lc, g, z, aux);
+                    acc = kfma<T>(C[o + O * (g + G * i)], phi, acc);
+                }
+            }
+            if (lc.use_base) bas = kfma<T>(W[o + O * i], swish<T>(M, xi), bas);
+        }
+    }
+    return j < O ? (lc.use_base ? acc + bas : acc) : T(0);
+}
+// Its pullback: lane o holds ȳ_o; it adds ȳ_o φ_c(x) and ȳ_o swish(x_i) into its own entries of the
+// group's gradient row and its terms of x̄_i, which the row sums over o; lane i keeps x̄_i.
+template <typename T, int NORM, int PATH>
+__device__ __forceinline__ T layer_pull_outmajor(const Math<T>& M, const LayerConst& lc, const T* ps,
+                                                 T* __restrict__ row, int I, int O, int G, int j, T a, T ybar) {
+    const T* __restrict__ C = ps + lc.p_off;
+    const T* __restrict__ W = ps + lc.w_off;
+    const bool live = j < O;
+    const int o = live ? j : 0;
+    const T yb = live ? ybar : T(0);
+    const T invh = T(lc.invh);
+    T xb = T(0);
+#pragma unroll
+    for (int i = 0; i < kOutMajorMaxI; ++i) {
+        if (i < I) {
+            const T xi = row16_bcast(a, i);
+            const T n = normalize<NORM, T>(M, lc.norm, xi);
+            BasisStream<T, PATH> bs;
+            bs.init(M, lc, n);
+            T sc = T(0);
+#pragma unroll
+            for (int g = 0; g < kMaxGrid; ++g) {
+                if (g < G) {
+                    T z, aux;
+                    const T phi = bs.next(M, lc, g, z, aux);
+                    const int c = g + G * i;
+                    if (live) row[lc.p_off + O * c + o] = kfma<T>(yb, phi, row[lc.p_off + O * c + o]);
+                    sc = sc + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, C[o + O * c] * yb) * invh;
+                }
+            }
+            T v = row16_sum(sc) * dnormalize<NORM, T>(lc.norm, n);
+            if (lc.use_base) {
+                T sw, dsw;
+                swish_and_grad<T>(M, xi, sw, dsw);
+                if (live) row[lc.w_off + O * i + o] = kfma<T>(yb, sw, row[lc.w_off + O * i + o]);
+                v = v + row16_sum(W[o + O * i] * yb) * dsw;
+            }
+            if (j == i) xb = v;
+        }
+    }
+    return xb;
+}
+
 template <typename T, int NORM, int PATH, class S>
 __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps, int j, T a) {
     auto layer = [&](int l) {
         const LayerConst& lc = lcl[l];
         const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
+        if (KAN_CHAIN_OUTMAJOR && out_major<S>(l)) {
+            a = layer_fwd_outmajor<T, NORM, PATH>(M, lc, ps, I, O, G, j, a);
+            return;
+        }
         const T* __restrict__ C = ps + lc.p_off;
         const T* __restrict__ W = ps + lc.w_off;
         T acc[kChainDim], bas[kChainDim];
@@ -452,7 +537,11 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
 #pragma unroll
     for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
         act[l + 1] = T(0);
-        if (l + 1 < sh_nl<S>(nl)) {
+        if (l + 1 < sh_nl<S>(nl) && KAN_CHAIN_OUTMAJOR && out_major<S>(l)) {
+            const LayerConst& lc = lcl[l];
+            act[l + 1] = layer_fwd_outmajor<T, NORM, PATH>(M, lc, ps, sh_I<S>(lc, l), sh_O<S>(lc, l), sh_G<S>(lc), j,
+                                                           act[l]);
+        } else if (l + 1 < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
             const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
             const T* __restrict__ C = ps + lc.p_off;
@@ -495,7 +584,11 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
     T ybar = lj;
 #pragma unroll
     for (int l = kChainMaxLayers - 1; l >= 0; --l) {
-        if (l < sh_nl<S>(nl)) {
+        if (l < sh_nl<S>(nl) && KAN_CHAIN_OUTMAJOR && out_major<S>(l)) {
+            const LayerConst& lc = lcl[l];
+            ybar = layer_pull_outmajor<T, NORM, PATH>(M, lc, ps, row, sh_I<S>(lc, l), sh_O<S>(lc, l), sh_G<S>(lc), j,
+                                                      act[l], ybar);
+        } else if (l < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
             const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
             const T* __restrict__ C = ps + lc.p_off;
@@ -1018,6 +1111,7 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
     };
     extern __shared__ __attribute__((aligned(16))) unsigned char ca_raw[];
     const int NG = blockDim.x / kChainDim;
+    const int NGa = B < NG ? (int)B : NG;   // groups holding a trajectory
     LayerConst* lcl = reinterpret_cast<LayerConst*>(ca_raw);
     T* ps = reinterpret_cast<T*>(ca_raw + nl * sizeof(LayerConst));
     T* rows = ps + P;                        // [NG][P] gradient rows
@@ -1091,16 +1185,17 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
         }
         const T lj = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, row, j, y, act ? ls : T(0));
         __syncthreads();
-        // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order
+        // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order.  The
+        // rows of groups without a trajectory (g >= B) stay zero, so they are left out of the sum
         for (int q = threadIdx.x; q < P; q += blockDim.x) {
             T tot = T(0);
-            for (int g0 = 0; g0 < NG; g0 += 4) {
+            for (int g0 = 0; g0 < NGa; g0 += 4) {
                 T sblk = rows[(size_t)g0 * P + q];
-                for (int g = g0 + 1; g < g0 + 4 && g < NG; ++g) sblk = sblk + rows[(size_t)g * P + q];
+                for (int g = g0 + 1; g < g0 + 4 && g < NGa; ++g) sblk = sblk + rows[(size_t)g * P + q];
                 tot = g0 == 0 ? sblk : tot + sblk;
             }
             km[(size_t)slot * P + q] = tot;
-            for (int g = 0; g < NG; ++g) rows[(size_t)g * P + q] = T(0);
+            for (int g = 0; g < NGa; ++g) rows[(size_t)g * P + q] = T(0);
         }
         __syncthreads();
         return act ? lj : T(0);
