@@ -111,7 +111,12 @@ def test_native_adjoint_matches_python_adjoint(name):
     (gp, gu, sn), (rp, ru, sp) = out
     assert sn["naccept"] == sp["naccept"]
     na, nb = sn["adjoint"]["naccept"], sp["adjoint"]["naccept"]
-    if na == nb and sn["adjoint"]["nreject"] == sp["adjoint"]["nreject"]:
+    # The two drivers sum the [λ; μ] error norm in different orders (native: the fused step's wave and
+    # block partials; Python: per-stage launches), so their step sizes agree to the norm's rounding.
+    # FK256's adjoint is stability-limited (~2000 steps hovering at EEst ~ 1), where those last-bit
+    # step differences are carried to ~1e-8 even with equal step counts: compared at the tolerance.
+    stiff = name == "fk256"
+    if na == nb and sn["adjoint"]["nreject"] == sp["adjoint"]["nreject"] and not stiff:
         tol = 1e-9 if u0.dtype == torch.float64 else 1e-3      # same step sequence: rounding only
     else:
         # A stability-limited adjoint (FK256: ~2000 steps hovering at EEst ~ 1) can flip one
