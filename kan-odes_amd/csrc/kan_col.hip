@@ -170,12 +170,21 @@ constexpr int kChainDim = 16;    // lanes per column = max layer width
 // bases, and lane o < O forms output o itself -- no cross-lane sums (input-major, each of the O
 // outputs costs two 16-lane row sums: 20 of them for the LV layer).
 constexpr int kOutMajorMaxI = 4;
-template <class S> __device__ __forceinline__ constexpr bool out_major(int l) {
-    return S::NL > 0 && S::dim(l) <= kOutMajorMaxI && S::dim(l + 1) > 2 * S::dim(l);
+constexpr int kOutMajorMaxG = 8;
+template <class S> __host__ __device__ constexpr bool out_major(int l) {
+    return S::NL > 0 && S::dim(l) <= kOutMajorMaxI && S::dim(l + 1) > 2 * S::dim(l) && S::GG <= kOutMajorMaxG;
 }
+// The bases of an output-major layer's inputs as its forward evaluated them, for its pullback in the
+// same chain_pullback call (one wave per column: the registers are there; saves the normalizer,
+// anchor exponentials and basis recurrence of every input a second time)
+template <typename T>
+struct OMCache {
+    T n[kOutMajorMaxI], sw[kOutMajorMaxI], dsw[kOutMajorMaxI];
+    T phi[kOutMajorMaxI][kOutMajorMaxG], z[kOutMajorMaxI][kOutMajorMaxG], aux[kOutMajorMaxI][kOutMajorMaxG];
+};
 template <typename T, int NORM, int PATH>
 __device__ __forceinline__ T layer_fwd_outmajor(const Math<T>& M, const LayerConst& lc, const T* ps, int I, int O,
-                                                int G, int j, T a) {
+                                                int G, int j, T a, OMCache<T>* cache = nullptr) {
     const T* __restrict__ C = ps + lc.p_off;
     const T* __restrict__ W = ps + lc.w_off;
     const int o = j < O ? j : 0;   // lanes >= O evaluate output 0 and discard it
@@ -184,17 +193,33 @@ __device__ __forceinline__ T layer_fwd_outmajor(const Math<T>& M, const LayerCon
     for (int i = 0; i < kOutMajorMaxI; ++i) {
         if (i < I) {
             const T xi = row16_bcast(a, i);
+            const T n = normalize<NORM, T>(M, lc.norm, xi);
             BasisStream<T, PATH> bs;
-            bs.init(M, lc, normalize<NORM, T>(M, lc.norm, xi));
+            bs.init(M, lc, n);
+            if (cache) cache->n[i] = n;
 #pragma unroll
-            for (int g = 0; g < kMaxGrid; ++g) {
+            for (int g = 0; g < kOutMajorMaxG; ++g) {
                 if (g < G) {
                     T z, aux;
                     const T phi = bs.next(M, lc, g, z, aux);
                     acc = kfma<T>(C[o + O * (g + G * i)], phi, acc);
+                    if (cache) {
+                        cache->phi[i][g] = phi;
+                        cache->z[i][g] = z;
+                        cache->aux[i][g] = aux;
+                    }
                 }
             }
-            if (lc.use_base) bas = kfma<T>(W[o + O * i], swish<T>(M, xi), bas);
+            if (lc.use_base) {
+                T sw;
+                if (cache) {
+                    swish_and_grad<T>(M, xi, cache->sw[i], cache->dsw[i]);   // (the same Ω as swish)
+                    sw = cache->sw[i];
+                } else {
+                    sw = swish<T>(M, xi);
+                }
+                bas = kfma<T>(W[o + O * i], sw, bas);
+            }
         }
     }
     return j < O ? (lc.use_base ? acc + bas : acc) : T(0);
@@ -203,7 +228,8 @@ __device__ __forceinline__ T layer_fwd_outmajor(const Math<T>& M, const LayerCon
 // group's gradient row and its terms of x̄_i, which the row sums over o; lane i keeps x̄_i.
 template <typename T, int NORM, int PATH>
 __device__ __forceinline__ T layer_pull_outmajor(const Math<T>& M, const LayerConst& lc, const T* ps,
-                                                 T* __restrict__ row, int I, int O, int G, int j, T a, T ybar) {
+                                                 T* __restrict__ row, int I, int O, int G, int j, T a, T ybar,
+                                                 const OMCache<T>* cache = nullptr) {
     const T* __restrict__ C = ps + lc.p_off;
     const T* __restrict__ W = ps + lc.w_off;
     const bool live = j < O;
@@ -214,16 +240,22 @@ __device__ __forceinline__ T layer_pull_outmajor(const Math<T>& M, const LayerCo
 #pragma unroll
     for (int i = 0; i < kOutMajorMaxI; ++i) {
         if (i < I) {
-            const T xi = row16_bcast(a, i);
-            const T n = normalize<NORM, T>(M, lc.norm, xi);
+            const T xi = cache ? T(0) : row16_bcast(a, i);
+            const T n = cache ? cache->n[i] : normalize<NORM, T>(M, lc.norm, xi);
             BasisStream<T, PATH> bs;
-            bs.init(M, lc, n);
+            if (!cache) bs.init(M, lc, n);
             T sc = T(0);
 #pragma unroll
-            for (int g = 0; g < kMaxGrid; ++g) {
+            for (int g = 0; g < kOutMajorMaxG; ++g) {
                 if (g < G) {
-                    T z, aux;
-                    const T phi = bs.next(M, lc, g, z, aux);
+                    T z, aux, phi;
+                    if (cache) {
+                        phi = cache->phi[i][g];
+                        z = cache->z[i][g];
+                        aux = cache->aux[i][g];
+                    } else {
+                        phi = bs.next(M, lc, g, z, aux);
+                    }
                     const int c = g + G * i;
                     if (live) row[lc.p_off + O * c + o] = kfma<T>(yb, phi, row[lc.p_off + O * c + o]);
                     sc = sc + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, C[o + O * c] * yb) * invh;
@@ -232,7 +264,12 @@ __device__ __forceinline__ T layer_pull_outmajor(const Math<T>& M, const LayerCo
             T v = row16_sum(sc) * dnormalize<NORM, T>(lc.norm, n);
             if (lc.use_base) {
                 T sw, dsw;
-                swish_and_grad<T>(M, xi, sw, dsw);
+                if (cache) {
+                    sw = cache->sw[i];
+                    dsw = cache->dsw[i];
+                } else {
+                    swish_and_grad<T>(M, xi, sw, dsw);
+                }
                 if (live) row[lc.w_off + O * i + o] = kfma<T>(yb, sw, row[lc.w_off + O * i + o]);
                 v = v + row16_sum(W[o + O * i] * yb) * dsw;
             }
@@ -534,13 +571,14 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
     // forward: the input activation of every layer (lane j holds entry j)
     T act[kChainMaxLayers];
     act[0] = yj;
+    OMCache<T> omc0;   // layer 0's bases when it is output-major (the only such layer of a fixed shape)
 #pragma unroll
     for (int l = 0; l + 1 < kChainMaxLayers; ++l) {
         act[l + 1] = T(0);
         if (l + 1 < sh_nl<S>(nl) && KAN_CHAIN_OUTMAJOR && out_major<S>(l)) {
             const LayerConst& lc = lcl[l];
             act[l + 1] = layer_fwd_outmajor<T, NORM, PATH>(M, lc, ps, sh_I<S>(lc, l), sh_O<S>(lc, l), sh_G<S>(lc), j,
-                                                           act[l]);
+                                                           act[l], l == 0 ? &omc0 : nullptr);
         } else if (l + 1 < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
             const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
@@ -587,7 +625,7 @@ __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* 
         if (l < sh_nl<S>(nl) && KAN_CHAIN_OUTMAJOR && out_major<S>(l)) {
             const LayerConst& lc = lcl[l];
             ybar = layer_pull_outmajor<T, NORM, PATH>(M, lc, ps, row, sh_I<S>(lc, l), sh_O<S>(lc, l), sh_G<S>(lc), j,
-                                                      act[l], ybar);
+                                                      act[l], ybar, l == 0 ? &omc0 : nullptr);
         } else if (l < sh_nl<S>(nl)) {
             const LayerConst& lc = lcl[l];
             const int I = sh_I<S>(lc, l), O = sh_O<S>(lc, l), G = sh_G<S>(lc);
