@@ -1355,8 +1355,11 @@ struct StepOut {
     double* u_new;
     int32_t qform;    // dense output as u_n + Σ_m θ^(m+1) Q_m, Q_m = dt Σ_i RI[i][m] k_i
 };
+#ifndef KAN_FSTEP_WPE
+#define KAN_FSTEP_WPE KAN_PP_WPE
+#endif
 template <int NORM, int BASIS, int NP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_FSTEP_WPE)))
 fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                        const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
                        const double* __restrict__ u, const double* __restrict__ k1, StepOut so, StepCoef sc,
