@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--adaptive", action="store_true")
+    ap.add_argument("--dump-grad", default=None, help="save the first variant's gradient (.npy) for cross-library checks")
     a = ap.parse_args()
     variants = a.variants.split(";")
     dev = torch.device("cuda:0")
@@ -61,6 +62,8 @@ def main():
                     first[v] = tr.loss_and_grad()[1].cpu().numpy()
         print(f"round {r}: " + "  ".join(f"[{v}] {times[v][-1]:.3f} ms" for v in variants), flush=True)
     ref = first[variants[0]]
+    if a.dump_grad:
+        np.save(a.dump_grad, ref)
     for v in variants:
         d = np.max(np.abs(first[v] - ref)) / max(np.max(np.abs(ref)), 1e-300)
         print(f"[{v}]: median {np.median(times[v]):.3f} ms/epoch  min {np.min(times[v]):.3f}  "
