@@ -362,11 +362,13 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
         T a = T(0), x0 = T(0);
         double ev = 0.0;
         if (j < I0) {
+            T kv[kMaxStages];
+            stage_ld<T>(sa, x, idx, kv);
             a = x0 = x[idx];
 #pragma unroll
             for (int m = 0; m < kMaxStages; ++m) {
                 if (m < sa.nk) {
-                    const T km = sa.k[m][idx];
+                    const T km = kv[m];
                     a = kfma<T>((T)(sa.c[m] * sc), km, a);
                     if (want_err) ev = ::fma(sa.ec[m] * sc, (double)km, ev);
                 }
@@ -716,16 +718,19 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
         T yj = T(0), lj = T(0), l0 = T(0);
         double ev = 0.0;
         if (j < N0) {
+            T kv[kMaxStages], kw[kMaxStages];
+            stage_ld<T>(su, u, idx, kv);
+            stage_ld<T>(sl, lam, idx, kw);
             yj = u[idx];
 #pragma unroll
             for (int m = 0; m < kMaxStages; ++m)
-                if (m < su.nk) yj = kfma<T>((T)(su.c[m] * suc), su.k[m][idx], yj);
+                if (m < su.nk) yj = kfma<T>((T)(su.c[m] * suc), kv[m], yj);
             lj = lam[idx];
             l0 = lj;
 #pragma unroll
             for (int m = 0; m < kMaxStages; ++m) {
                 if (m < sl.nk) {
-                    const T km = sl.k[m][idx];
+                    const T km = kw[m];
                     lj = kfma<T>((T)(sl.c[m] * slc), km, lj);
                     if (want_err) ev = ::fma(sl.ec[m] * slc, (double)km, ev);
                 }

@@ -43,6 +43,15 @@ __device__ __forceinline__ double stage_ec_last(const SA& sa) {
         if (j == sa.nk) e = sa.ec[j];
     return e;
 }
+// Element idx of every stage array, all loads issued before any value is used.  An unused slot
+// (j >= nk) reads `safe` instead, so no load sits behind a branch: a branch per load made the
+// compiler wait for each array before loading the next (one memory round trip per stage array,
+// up to 7 per stage input).  Callers combine kv[j] under `j < nk` exactly as before.
+template <typename T>
+__device__ __forceinline__ void stage_ld(const StageArgs<T>& sa, const T* safe, int64_t idx, T (&kv)[kMaxStages]) {
+#pragma unroll
+    for (int j = 0; j < kMaxStages; ++j) kv[j] = (j < sa.nk ? sa.k[j] : safe)[idx];
+}
 template <typename T>
 hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st);
 // per-block partials into `slab` (<= slab_blocks rows), then out[0] = ordered total
@@ -298,17 +307,33 @@ hipError_t launch_kd_vjp_wideout(const LayerConst& h, const LayerConst* lc, cons
 // inputs per block of the wide-in forward (kd_fwd_widein_co_kernel: at most kWIMaxV C and kWIMaxW W
 // entries per thread of 256) and its chunk count
 constexpr int kWideInMaxInputs = 64;
-constexpr int kWIMaxV = 32;
+#ifndef KAN_WIDEIN_MAXV
+#define KAN_WIDEIN_MAXV 32
+#endif
+constexpr int kWIMaxV = KAN_WIDEIN_MAXV;
 constexpr int kWIMaxW = 8;
-__host__ __device__ inline int widein_cw(int O, int G) {
+// The launch is latency-bound at a few columns: a wide input (I >= 32·kWideInMinChunks) gets at
+// least kWideInMinChunks chunks (blocks per column), so Burgers' I = 512 is not left to 8
+// long-running blocks (RHS 12.3 -> 9.5 us at B = 4).  Narrower inputs keep one chunk per
+// kWIMaxV·tn entries (their launches are short anyway, and the summation order stays the one the
+// narrow-layer parity tests were pinned with).
+#ifndef KAN_WIDEIN_MIN_CHUNKS
+#define KAN_WIDEIN_MIN_CHUNKS 16
+#endif
+constexpr int kWideInMinChunks = KAN_WIDEIN_MIN_CHUNKS;
+__host__ __device__ inline int widein_cw(int O, int G, int I) {
     const int tn = (256 / O) * O;
     int cw = (kWIMaxV * tn) / (O * G);
     if (cw > kWideInMaxInputs) cw = kWideInMaxInputs;
     if (cw * O > kWIMaxW * tn) cw = (kWIMaxW * tn) / O;
+    if (kWideInMinChunks > 0 && I >= 32 * kWideInMinChunks) {
+        const int cmin = (I + kWideInMinChunks - 1) / kWideInMinChunks;
+        if (cw > cmin) cw = cmin;
+    }
     return cw < 1 ? 1 : cw;
 }
 inline int widein_chunks(const LayerConst& h) {
-    const int cw = widein_cw(h.O, h.G);
+    const int cw = widein_cw(h.O, h.G, h.I);
     return (h.I + cw - 1) / cw;
 }
 template <typename T>

@@ -19,10 +19,12 @@ stage_lincomb_kernel(const T* __restrict__ u, StageArgs<T> sa, T* __restrict__ y
     if (stage_skip(sa.skip)) return;
     const double sc = stage_scale(sa.cscale);
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        T kv[kMaxStages];
+        stage_ld<T>(sa, u, i, kv);
         T v = u[i];
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j)
-            if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), sa.k[j][i], v);
+            if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), kv[j], v);
         y[i] = v;
     }
 }
@@ -37,10 +39,12 @@ stage_error_kernel(const T* __restrict__ u, const T* __restrict__ y, const T* __
     const double sc = stage_scale(sa.cscale);
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        T kv[kMaxStages];
+        stage_ld<T>(sa, u, i, kv);
         double e = 0.0;
 #pragma unroll
         for (int j = 0; j < kMaxStages; ++j)
-            if (j < sa.nk) e = ::fma(sa.ec[j] * sc, (double)sa.k[j][i], e);
+            if (j < sa.nk) e = ::fma(sa.ec[j] * sc, (double)kv[j], e);
         e = ::fma(stage_ec_last(sa) * sc, (double)du[i], e);
         const double sk = ::fma(sa.reltol, fmax(kabs((double)u[i]), kabs((double)y[i])), sa.abstol);
         const double r = e / sk;

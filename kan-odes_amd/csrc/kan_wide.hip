@@ -99,13 +99,17 @@ __device__ __forceinline__ T layer_in(const T* __restrict__ x, const T* __restri
 template <typename T>
 __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const StageArgs<T>& sa, int64_t idx) {
     const double sc = stage_scale(sa.cscale);
+    T kv[kMaxStages];
+    stage_ld<T>(sa, base, idx, kv);
     T v = base[idx];
 #pragma unroll
     for (int j = 0; j < kMaxStages; ++j)
-        if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), sa.k[j][idx], v);
+        if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), kv[j], v);
     return v;
 }
-template <typename T, bool STAGE>
+// MV / MW: C / W load slots per thread (>= the chunk's entries / tn; the launch picks the smallest
+// instantiation that covers the chunk -- unused predicated slots still cost instructions).
+template <typename T, bool STAGE, int MV, int MW>
 __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, T* __restrict__ slab, int64_t K,
                                                 const WideStageIn<T>* si) {
@@ -113,11 +117,10 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
     __shared__ T swL[kWideInMaxInputs];
     __shared__ T xL[kWideInMaxInputs];
     __shared__ T red[256];
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
+    const Math<T> M{kExp2Tab256};
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
-    const int cw = widein_cw(O, G);
+    const int cw = widein_cw(O, G, I);
     const int i0 = blockIdx.x * cw;
     const int ni = I - i0 < cw ? I - i0 : cw;
     const int tn = (256 / O) * O, t = threadIdx.x;
@@ -126,14 +129,14 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
     const T* __restrict__ Wb = p + lc.w_off + (int64_t)O * i0;
     const int c0 = t / O, cs = tn / O;   // entry t + m·tn belongs to basis slot c0 + m·cs
     for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
-        T cv[kWIMaxV], wv[kWIMaxW];
+        T cv[MV], wv[MW];
 #pragma unroll
-        for (int m = 0; m < kWIMaxV; ++m) {
+        for (int m = 0; m < MV; ++m) {
             const int f = t + m * tn;
             cv[m] = t < tn && f < nf ? Cb[f] : T(0);
         }
 #pragma unroll
-        for (int m = 0; m < kWIMaxW; ++m) {
+        for (int m = 0; m < MW; ++m) {
             const int f = t + m * tn;
             wv[m] = t < tn && f < nw ? Wb[f] : T(0);
         }
@@ -160,10 +163,10 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
         T acc = T(0);
         if (t < tn) {
 #pragma unroll
-            for (int m = 0; m < kWIMaxV; ++m)
+            for (int m = 0; m < MV; ++m)
                 if (t + m * tn < nf) acc = kfma<T>(cv[m], phiL[c0 + m * cs], acc);
 #pragma unroll
-            for (int m = 0; m < kWIMaxW; ++m)
+            for (int m = 0; m < MW; ++m)
                 if (t + m * tn < nw) acc = kfma<T>(wv[m], swL[c0 + m * cs], acc);
         }
         red[t] = acc;
@@ -178,17 +181,17 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
     }
 }
 // (two kernels: the plain forward keeps a small argument block, the stage form carries StageArgs)
-template <typename T>
+template <typename T, int MV, int MW>
 __global__ void __launch_bounds__(256)
 kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                         T* __restrict__ slab, int64_t K) {
-    widein_fwd_body<T, false>(lcp, p, x, slab, K, nullptr);
+    widein_fwd_body<T, false, MV, MW>(lcp, p, x, slab, K, nullptr);
 }
-template <typename T>
+template <typename T, int MV, int MW>
 __global__ void __launch_bounds__(256)
 kd_fwd_widein_stage_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                            T* __restrict__ slab, int64_t K, WideStageIn<T> si) {
-    widein_fwd_body<T, true>(lcp, p, x, slab, K, &si);
+    widein_fwd_body<T, true, MV, MW>(lcp, p, x, slab, K, &si);
 }
 
 // y[o + O*k] = Σ_b slab[(b*K + k)*O + o]   (ordered over b)
@@ -239,8 +242,7 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
                       const T* __restrict__ xslab, int nblk, T* __restrict__ y, int64_t K) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     __shared__ T red[kSW][kKT][kWOB];
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
+    const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const int GI = G * I;
@@ -410,8 +412,7 @@ __global__ void __launch_bounds__(kWOX)
 kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                                const T* __restrict__ xslab, int nblk, const T* __restrict__ ybar, T* __restrict__ S,
                                T* __restrict__ pbar, int64_t K, int nd, int tiles, int nrc, int assign) {
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
+    const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const int b = blockIdx.x;
     if (b < nd) {
         const int ir = lcp->I * (lcp->G + (lcp->use_base ? 1 : 0));
@@ -426,7 +427,7 @@ template <typename T, int PATH>
 __global__ void __launch_bounds__(kBlock)
 kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ xslab,
                            int nblk, const T* __restrict__ S, T* __restrict__ xbar, int64_t K) {
-    KAN_EXP_TABLE_LDS(tab);
+    KAN_EXP_TABLE_LDS(tab);   // G + 2 dependent exponentials per thread: the LDS copy pays here
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
     const int I = lc.I, G = lc.G;
@@ -468,11 +469,10 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                         const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
-                        int nxg, int cw, int assign) {
+                        int nsub, int nxg, int cw, int assign) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wv_raw[];
     T* L = reinterpret_cast<T*>(wv_raw);
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<T> M{tab};
+    const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     
@@ -481,17 +481,21 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
     const int t = threadIdx.x;
     const bool base = lc.use_base != 0;
     const T invh = T(lc.invh);
-    if ((int)blockIdx.y < np) {
-        // output o = blockIdx.y: dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k) for the chunk's basis slots c, basis
-        // by the direct formula; dW[o, i] += Σ_k ȳ[o, k] swish(x_ik).  With cw·G <= 128 the block's
-        // threads are nq = 256 / (cw·G) column lanes per slot (columns k ≡ q mod nq), summed over the
-        // lanes in order through LDS; otherwise one lane, slots t, t + 256, ...
-        const int o = blockIdx.y;
-        const int nc = ni * G, ncp = cw * G;
-        const int nq = ncp <= 128 ? 256 / ncp : 1;
+    if ((int)blockIdx.y < np * nsub) {
+        // output o = blockIdx.y / nsub: dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k) for the basis slots c of
+        // sub-chunk blockIdx.y % nsub (spb consecutive slots of the chunk), basis by the direct
+        // formula; dW[o, i] += Σ_k ȳ[o, k] swish(x_ik).  With spb <= 128 the block's threads are
+        // nq = 256 / spb column lanes per slot (columns k ≡ q mod nq), summed over the lanes in order
+        // through LDS; otherwise one lane, slots t, t + 256, ...  (nsub > 1 keeps spb <= 128 for a
+        // wide chunk, so a thread evaluates ~K/nq bases instead of K·ncp/256.)
+        const int o = (int)blockIdx.y / nsub, sub = (int)blockIdx.y - o * nsub;
+        const int ncp = cw * G, spb = (ncp + nsub - 1) / nsub;
+        const int c0 = sub * spb, nc = ni * G;
+        const int c1 = c0 + spb < nc ? c0 + spb : nc;
+        const int nq = spb <= 128 ? 256 / spb : 1;
         constexpr int kS = (kWideInMaxInputs * kMaxGrid + 255) / 256;
-        const int q = nq > 1 ? t / ncp : 0;
-        const int cb = nq > 1 ? t - q * ncp : t;
+        const int q = nq > 1 ? t / spb : 0;
+        const int cb = nq > 1 ? t - q * spb : t;
         T dcv[kS], dwv[kS];
 #pragma unroll
         for (int m = 0; m < kS; ++m) dcv[m] = dwv[m] = T(0);
@@ -500,8 +504,8 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
                 const T yb = ybar[(int64_t)O * k + o];
 #pragma unroll
                 for (int m = 0; m < kS; ++m) {
-                    const int c = cb + 256 * m;
-                    if ((nq == 1 || m == 0) && c < nc) {
+                    const int c = c0 + cb + 256 * m;
+                    if ((nq == 1 || m == 0) && c < c1) {
                         const int i = c / G, g = c - i * G;
                         const T xi = x[(int64_t)I * k + i0 + i];
                         const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
@@ -516,8 +520,8 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
         if (nq == 1) {
 #pragma unroll
             for (int m = 0; m < kS; ++m) {
-                const int c = t + 256 * m;
-                if (c < nc) {
+                const int c = c0 + t + 256 * m;
+                if (c < c1) {
                     T* d = dC + (int64_t)O * c;
                     *d = assign ? dcv[m] : *d + dcv[m];
                     if (base && c % G == 0) {
@@ -527,22 +531,23 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
                 }
             }
         } else {
-            T* red = L;           // [nq][ncp] slot partials, then [nq][cw] swish partials
-            T* redw = L + nq * ncp;
+            T* red = L;                 // [nq][spb] slot partials
+            T* redw = L + nq * spb;     // [nq][spb] swish partials (g = 0 slots)
             if (q < nq) {
                 red[t] = dcv[0];
-                if (cb < nc && cb % G == 0) redw[q * cw + cb / G] = dwv[0];
+                if (c0 + cb < c1 && (c0 + cb) % G == 0) redw[t] = dwv[0];
             }
             __syncthreads();
-            if (t < nc) {
+            const int c = c0 + t;
+            if (t < spb && c < c1) {
                 T sum = red[t];
-                for (int r = 1; r < nq; ++r) sum += red[r * ncp + t];
-                T* d = dC + (int64_t)O * t;
+                for (int r = 1; r < nq; ++r) sum += red[r * spb + t];
+                T* d = dC + (int64_t)O * c;
                 *d = assign ? sum : *d + sum;
-                if (base && t % G == 0) {
-                    T sw = redw[t / G];
-                    for (int r = 1; r < nq; ++r) sw += redw[r * cw + t / G];
-                    T* dw = pbar + lc.w_off + (int64_t)O * (i0 + t / G) + o;
+                if (base && c % G == 0) {
+                    T sw = redw[t];
+                    for (int r = 1; r < nq; ++r) sw += redw[r * spb + t];
+                    T* dw = pbar + lc.w_off + (int64_t)O * (i0 + c / G) + o;
                     *dw = assign ? sw : *dw + sw;
                 }
             }
@@ -559,7 +564,7 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
     T* dsL = dnL + cw;           // [cw] swish'(x_i)
     const T* __restrict__ C = p + lc.p_off + (int64_t)O * G * i0;
     const T* __restrict__ W = p + lc.w_off + (int64_t)O * i0;
-    for (int64_t k = (int64_t)blockIdx.y - np; k < K; k += nxg) {
+    for (int64_t k = (int64_t)blockIdx.y - np * nsub; k < K; k += nxg) {
         __syncthreads();
         for (int c = t; c < nc; c += blockDim.x) {
             const int i = c / G, g = c - i * G;
@@ -615,8 +620,17 @@ hipError_t launch_kd_fwd_widein(const LayerConst& h, const LayerConst* lc, const
                                 int64_t K, hipStream_t st, const WideStageIn<T>* si) {
     const int nblk = widein_chunks(h);
     const dim3 grid(nblk, (unsigned)(K < 65535 ? K : 65535));
-    if (si) hipLaunchKernelGGL((kd_fwd_widein_stage_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K, *si);
-    else hipLaunchKernelGGL((kd_fwd_widein_co_kernel<T>), grid, dim3(256), 0, st, lc, p, x, slab, K);
+    const int cw = widein_cw(h.O, h.G, h.I), tn = (256 / h.O) * h.O;
+    const int nv = (h.O * h.G * cw + tn - 1) / tn, nw = (h.O * cw + tn - 1) / tn;   // load slots needed
+#define KAN_WIN(MV, MW)                                                                                          \
+    do {                                                                                                         \
+        if (si) hipLaunchKernelGGL((kd_fwd_widein_stage_kernel<T, MV, MW>), grid, dim3(256), 0, st, lc, p, x, slab, K, *si); \
+        else hipLaunchKernelGGL((kd_fwd_widein_co_kernel<T, MV, MW>), grid, dim3(256), 0, st, lc, p, x, slab, K); \
+    } while (0)
+    if (nv <= 8 && nw <= 2) KAN_WIN(8, 2);
+    else if (nv <= 16 && nw <= 4) KAN_WIN(16, 4);
+    else KAN_WIN(kWIMaxV, kWIMaxW);
+#undef KAN_WIN
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !y) return e;   // y == nullptr: the consumer sums the slab itself
     const int64_t n = (int64_t)h.O * K;
@@ -671,16 +685,26 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
                                 T* pbar, int64_t K, hipStream_t st, bool assign) {
     // few columns: the forward's chunks; many: chunks of <= 64 basis slots, so the parameter blocks
     // spread the columns over 256 / (cw·G) >= 4 lanes per slot
-    const int cw = K > 8 ? (64 / h.G > 1 ? 64 / h.G : 1) : widein_cw(h.O, h.G);
+#ifndef KAN_VJP_WIDEIN_SMALL_CW
+#define KAN_VJP_WIDEIN_SMALL_CW 0
+#endif
+#ifndef KAN_VJP_WIDEIN_SUBCHUNKS
+#define KAN_VJP_WIDEIN_SUBCHUNKS 0   // measured neutral (Schrodinger VJP 44.0-45.1 vs 44.8-46.2 us): off
+#endif
+    const int cw = (K > 8 || KAN_VJP_WIDEIN_SMALL_CW) ? (64 / h.G > 1 ? 64 / h.G : 1) : widein_cw(h.O, h.G, h.I);
     const int nblk = (h.I + cw - 1) / cw;
     const int np = pbar ? h.O : 0;
     const int nxg = xb ? (int)(K < 4096 ? K : 4096) : 0;
     if (np + nxg == 0) return hipSuccess;
-    const dim3 grid(nblk, np + nxg);
+    // parameter blocks: a chunk of more than 128 basis slots is split into sub-chunks of <= 128, so
+    // every slot gets >= 2 column lanes (Schrodinger [2048 -> 10], G = 10: 640 slots, 5 sub-chunks)
+    const int ncp = cw * h.G;
+    const int nsub = np > 0 && ncp > 128 && KAN_VJP_WIDEIN_SUBCHUNKS ? (ncp + 127) / 128 : 1;
+    const dim3 grid(nblk, np * nsub + nxg);
     size_t lds = (size_t)4 * cw * h.G + kOWide + 2 * (size_t)cw;   // x̄ blocks
     lds = sizeof(T) * (lds > 512 ? lds : 512);                         // parameter blocks' lane sums
-    hipLaunchKernelGGL((kd_vjp_widein_co_kernel<T>), grid, dim3(256), lds, st, lc, p, x, yb, xb, pbar, K, np, nxg,
-                       cw, assign ? 1 : 0);
+    hipLaunchKernelGGL((kd_vjp_widein_co_kernel<T>), grid, dim3(256), lds, st, lc, p, x, yb, xb, pbar, K, np, nsub,
+                       nxg, cw, assign ? 1 : 0);
     return hipGetLastError();
 }
 
