@@ -49,6 +49,7 @@ __device__ __forceinline__ double stage_ec_last(const SA& sa) {
 // up to 7 per stage input).  Callers combine kv[j] under `j < nk` exactly as before.
 template <typename T>
 __device__ __forceinline__ void stage_ld(const StageArgs<T>& sa, const T* safe, int64_t idx, T (&kv)[kMaxStages]) {
+    if (sa.nk == 0) return;   // a plain RHS call (nothing combined): no loads at all
 #pragma unroll
     for (int j = 0; j < kMaxStages; ++j) kv[j] = (j < sa.nk ? sa.k[j] : safe)[idx];
 }
