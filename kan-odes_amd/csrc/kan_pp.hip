@@ -104,7 +104,11 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
         if (!same) pp_build_block(lcp, pcp, p, tables, fns);
         __syncthreads();   // every thread of this block has written its coefficients
         if (threadIdx.x == 0) {
-            __threadfence();
+            // no fence: the counter only has to order every block's stamp comparison (completed
+            // before the barrier above: its value decided `same`) before the last block's stamp
+            // write; the table and stamp stores reach the consumers through the kernel boundary.
+            // (An agent-scope __threadfence here wrote back the whole L2 once per block:
+            // buffer_wbl2, 64 of them per build.)
             unsigned* cnt = reinterpret_cast<unsigned*>(stamp + kPPStampCount);
             if (atomicAdd(cnt, 1u) == gridDim.x - 1) {
                 for (int j = 0; j <= G0; ++j) stamp[j] = j < G0 || lcp->use_base ? p[j] : 0.0;
