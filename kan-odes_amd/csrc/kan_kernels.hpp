@@ -125,11 +125,17 @@ struct AdjStepArgs {
     double* slab[6];           // per stage: [grid][P] moment rows
     double* err_slab;          // [grid] (null: no error)
     int32_t reload[6];         // (set by the launcher) stage s reads u_i, Q_m other than stage s-1's
+    // combine (fixed step): stages 0..4 are not reduced one by one; each thread accumulates
+    // A = Σ_{s<5} a[5][s+1]·moments_s and the block rows of A go to slab[0], stage 5's (kμ_7, the
+    // next step's FSAL kμ_1) to slab[5]: 2 block reductions per step instead of 6.  Only the rows
+    // kernel combines; the launcher clears it otherwise.
+    int32_t combine;
 };
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
-                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true);
+                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true,
+                                 int* combined_out = nullptr);
 constexpr int kMaxFinishJobs = 8;
 struct FinishJob {
     const double* slab;

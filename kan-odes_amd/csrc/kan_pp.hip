@@ -1132,6 +1132,10 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     const RecScalars<double> rc(lc);
     const int P = GT + (lc.use_base ? 1 : 0);
     double eacc = 0.0;
+    const bool combine = a.combine != 0;
+    double comb[GT + 1];
+#pragma unroll
+    for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         double S0[GT];
@@ -1243,8 +1247,17 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             if (threadIdx.x == 0) a.slab[s][(int64_t)blockIdx.x * P] = t;
         }
 #else
-        block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+        if (combine && s < 5) {
+#pragma unroll
+            for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
+        } else {
+            block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+        }
 #endif
+    }
+    if (combine) {
+        __syncthreads();   // red is reused
+        block_sum_to<double, GT + 1>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
     }
     if (a.err_slab) {
         const double v[1] = {eacc};
@@ -1788,7 +1801,8 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
-                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows) {
+                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows,
+                                 int* combined_out) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1799,6 +1813,8 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     int grid = 0;
     // one row per wave, the row's stages in registers, where the grid of one row per wave fits the slab
     const bool use_rows = rows && grid_ovr == 0 && Nx <= 256 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks;
+    if (!use_rows || a.err_slab) a.combine = 0;   // only the rows kernel combines, and only without the error
+    if (combined_out) *combined_out = a.combine;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
         bool same = a.su_u[s] == a.su_u[s - 1];

@@ -1166,8 +1166,10 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
     return KANODE_OK;
 }
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
-                                              double* err_out, int64_t batch, void* stream, bool& launched) {
+                                              double* err_out, int64_t batch, void* stream, bool& launched,
+                                              bool* combined) {
     launched = false;
+    if (combined) *combined = false;
     if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
         !kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx) || !h->fused_step)
         return KANODE_OK;
@@ -1177,13 +1179,29 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
     const double dx2 = h->spec.dx * h->spec.dx;
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     a->err_slab = err_out ? (double*)h->step_slab : nullptr;   // relocated by the launcher
-    int grid = 0;
+    int grid = 0, comb = 0;
+    a->combine = combined != nullptr && err_out == nullptr ? 1 : 0;
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                           (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
                                           table_build(h, h->built_vjp), h->grid_ovr.vstep,
-                                          h->grid_ovr.vstep_rows));
+                                          h->grid_ovr.vstep_rows, &comb));
     kan::FinishJobs jobs{};
     double* base = (double*)h->step_slab;
+    if (comb) {
+        // km[0] <- Σ_{s<5} h·a6_{s+1}·kμ_{s+2} (the kernel's combined rows), km[5] <- kμ_7
+        for (int q = 0; q < 2; ++q) {
+            const int s = q == 0 ? 0 : 5;
+            kan::FinishJob& jb = jobs.j[q];
+            jb.slab = base + (int64_t)s * grid * P;
+            jb.dp = (double*)km[s];
+            jb.nblk = grid;
+            jb.assign = 1;
+        }
+        HIP_TRY(h, kan::launch_vjp_finish_jobs(jobs, 2, P, st));
+        *combined = true;
+        launched = true;
+        return KANODE_OK;
+    }
     for (int s = 0; s < 6; ++s) {
         kan::FinishJob& jb = jobs.j[s];
         jb.slab = base + (int64_t)s * grid * P;

@@ -908,6 +908,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         hstep = std::min(hstep, stops[si] - tau);
         const int nxt = cur ^ 1;
         bool fused_step = false;   // Fisher-KPP table path, Q-form dense output: the six stages in one launch
+        bool combined = false;     // fixed step: km[1] holds Σ_{j>=1} h·a6_j·kμ_{j+1} (kanode_internal_fk_adjoint_step)
         if (s->qform) {
             kan::AdjStepArgs a{};
             for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];
@@ -931,7 +932,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             a.lam_out = (double*)lam[nxt];
             void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
             SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? s->dscal + 0 : nullptr, s->batch,
-                                                      st, fused_step));
+                                                      st, fused_step, &combined));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];
@@ -950,7 +951,12 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
-        SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
+        if (combined) {   // μ_new = μ + h a_61 km_1 + (the step's combined Σ_{j>=2} h a_6j km_j)
+            const double w2[2] = {a6[0], 1.0};
+            SOLVE_TRY(lincomb<T>(h, mu[cur], 2, km, w2, mu[nxt], P, st));
+        } else {
+            SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
+        }
         double hnew = hstep;
         if (o.adaptive) {
             double ec[7];
