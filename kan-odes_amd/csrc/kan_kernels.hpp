@@ -145,6 +145,11 @@ struct FinishJob {
     int64_t nblk;
     int32_t assign;
     int32_t pad;
+    // base != null: dp[q] = fma(1, Σ, fma(coef, other[q], base[q])) -- a two-term stage_lincomb of
+    // (base; other, Σ) in its own order, so the μ update of a combined adjoint step needs no launch
+    const double* base;
+    const double* other;
+    double coef;
 };
 struct FinishJobs {
     FinishJob j[kMaxFinishJobs];

@@ -1310,8 +1310,12 @@ __global__ void __launch_bounds__(kBlock) vjp_finish_jobs_kernel(FinishJobs jobs
     if (threadIdx.x == 0) {
         double t = red[0];
         for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
-        if (q < P) jb.dp[q] = jb.assign ? t : jb.dp[q] + t;
-        else jb.err_out[0] = t;
+        if (q < P) {
+            if (jb.base) jb.dp[q] = ::fma(1.0, t, ::fma(jb.coef, jb.other[q], jb.base[q]));
+            else jb.dp[q] = jb.assign ? t : jb.dp[q] + t;
+        } else {
+            jb.err_out[0] = t;
+        }
     }
 }
 

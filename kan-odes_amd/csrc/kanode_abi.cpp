@@ -1167,7 +1167,7 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
 }
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
                                               double* err_out, int64_t batch, void* stream, bool& launched,
-                                              bool* combined) {
+                                              bool* combined, const AdjMuUpdate* mu) {
     launched = false;
     if (combined) *combined = false;
     if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
@@ -1196,6 +1196,12 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
             jb.dp = (double*)km[s];
             jb.nblk = grid;
             jb.assign = 1;
+            if (q == 0 && mu) {   // μ_new = μ + a61·kμ_1 + A in the same launch (A itself is not stored)
+                jb.dp = mu->mu_new;
+                jb.base = mu->mu;
+                jb.other = mu->km1;
+                jb.coef = mu->a61;
+            }
         }
         HIP_TRY(h, kan::launch_vjp_finish_jobs(jobs, 2, P, st));
         *combined = true;

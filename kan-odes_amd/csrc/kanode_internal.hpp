@@ -61,9 +61,16 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
                                          bool& launched);
 // one InterpolatingAdjoint step on the Fisher-KPP table path (fk_vjp_step_pp_wave_kernel) plus
 // its reductions: kμ of the six stages -> km[0..5] (assigned), the λ error -> err_out
+// μ update a combined (fixed-step) adjoint step applies itself: mu_new = mu + a61·km1 + A
+struct AdjMuUpdate {
+    const double* mu;
+    double* mu_new;
+    const double* km1;
+    double a61;
+};
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
                                               double* err_out, int64_t batch, void* stream, bool& launched,
-                                              bool* combined = nullptr);
+                                              bool* combined = nullptr, const AdjMuUpdate* mu = nullptr);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

@@ -931,8 +931,9 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             a.lam = (const double*)lam[cur];
             a.lam_out = (double*)lam[nxt];
             void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
+            const AdjMuUpdate mup{(const double*)mu[cur], (double*)mu[nxt], (const double*)km[0], hstep * TA[5][0]};
             SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? s->dscal + 0 : nullptr, s->batch,
-                                                      st, fused_step, &combined));
+                                                      st, fused_step, &combined, &mup));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];
@@ -951,9 +952,9 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
-        if (combined) {   // μ_new = μ + h a_61 km_1 + (the step's combined Σ_{j>=2} h a_6j km_j)
-            const double w2[2] = {a6[0], 1.0};
-            SOLVE_TRY(lincomb<T>(h, mu[cur], 2, km, w2, mu[nxt], P, st));
+        if (combined) {
+            // μ_new = μ + h a_61 km_1 + (the step's combined Σ_{j>=2} h a_6j km_j): formed by the step's
+            // reduction launch (kanode_internal_fk_adjoint_step, AdjMuUpdate)
         } else {
             SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
         }
