@@ -319,6 +319,98 @@ def surrogate_bench(dev, with_cpu: bool, only: str | None = None, reps: int = 3)
     return out
 
 
+def _surrogate_problem(name: str, B: int, seed: int):
+    """Synthetic ICs and random-init parameters of the BASELINE configs[3]/[4] surrogates:
+    burgers512 u0 = -sin(pi x) + sum_k a_k sin(k pi x) on [-1, 1]; schrodinger1024 u0 = A 2 sech(x)
+    (cos th, sin th) on [-5, 5] as the [Re; Im] state."""
+    rng = np.random.default_rng(seed)
+    if name == "burgers512":
+        x = np.linspace(-1.0, 1.0, 512)
+        a = rng.normal(0.0, 0.1, (B, 3))
+        return -np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3))
+    x = np.linspace(-5.0, 5.0, 1024)
+    amp, th = rng.uniform(0.8, 1.2, (B, 1)), rng.uniform(0.0, 2 * np.pi, (B, 1))
+    env = amp * 2.0 / np.cosh(x)[None, :]
+    return np.concatenate([env * np.cos(th), env * np.sin(th)], axis=1)
+
+
+def _max_over_ranks(v: float, dev, backend: str, group=None) -> float:
+    import torch.distributed as tdist
+    t = torch.tensor([v], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def surrogate_dist_bench(dev, rank: int, world: int, backend: str, reps: int = 2):
+    """BASELINE configs[3] and [4] on their multi-GPU layouts, one training iteration each (adaptive
+    Tsit5 at the default tolerances, InterpolatingAdjoint, Adam), time = max over ranks.
+    bu512_tp: KAN [512, 10, 512] G=5 with the 512-point grid sharded over groups of up to 4 ranks
+      (Burgers_Surrogate.jl:85-97 "grid sharded 4x"; kanode.GridShardedChainRHS: per RHS one
+      all_reduce of the [10, B] hidden partials, per adjoint stage two, shard-local gradients); with
+      more than 4 ranks the groups train different ICs and all-reduce their gradients across groups.
+      4 ICs per group, saveat every 0.005 over (0, 1), ADAM(1e-2).
+    sc1024_dp: KAN [2048, 10, 2048] G=10, one IC per rank (Schrodinger_Surrogate.jl:93-104, 8 ICs over
+      8 GPUs), native solve + adjoint per rank, one all_reduce(SUM) of [dL/dp ; L] (450,561 doubles)
+      per iteration, ADAM(1e-3)."""
+    import torch.distributed as tdist
+    out = {}
+    # ---- BU512: grid-sharded over tp ranks ------------------------------------------------------
+    tp_size = max(d for d in (1, 2, 3, 4) if world % d == 0)
+    n_groups = world // tp_size
+    tp_groups = [tdist.new_group(list(range(g * tp_size, (g + 1) * tp_size))) for g in range(n_groups)]
+    dp_groups = [tdist.new_group(list(range(j, world, tp_size))) for j in range(tp_size)]
+    my_tp = tp_groups[rank // tp_size]
+    my_dp = dp_groups[rank % tp_size] if n_groups > 1 else None
+    c1 = kanode.LayerCfg(512, 10, 5, normalizer="softsign")
+    c2 = kanode.LayerCfg(10, 512, 5, normalizer="softsign")
+    tp = kanode.GridShardedChainRHS(c1, c2, group=my_tp, device=dev)
+    chain = kanode.Chain(kanode.KDense(512, 10, 5, normalizer="softsign"), kanode.KDense(10, 512, 5, normalizer="softsign"))
+    p_full = torch.as_tensor(chain.setup(np.random.default_rng(0))[0].astype(np.float64), device=dev)
+    u0 = torch.as_tensor(_surrogate_problem("burgers512", 4, 5 + rank // tp_size), device=dev)
+    u_loc = u0[:, tp.a:tp.b].contiguous()
+    saveat = [0.005 * i for i in range(201)]
+    target = (0.9 * u_loc).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+    tr = kanode.Trainer(tp, u_loc, (0.0, 1.0), saveat, target, tp.shard_params(p_full), eta=1e-2, group=my_dp,
+                        tp=True)
+    tr.step()
+    torch.cuda.synchronize()
+    tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    it = _max_over_ranks((time.perf_counter() - t0) / reps, dev, backend)
+    _, _, sol = tr.loss_and_grad()
+    out["bu512_tp"] = {"unit": "ms/iteration", "ms_per_iteration": it * 1e3, "ranks": world,
+                       "grid_shards": tp_size, "data_parallel_groups": n_groups, "ics_per_group": 4,
+                       "grid_points_per_rank": tp.n, "sensealg": tr.sensealg,
+                       "forward_steps": sol.stats["naccept"],
+                       "collectives": "per RHS: all_reduce of [10, 4] hidden partials; per adjoint stage: two; "
+                                      "per step: error-norm scalar" + ("; per iteration: gradient all_reduce "
+                                                                       "across groups" if n_groups > 1 else "")}
+    # ---- SC1024: one IC per rank, data parallel --------------------------------------------------
+    N = 2048
+    chain = kanode.Chain(kanode.KDense(N, 10, 10, normalizer="softsign"), kanode.KDense(10, N, 10, normalizer="softsign"))
+    rhs = kanode.ChainRHS(chain, device=dev)
+    p = torch.as_tensor(chain.setup(np.random.default_rng(0))[0].astype(np.float64), device=dev)
+    u = torch.as_tensor(_surrogate_problem("schrodinger1024", 1, 100 + rank), device=dev)
+    saveat = [0.1 + 0.2 * i for i in range(8)]
+    target = (0.9 * u).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+    tr = kanode.Trainer(rhs, u, (0.0, np.pi / 2), saveat, target, p, eta=1e-3, group=tdist.group.WORLD)
+    tr.step()
+    torch.cuda.synchronize()
+    tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    it = _max_over_ranks((time.perf_counter() - t0) / reps, dev, backend)
+    out["sc1024_dp"] = {"unit": "ms/iteration", "ms_per_iteration": it * 1e3, "ranks": world, "ics_per_rank": 1,
+                        "P": int(p.numel()), "sensealg": tr.sensealg,
+                        "collective": f"one all_reduce(SUM) of [dL/dp ; L] ({p.numel() + 1} doubles) per iteration"}
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -333,6 +425,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vjp", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
+    ap.add_argument("--no-dist-surrogates", action="store_true",
+                    help="skip the multi-rank configs[3]/[4] training legs (N > 1 only)")
     ap.add_argument("--epoch-batch", type=int, default=4096, help="trajectories in the training-epoch leg")
     ap.add_argument("--epoch-steps", type=int, default=50, help="fixed Tsit5 steps per epoch (dt = 1e-3)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -488,6 +582,11 @@ def main() -> None:
                          world=world)
         if rank == 0:
             out["epoch"] = ep
+
+    if dist and not args.no_dist_surrogates:
+        sd = surrogate_dist_bench(dev, rank, world, args.dist_backend)
+        if rank == 0:
+            out.update(sd)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(nx, dx, D, p_np, args.cpu_seconds)

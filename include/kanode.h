@@ -153,6 +153,9 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     trajectory row's stage values in the registers of one wave (batches up to 8192 rows
  *     of <= 256 points, GRID_ADJ_STEP unset); 0 = the persistent-grid step kernel, whose
  *     stages pass kλ through memory.  Same λᵀJ and λ bitwise; dp to the reduction order.
+ *   KANODE_OPT_PAIR_VJP (default 1): the VJP / adjoint stage of a surrogate chain KAN [N, H, N]
+ *     (wide-in then wide-out layer) runs as two launches (batches up to 512); 0 = the four-launch
+ *     path.  Bitwise equal results.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -163,7 +166,8 @@ typedef enum {
     KANODE_OPT_GRID_RHS = 5,
     KANODE_OPT_GRID_VJP = 6,
     KANODE_OPT_GRID_ADJ_STEP = 7,
-    KANODE_OPT_ADJ_STEP_ROWS = 8
+    KANODE_OPT_ADJ_STEP_ROWS = 8,
+    KANODE_OPT_PAIR_VJP = 9
 } kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);
@@ -283,6 +287,20 @@ kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0
 kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,
                                    const void* dl_du, void* du0, void* dp, const kanode_solver_options* opt,
                                    kanode_solve_stats* stats, void* stream);
+
+/* --- the optimiser step after the gradient all-reduce -----------
+ * Flux 0.14 Optimise.Adam + update!(opt, x, Δ) (LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:
+ * 167,201), one stream-ordered launch over the n entries of x (x, m, v, g device arrays of `dtype`):
+ *     Δ = scale·g            (scale = 1/world_size when g is the SUM all-reduce of [dp; L])
+ *     m = β1·m + (1-β1)·Δ;   v = β2·v + ((1-β2)·Δ)·Δ
+ *     x -= η · (m / (1 - β1ᵗ)) / (√(v / (1 - β2ᵗ)) + ε)
+ * computed in double (Flux's Float64 hyper-parameters) and rounded to `dtype` on store.  beta1_t = β1ᵗ, beta2_t = β2ᵗ are Flux's running powers βp at this step (β at
+ * the first step; the caller advances them).  m and v are caller-owned, persist across steps and
+ * start at zero.  No handle: KANODE_ERR_INVALID_ARG on bad sizes / hyper-parameters,
+ * KANODE_ERR_HIP when the launch fails. */
+kanode_status kanode_adam_step(void* x, void* m, void* v, const void* g, int64_t n, int32_t dtype, double scale,
+                               double eta, double beta1, double beta2, double eps, double beta1_t, double beta2_t,
+                               void* stream);
 
 /* host-pointer variants (synchronous) */
 kanode_status kanode_rhs_host(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch);

@@ -1,19 +1,40 @@
 # KANODEHip.jl — Julia binding of libkanode.so (include/kanode.h), the shim a maintainer adds next to
 # src/KolmogorovArnold.jl of the reference (INTEGRATION.md).  Not compiled or executed here: Julia is
-# absent from this image; tests/test_julia_shim.py checks it textually against the C header (every
-# ccall'd symbol is declared, every mirrored struct has the header's fields in order).
+# absent from this image.  tests/test_julia_shim.py checks it textually against the C header (every
+# ccall'd symbol is declared, every mirrored struct has the header's fields in order) and checks that
+# the Lux / ChainRules surface below exists and that every kernel call is guarded by the shape checks.
+#
+# What it replaces (file:line relative to the reference):
+#   KANChainHip      Lux.Chain(KDense(...), KDense(...))           Lotka-Volterra/LV_driver_KANODE.jl:139-143
+#                    incl. Lux.setup / ComponentArray(pM) axes      :143,162,173-175 (kdense.jl:70-107)
+#   RCKanodeHip      rc_kanode(u, p, t)                             PDE examples/Fisher-KPP_Source.jl:95-98
+#   solve_tsit5      solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat) + its InterpolatingAdjoint
+#                                                                   LV_driver_KANODE.jl:180-184,
+#                                                                   Fisher-KPP_Source.jl:102-103,198
 module KANODEHip
-using LuxCore, ChainRulesCore, Libdl
-const LIB = Ref{Ptr{Cvoid}}(C_NULL)
-lib() = (LIB[] == C_NULL && (LIB[] = Libdl.dlopen(get(ENV, "KANODE_LIB", "libkanode.so"))); LIB[])
 
-# mirrors kanode_layer_spec / kanode_spec in include/kanode.h
+using LuxCore, ChainRulesCore, Libdl, Random
+using WeightInitializers: glorot_uniform
+
+const LIB = Ref{Ptr{Cvoid}}(C_NULL)
+function lib()
+    if LIB[] == C_NULL
+        LIB[] = Libdl.dlopen(get(ENV, "KANODE_LIB", "libkanode.so"))
+    end
+    return LIB[]
+end
+sym(s::Symbol) = Libdl.dlsym(lib(), s)
+const HIPLIB = "libamdhip64"
+
+# ---- mirrors of the C structs (include/kanode.h) ------------------------------------------------
+# mirrors kanode_layer_spec
 struct LayerSpec
     in_dims::Int32; out_dims::Int32; grid_len::Int32
     normalizer::Int32; basis::Int32; use_base_act::Int32
     grid_lo::Float32; grid_hi::Float32; denominator::Float32
     iqf_reference_quirk::Int32
 end
+# mirrors kanode_spec
 struct Spec
     n_layers::Int32
     layers::NTuple{8,LayerSpec}
@@ -21,57 +42,205 @@ struct Spec
     nx::Int64; diffusion::Float64; dx::Float64
     device::Int32
 end
-const NORM = Dict(:tanh_fast => 0, :tanh => 1, :softsign => 2, :sigmoid => 3, :sigmoid_fast => 4, :identity => 5)
-layerspec(I, O, G; normalizer = :tanh_fast) =
-    LayerSpec(I, O, G, NORM[normalizer], 0, 1, -1f0, 1f0, 0f0, 1)
+
+const NORM = Dict(:tanh_fast => 0, :tanh => 1, :softsign => 2, :sigmoid => 3, :σ => 3, :sigmoid_fast => 4,
+                  :identity => 5)
+const BASIS = Dict(:rbf => 0, :rswaf => 1, :iqf => 2)
+# NNlib.fast_act under allow_fast_activation = true (kdense.jl:57-61): tanh -> tanh_fast, sigmoid -> sigmoid_fast
+const FAST = Dict(:tanh => :tanh_fast, :sigmoid => :sigmoid_fast, :σ => :sigmoid_fast)
+const DTYPE = Dict(Float32 => Int32(0), Float64 => Int32(1))
+
+# the drivers pass the functions themselves (basis_func = rbf, normalizer = softsign); Symbols work too
+actname(f::Symbol) = f
+actname(f::Function) = nameof(f)
+
+"""layerspec(in, out, G; normalizer, basis_func, use_base_act, grid_lims, denominator, ...) — the KDense
+constructor arguments (kdense.jl:20-37), with the reference's defaults: normalizer = tanh (fast_act ->
+tanh_fast), basis_func = rbf, use_base_act = true, grid_lims = (-1f0, 1f0), denominator = Float32(2/(G-1))."""
+function layerspec(I::Integer, O::Integer, G::Integer; normalizer = :tanh, basis_func = :rbf,
+                   use_base_act::Bool = true, grid_lims = (-1.0f0, 1.0f0), denominator = Float32(2 / (G - 1)),
+                   allow_fast_activation::Bool = true, iqf_reference_quirk::Bool = true)
+    n = actname(normalizer)
+    if allow_fast_activation
+        n = get(FAST, n, n)
+    end
+    haskey(NORM, n) || throw(ArgumentError("normalizer $n is not implemented by libkanode"))
+    b = actname(basis_func)
+    haskey(BASIS, b) || throw(ArgumentError("basis_func $b is not implemented by libkanode"))
+    return LayerSpec(Int32(I), Int32(O), Int32(G), Int32(NORM[n]), Int32(BASIS[b]), Int32(use_base_act),
+                     Float32(grid_lims[1]), Float32(grid_lims[2]), Float32(denominator), Int32(iqf_reference_quirk))
+end
 pad(ls) = ntuple(i -> i <= length(ls) ? ls[i] : layerspec(1, 1, 2), 8)
 
-mutable struct Handle; ptr::Ptr{Cvoid}; end
-function Handle(ls::Vector{LayerSpec}; rhs_kind = 0, nx = 0, D = 0.0, dx = 1.0, device = 0)
-    s = Ref(Spec(length(ls), pad(ls), 1, rhs_kind, nx, D, dx, device))
+# ---- the handle ----------------------------------------------------------------------------------
+mutable struct Handle
+    ptr::Ptr{Cvoid}
+    T::DataType        # element type of u, p and every output (Float32 or Float64)
+    P::Int             # kanode_param_length: the flat ComponentArray length
+    nin::Int           # rows of the [N, B] input
+    nout::Int          # rows of the [N, B] output
+end
+errmsg(ptr::Ptr{Cvoid}) = unsafe_string(ccall(sym(:kanode_last_error), Cstring, (Ptr{Cvoid},), ptr))
+function Handle(ls::Vector{LayerSpec}; T::Type = Float64, rhs_kind::Integer = 0, nx::Integer = 0, D::Real = 0.0,
+                dx::Real = 1.0, device::Integer = 0)
+    haskey(DTYPE, T) || throw(ArgumentError("libkanode computes in Float32 or Float64, not $T"))
+    s = Ref(Spec(Int32(length(ls)), pad(ls), DTYPE[T], Int32(rhs_kind), Int64(nx), Float64(D), Float64(dx),
+                 Int32(device)))
     out = Ref{Ptr{Cvoid}}(C_NULL)
-    st = ccall(dlsym(lib(), :kanode_create), Cint, (Ref{Spec}, Ref{Ptr{Cvoid}}), s, out)
-    st == 0 || error("kanode_create: ", unsafe_string(ccall(dlsym(lib(), :kanode_last_error), Cstring, (Ptr{Cvoid},), out[])))
-    h = Handle(out[]); finalizer(x -> ccall(dlsym(lib(), :kanode_destroy), Cvoid, (Ptr{Cvoid},), x.ptr), h); h
+    st = ccall(sym(:kanode_create), Cint, (Ref{Spec}, Ref{Ptr{Cvoid}}), s, out)
+    if st != 0
+        msg = out[] == C_NULL ? unsafe_string(ccall(sym(:kanode_status_string), Cstring, (Cint,), st)) :
+              errmsg(out[])
+        out[] == C_NULL || ccall(sym(:kanode_destroy), Cvoid, (Ptr{Cvoid},), out[])
+        error("kanode_create: ", msg)
+    end
+    P = Int(ccall(sym(:kanode_param_length), Int64, (Ptr{Cvoid},), out[]))
+    nin = rhs_kind == 1 ? Int(nx) : Int(ls[1].in_dims)
+    nout = rhs_kind == 1 ? Int(nx) : Int(ls[end].out_dims)
+    h = Handle(out[], T, P, nin, nout)
+    finalizer(x -> ccall(sym(:kanode_destroy), Cvoid, (Ptr{Cvoid},), x.ptr), h)
+    return h
 end
-check(h, st) = st == 0 || error(unsafe_string(ccall(dlsym(lib(), :kanode_last_error), Cstring, (Ptr{Cvoid},), h.ptr)))
+check(h::Handle, st) = st == 0 || error("libkanode: ", errmsg(h.ptr))
 
-# du = f(u; p) for u::Matrix{Float64} [N, B] (or a Vector: B = 1)
-function rhs(h::Handle, p::Vector{Float64}, u::AbstractVecOrMat{Float64}, nout::Int)
-    B = size(u, 2); du = similar(u, nout, B)
-    GC.@preserve p u du check(h, ccall(dlsym(lib(), :kanode_rhs_host), Cint,
-        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64), h.ptr, p, u, du, B))
-    u isa AbstractVector ? vec(du) : du
-end
-# (λᵀ∂f/∂u, λᵀ∂f/∂p)
-function vjp(h::Handle, p::Vector{Float64}, u::AbstractVecOrMat{Float64}, λ::AbstractVecOrMat{Float64})
-    B = size(u, 2); λJ = similar(u); dp = zero(p)
-    GC.@preserve p u λ λJ dp check(h, ccall(dlsym(lib(), :kanode_vjp_host), Cint,
-        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64),
-        h.ptr, p, u, λ, λJ, dp, B))
-    λJ, dp
+# Host copies in the handle's element type.  Duals (ForwardDiff) cannot go through the kernels: the
+# automatic sensealg of a small problem (ForwardDiffSensitivity, e.g. Fisher-KPP at Nx = 26) must be
+# replaced by InterpolatingAdjoint(autojacvec = ZygoteVJP()), whose VJPs are the rrules below.
+function tohost(::Type{T}, a::AbstractArray) where {T}
+    eltype(a) <: Real && !(eltype(a) <: Bool) ||
+        throw(ArgumentError("libkanode takes real arrays, got eltype $(eltype(a))"))
+    eltype(a) <: Union{Float32,Float64,Integer} ||
+        throw(ArgumentError("eltype $(eltype(a)) cannot enter the HIP kernels (forward-mode AD?): solve with " *
+                            "sensealg = InterpolatingAdjoint(autojacvec = ZygoteVJP())"))
+    return a isa Array{T} ? a : Array{T}(a)
 end
 
-# A whole KDense chain as one Lux layer: drop-in for `Lux.Chain(KDense(...), KDense(...))`
-# inside NeuralODE (LV_driver_KANODE.jl:139-143,180): out-of-place, differentiable by rrule.
+# every kernel call goes through these checks: the C side trusts the sizes it is given
+function checkp(h::Handle, p::AbstractVector)
+    length(p) == h.P || throw(DimensionMismatch("p has length $(length(p)); the KAN has $(h.P) parameters " *
+                                                "(kanode_param_length)"))
+    return nothing
+end
+function checku(h::Handle, u::AbstractVecOrMat, rows::Int, what::String)
+    size(u, 1) == rows || throw(DimensionMismatch("$what has $(size(u, 1)) rows; the handle expects $rows"))
+    return nothing
+end
+
+"""rhs(h, p, u) -> du: kanode_rhs_host on a Julia [N] or [N, B] array."""
+function rhs(h::Handle, p::AbstractVector, u::AbstractVecOrMat)
+    checkp(h, p)
+    checku(h, u, h.nin, "u")
+    T = h.T
+    pv, uc = tohost(T, p), tohost(T, u)
+    B = size(uc, 2)
+    du = Matrix{T}(undef, h.nout, B)
+    GC.@preserve pv uc du check(h, ccall(sym(:kanode_rhs_host), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64), h.ptr, pv, uc, du, B))
+    return u isa AbstractVector ? vec(du) : du
+end
+
+"""vjp(h, p, u, λ) -> (λᵀ∂f/∂u, λᵀ∂f/∂p): kanode_vjp_host (dp starts at zero)."""
+function vjp(h::Handle, p::AbstractVector, u::AbstractVecOrMat, λ::AbstractVecOrMat)
+    checkp(h, p)
+    checku(h, u, h.nin, "u")
+    checku(h, λ, h.nout, "λ")
+    size(λ, 2) == size(u, 2) || throw(DimensionMismatch("λ and u have different batch sizes"))
+    h.nin == h.nout || throw(ArgumentError("the RHS VJP needs a chain with in_dims == out_dims"))
+    T = h.T
+    pv, uc, λc = tohost(T, p), tohost(T, u), tohost(T, λ)
+    B = size(uc, 2)
+    λJ = similar(uc)
+    dp = zeros(T, h.P)
+    GC.@preserve pv uc λc λJ dp check(h, ccall(sym(:kanode_vjp_host), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64),
+        h.ptr, pv, uc, λc, λJ, dp, B))
+    return λJ, dp
+end
+
+# p̄ in p's own type: a ComponentArray keeps its axes (similar), a Vector stays a Vector
+ptangent(p::Vector, dp) = dp
+ptangent(p::AbstractVector, dp) = copyto!(similar(p, eltype(dp)), dp)
+xtangent(x::AbstractVector, g) = vec(g)
+xtangent(x::AbstractMatrix, g) = g
+
+# ---- the Lux layer -------------------------------------------------------------------------------
+"""KANChainHip(layerspecs; T) — a whole KDense chain as one Lux layer, the drop-in for
+`Lux.Chain(KDense(...), KDense(...))` inside NeuralODE (LV_driver_KANODE.jl:139-143,180).
+`Lux.setup(rng, kan1)` returns the reference's (layer_1 = (C, W), layer_2 = (C, W)) parameters with the
+same Glorot-uniform Float32 init and RNG order (kdense.jl:70-86), so `ComponentArray(pM)` has the
+reference axes and `getdata(ComponentArray(pM)) ./ 1e5` (:173-175) is the flat vector the kernels take."""
 struct KANChainHip <: LuxCore.AbstractLuxLayer
-    h::Handle; nin::Int; nout::Int; P::Int
+    h::Handle
+    specs::Vector{LayerSpec}
 end
-KANChainHip(ls::Vector{LayerSpec}) = (h = Handle(ls);
-    KANChainHip(h, ls[1].in_dims, ls[end].out_dims, ccall(dlsym(lib(), :kanode_param_length), Int64, (Ptr{Cvoid},), h.ptr)))
-LuxCore.parameterlength(l::KANChainHip) = l.P
-(l::KANChainHip)(x, p, st) = (rhs(l.h, collect(Float64, p), x, l.nout), st)
-function ChainRulesCore.rrule(l::KANChainHip, x, p, st)
-    pv = collect(Float64, p); y = rhs(l.h, pv, x, l.nout)
-    pullback(ȳ) = ((λJ, dp) = vjp(l.h, pv, x, collect(Float64, first(ȳ)));
-                   (NoTangent(), λJ, dp, NoTangent()))
-    (y, st), pullback
+KANChainHip(ls::Vector{LayerSpec}; T::Type = Float64, device::Integer = 0) = KANChainHip(Handle(ls; T, device), ls)
+
+layernames(l::KANChainHip) = ntuple(i -> Symbol("layer_", i), length(l.specs))
+
+function initlayer(rng::AbstractRNG, s::LayerSpec)
+    C = glorot_uniform(rng, Int(s.out_dims), Int(s.grid_len) * Int(s.in_dims))   # [O, G·I]  kdense.jl:74
+    if s.use_base_act == 1
+        return (; C, W = glorot_uniform(rng, Int(s.out_dims), Int(s.in_dims)))   # kdense.jl:80
+    end
+    return (; C)
+end
+function LuxCore.initialparameters(rng::AbstractRNG, l::KANChainHip)
+    return NamedTuple{layernames(l)}(ntuple(i -> initlayer(rng, l.specs[i]), length(l.specs)))
+end
+# st = (grid = collect(LinRange(grid_lims..., G)),) per layer (kdense.jl:88-92)
+function LuxCore.initialstates(::AbstractRNG, l::KANChainHip)
+    g(s) = (; grid = collect(LinRange(s.grid_lo, s.grid_hi, Int(s.grid_len))))
+    return NamedTuple{layernames(l)}(ntuple(i -> g(l.specs[i]), length(l.specs)))
+end
+LuxCore.parameterlength(l::KANChainHip) = l.h.P
+LuxCore.statelength(l::KANChainHip) = sum(Int(s.grid_len) for s in l.specs)
+
+# the flat parameter vector in ComponentArray order (layer_1.C, layer_1.W, layer_2.C, ...)
+flatp(p::AbstractVector) = p
+flatp(p::NamedTuple) = reduce(vcat, [vec(q) for layer in values(p) for q in values(layer)])
+
+(l::KANChainHip)(x::AbstractVecOrMat, p, st) = (rhs(l.h, flatp(p), x), st)
+
+function ChainRulesCore.rrule(l::KANChainHip, x::AbstractVecOrMat, p::AbstractVector, st)
+    y = rhs(l.h, p, x)
+    function kanchain_pullback(Δ)
+        ȳ = unthunk(unthunk(Δ)[1])
+        if ȳ isa AbstractZero
+            return (NoTangent(), ZeroTangent(), ZeroTangent(), NoTangent())
+        end
+        λJ, dp = vjp(l.h, p, x, ȳ)
+        return (NoTangent(), xtangent(x, λJ), ptangent(p, dp), NoTangent())
+    end
+    return (y, st), kanchain_pullback
 end
 
-# The whole forward solve + InterpolatingAdjoint on the device (kanode_solve_tsit5 /
-# kanode_adjoint_tsit5).  u0, p, the saveat output and dL/du are DEVICE buffers here (e.g.
-# hipMalloc'd through the same library's caller, or a ROCArray's pointer); mirrors
-# kanode_solver_options / kanode_solve_stats.
+# ---- Fisher-KPP: replaces rc_kanode (PDE examples/Fisher-KPP_Source.jl:95-98) ----------------------
+fk_handle(nx::Integer, dx::Real; D::Real = 0.01, G::Integer = 10, normalizer = :softsign, basis_func = :rbf,
+          T::Type = Float64, device::Integer = 0) =
+    Handle([layerspec(1, 1, G; normalizer, basis_func)]; T, rhs_kind = 1, nx, D, dx, device)
+
+"""rc_kanode_hip(h)(u, p, t) = D*lap*u + kan1_.(u), differentiable (rrule -> kanode_vjp_host)."""
+struct RCKanodeHip
+    h::Handle
+end
+rc_kanode_hip(h::Handle) = RCKanodeHip(h)
+(f::RCKanodeHip)(u::AbstractVecOrMat, p::AbstractVector, t) = rhs(f.h, p, u)
+
+function ChainRulesCore.rrule(f::RCKanodeHip, u::AbstractVecOrMat, p::AbstractVector, t)
+    du = rhs(f.h, p, u)
+    function rc_kanode_pullback(Δ)
+        ḡ = unthunk(Δ)
+        if ḡ isa AbstractZero
+            return (NoTangent(), ZeroTangent(), ZeroTangent(), NoTangent())
+        end
+        λJ, dp = vjp(f.h, p, u, ḡ)
+        return (NoTangent(), xtangent(u, λJ), ptangent(p, dp), NoTangent())
+    end
+    return du, rc_kanode_pullback
+end
+
+# ---- the whole solve + InterpolatingAdjoint on the device (kanode_solve_tsit5 / _adjoint_tsit5) -----
+# mirrors kanode_solver_options
 struct SolverOptions
     abstol::Float64; reltol::Float64; dt::Float64; adaptive::Int32
     maxiters::Int64; dtmin::Float64; beta1::Float64; beta2::Float64; gamma::Float64
@@ -80,34 +249,129 @@ struct SolverOptions
 end
 function default_options()
     o = Ref{SolverOptions}()
-    ccall(dlsym(lib(), :kanode_solver_options_default), Cvoid, (Ref{SolverOptions},), o); o[]
+    ccall(sym(:kanode_solver_options_default), Cvoid, (Ref{SolverOptions},), o)
+    return o[]
 end
+"""options(; abstol = 1e-6, reltol = 1e-3, dt, adaptive, maxiters, control): solve()'s keywords, with the
+OrdinaryDiffEq defaults (include/kanode.h kanode_solver_options)."""
+function options(; abstol::Real = 1e-6, reltol::Real = 1e-3, dt::Real = 0.0, adaptive::Bool = true,
+                 maxiters::Integer = 100000, control::Integer = 0)
+    d = default_options()
+    return SolverOptions(abstol, reltol, dt, Int32(adaptive), Int64(maxiters), d.dtmin, d.beta1, d.beta2, d.gamma,
+                         d.qmin, d.qmax, d.qoldinit, Int32(control), d.graph_steps)
+end
+# mirrors kanode_solve_stats
 struct SolveStats
     naccept::Int64; nreject::Int64; nf::Int64
 end
-# returns (stats, dense::Ptr) ; dense feeds adjoint!, then kanode_solution_free
-function solve!(h::Handle, p::Ptr{Float64}, u0::Ptr{Float64}, B, tspan, saveat::Vector{Float64},
-                usave::Ptr{Float64}; opt = default_options(), keep_dense = false, stream = C_NULL)
-    st = Ref{SolveStats}(); dense = Ref{Ptr{Cvoid}}(C_NULL)
-    check(h, ccall(dlsym(lib(), :kanode_solve_tsit5), Cint,
-        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Ptr{Float64}, Int64, Ptr{Float64},
+
+# device buffers through the HIP runtime (no AMDGPU.jl: hipMalloc / hipMemcpy / hipFree only)
+hipcheck(e, what) = e == 0 || error("$what failed with hipError $e")
+mutable struct DevBuf
+    ptr::Ptr{Cvoid}
+    nbytes::Int
+end
+function DevBuf(nbytes::Integer)
+    r = Ref{Ptr{Cvoid}}(C_NULL)
+    hipcheck(ccall((:hipMalloc, HIPLIB), Cint, (Ref{Ptr{Cvoid}}, Csize_t), r, max(nbytes, 1)), "hipMalloc")
+    b = DevBuf(r[], Int(nbytes))
+    finalizer(x -> ccall((:hipFree, HIPLIB), Cint, (Ptr{Cvoid},), x.ptr), b)
+    return b
+end
+function upload(a::Array)
+    b = DevBuf(sizeof(a))
+    GC.@preserve a hipcheck(ccall((:hipMemcpy, HIPLIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint),
+                                  b.ptr, a, sizeof(a), 1), "hipMemcpy H2D")
+    return b
+end
+function download!(a::Array, b::DevBuf)
+    sizeof(a) <= b.nbytes || throw(DimensionMismatch("device buffer smaller than the host array"))
+    GC.@preserve a hipcheck(ccall((:hipMemcpy, HIPLIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint),
+                                  a, b.ptr, sizeof(a), 2), "hipMemcpy D2H")
+    return a
+end
+
+# the forward dense output (kanode_solution), freed with the object
+mutable struct DenseOutput
+    ptr::Ptr{Cvoid}
+end
+function DenseOutput(ptr::Ptr{Cvoid})
+    d = DenseOutput(ptr)
+    finalizer(x -> (x.ptr == C_NULL || ccall(sym(:kanode_solution_free), Cvoid, (Ptr{Cvoid},), x.ptr)), d)
+    return d
+end
+
+# raw entry points on device pointers: returns (stats, dense::Ptr) ; dense feeds adjoint!, then free_dense
+function solve!(h::Handle, p::Ptr{Cvoid}, u0::Ptr{Cvoid}, B::Integer, tspan, saveat::Vector{Float64},
+                usave::Ptr{Cvoid}; opt::SolverOptions = default_options(), keep_dense::Bool = false,
+                stream::Ptr{Cvoid} = C_NULL)
+    st = Ref{SolveStats}()
+    dense = Ref{Ptr{Cvoid}}(C_NULL)
+    check(h, ccall(sym(:kanode_solve_tsit5), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Float64, Float64, Ptr{Float64}, Int64, Ptr{Cvoid},
          Ref{SolverOptions}, Ptr{Ptr{Cvoid}}, Ref{SolveStats}, Ptr{Cvoid}),
         h.ptr, p, u0, B, tspan[1], tspan[2], saveat, length(saveat), usave, opt,
         keep_dense ? dense : Ptr{Ptr{Cvoid}}(C_NULL), st, stream))
-    st[], dense[]
+    return st[], dense[]
 end
-function adjoint!(h::Handle, p::Ptr{Float64}, dense::Ptr{Cvoid}, dl_du::Ptr{Float64}, du0::Ptr{Float64},
-                  dp::Ptr{Float64}; opt = default_options(), stream = C_NULL)
+function adjoint!(h::Handle, p::Ptr{Cvoid}, dense::Ptr{Cvoid}, dl_du::Ptr{Cvoid}, du0::Ptr{Cvoid},
+                  dp::Ptr{Cvoid}; opt::SolverOptions = default_options(), stream::Ptr{Cvoid} = C_NULL)
     st = Ref{SolveStats}()
-    check(h, ccall(dlsym(lib(), :kanode_adjoint_tsit5), Cint,
-        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{SolverOptions},
+    check(h, ccall(sym(:kanode_adjoint_tsit5), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ref{SolverOptions},
          Ref{SolveStats}, Ptr{Cvoid}), h.ptr, p, dense, dl_du, du0, dp, opt, st, stream))
-    st[]
+    return st[]
 end
-free_dense(d::Ptr{Cvoid}) = ccall(dlsym(lib(), :kanode_solution_free), Cvoid, (Ptr{Cvoid},), d)
+free_dense(d::Ptr{Cvoid}) = ccall(sym(:kanode_solution_free), Cvoid, (Ptr{Cvoid},), d)
 
-# Fisher-KPP: replaces rc_kanode (PDE examples/Fisher-KPP_Source.jl:95-98)
-fk_handle(nx, dx; D = 0.01, G = 10) = Handle([layerspec(1, 1, G; normalizer = :softsign)];
-                                             rhs_kind = 1, nx = nx, D = D, dx = dx)
-rc_kanode_hip(h::Handle, nx) = (u, p, t) -> rhs(h, collect(Float64, p), u, nx)
+function solve_impl(h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector, saveat::AbstractVector,
+                    opt::SolverOptions, keep_dense::Bool)
+    checkp(h, p)
+    checku(h, u0, h.nin, "u0")
+    h.nin == h.nout || throw(ArgumentError("an ODE RHS needs a chain with in_dims == out_dims"))
+    T = h.T
+    ts = Vector{Float64}(saveat)
+    issorted(ts) || throw(ArgumentError("saveat must be ascending"))
+    B = size(u0, 2)
+    pd, ud = upload(tohost(T, p)), upload(tohost(T, u0))
+    out = Array{T}(undef, h.nin, B, length(ts))
+    od = DevBuf(sizeof(out))
+    st, dense = solve!(h, pd.ptr, ud.ptr, B, tspan, ts, od.ptr; opt, keep_dense)
+    download!(out, od)
+    sol = u0 isa AbstractVector ? reshape(out, h.nin, length(ts)) : out
+    return sol, st, (keep_dense ? DenseOutput(dense) : nothing), pd
+end
+
+"""solve_tsit5(h, u0, tspan, p, saveat; abstol, reltol, dt, adaptive) -> Array(sol): [N, n_save] for a
+vector u0, [N, B, n_save] for a matrix (the layout of `Array(solve(prob, Tsit5(); saveat))`).
+Differentiable in u0 and p by its rrule, whose pullback is kanode_adjoint_tsit5: SciMLSensitivity's
+InterpolatingAdjoint, the NeuralODE default (LV_driver_KANODE.jl:180), on the device."""
+function solve_tsit5(h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector, saveat::AbstractVector; kw...)
+    sol, _, _, _ = solve_impl(h, u0, tspan, p, saveat, options(; kw...), false)
+    return sol
+end
+
+function ChainRulesCore.rrule(::typeof(solve_tsit5), h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector,
+                              saveat::AbstractVector; kw...)
+    opt = options(; kw...)
+    sol, _, dense, pd = solve_impl(h, u0, tspan, p, saveat, opt, true)
+    function solve_tsit5_pullback(Δ)
+        ū = unthunk(Δ)
+        if ū isa AbstractZero
+            return (NoTangent(), NoTangent(), ZeroTangent(), NoTangent(), ZeroTangent(), NoTangent())
+        end
+        T = h.T
+        size(ū) == size(sol) || throw(DimensionMismatch("cotangent of the solution has the wrong shape"))
+        gd = upload(tohost(T, ū))
+        du0 = Array{T}(undef, size(u0))
+        dp = Array{T}(undef, h.P)
+        du0d, dpd = DevBuf(sizeof(du0)), DevBuf(sizeof(dp))
+        adjoint!(h, pd.ptr, dense.ptr, gd.ptr, du0d.ptr, dpd.ptr; opt)
+        download!(du0, du0d)
+        download!(dp, dpd)
+        return (NoTangent(), NoTangent(), du0, NoTangent(), ptangent(p, dp), NoTangent())
+    end
+    return sol, solve_tsit5_pullback
+end
+
 end # module

@@ -61,6 +61,17 @@ hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageAr
                               int slab_blocks, double* out, int64_t n, hipStream_t st);
 hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, hipStream_t st);
 
+// Flux Adam step after the gradient all-reduce (kan_optim.hip, kanode_adam_step)
+struct AdamArgs {
+    double scale;          // Δ = scale·g (1/world_size after a SUM all-reduce)
+    double beta1, beta2;   // β
+    double omb1, omb2;     // 1 - β
+    double c1, c2;         // 1 - βp (βp = β^t, Flux's running powers before this step advances them)
+    double eps, eta;
+};
+template <typename T>
+hipError_t launch_adam_step(T* x, T* m, T* v, const T* g, int64_t n, const AdamArgs& a, hipStream_t st);
+
 // piecewise-polynomial Fisher-KPP RHS / VJP (kan_pp.hip).  build = false reuses the
 // tables of an earlier launch with the same p (the integrator holds them per solve).  `tables` holds
 // kPPMaxFns slots of kPPCoef·ni doubles (slot = PPFn id); the build fills the listed
@@ -351,5 +362,15 @@ inline int widein_chunks(const LayerConst& h) {
 template <typename T>
 hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const T* p, const T* x, const T* yb, T* xb,
                                 T* pbar, int64_t K, hipStream_t st, bool assign = false);
+// The surrogate pair's whole pullback in two launches (kan_wide.hip): lc = the two layers' device
+// constants (lc[0] wide-in, lc[1] wide-out); x = layer-1 input (u; with si the stage base u, y formed
+// and written to si->y_out, λs to si->ls_out); ybar = λ (no si); xvjp = the layer-1 input the pullback
+// reads (u, or si->y_out); pslab = the wide-in chunk partials (widein_chunks·K·H), S = the wide-out dot
+// slab (H·(G+1)·K).  hipErrorNotSupported: K > kPairMaxK or the LDS would not fit (use the 4 launches).
+constexpr int64_t kPairMaxK = 512;
+template <typename T>
+hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
+                              const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
+                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign);
 
 }  // namespace kan

@@ -112,7 +112,7 @@ __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const S
 template <typename T, bool STAGE, int MV, int MW>
 __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, T* __restrict__ slab, int64_t K,
-                                                const WideStageIn<T>* si) {
+                                                const WideStageIn<T>* si, int bx, int by, int gy) {
     __shared__ T phiL[kWideInMaxInputs * kMaxGrid];
     __shared__ T swL[kWideInMaxInputs];
     __shared__ T xL[kWideInMaxInputs];
@@ -121,14 +121,14 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
     const int cw = widein_cw(O, G, I);
-    const int i0 = blockIdx.x * cw;
+    const int i0 = bx * cw;
     const int ni = I - i0 < cw ? I - i0 : cw;
     const int tn = (256 / O) * O, t = threadIdx.x;
     const int nf = O * G * ni, nw = lc.use_base ? O * ni : 0;
     const T* __restrict__ Cb = p + lc.p_off + (int64_t)O * G * i0;
     const T* __restrict__ Wb = p + lc.w_off + (int64_t)O * i0;
     const int c0 = t / O, cs = tn / O;   // entry t + m·tn belongs to basis slot c0 + m·cs
-    for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+    for (int64_t k = by; k < K; k += gy) {
         T cv[MV], wv[MW];
 #pragma unroll
         for (int m = 0; m < MV; ++m) {
@@ -175,7 +175,7 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             T sum = red[t];
 #pragma unroll 8
             for (int q = 1; q < cs; ++q) sum += red[t + q * O];
-            slab[((int64_t)blockIdx.x * K + k) * O + t] = sum;
+            slab[((int64_t)bx * K + k) * O + t] = sum;
         }
         __syncthreads();
     }
@@ -185,13 +185,13 @@ template <typename T, int MV, int MW>
 __global__ void __launch_bounds__(256)
 kd_fwd_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                         T* __restrict__ slab, int64_t K) {
-    widein_fwd_body<T, false, MV, MW>(lcp, p, x, slab, K, nullptr);
+    widein_fwd_body<T, false, MV, MW>(lcp, p, x, slab, K, nullptr, blockIdx.x, blockIdx.y, gridDim.y);
 }
 template <typename T, int MV, int MW>
 __global__ void __launch_bounds__(256)
 kd_fwd_widein_stage_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
                            T* __restrict__ slab, int64_t K, WideStageIn<T> si) {
-    widein_fwd_body<T, true, MV, MW>(lcp, p, x, slab, K, &si);
+    widein_fwd_body<T, true, MV, MW>(lcp, p, x, slab, K, &si, blockIdx.x, blockIdx.y, gridDim.y);
 }
 
 // y[o + O*k] = Σ_b slab[(b*K + k)*O + o]   (ordered over b)
@@ -365,10 +365,12 @@ __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const Layer
 //         (utils.jl:15-21, NNlib).
 constexpr int kWOX = 256;
 static_assert(kWOX == kWOB * kSW, "the dot and parameter bodies share one launch");
+// ls (nullable): ȳ is the adjoint stage input λs = ls->lam + Σ ls->sl.c·ls->sl.k, formed here in
+// wide_stage_comb's order (bitwise the values the wide-in stage forward writes to ls_out)
 template <typename T>
 __device__ __forceinline__ void wideout_dot_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                  const T* __restrict__ ybar, T* __restrict__ S, int64_t K, int bx,
-                                                 int by, int gy) {
+                                                 int by, int gy, const WideStageIn<T>* ls = nullptr) {
     __shared__ T red[kWOX / kWave][kKT];
     const LayerConst& lc = *lcp;
     const int O = lc.O, G = lc.G;
@@ -381,12 +383,21 @@ __device__ __forceinline__ void wideout_dot_body(const LayerConst* __restrict__ 
         T acc[kKT];
 #pragma unroll
         for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
+        if (ls) {
+#pragma unroll 2
+            for (int o = threadIdx.x; o < O; o += kWOX) {
+                const T cv = row[o];
+                for (int kk = 0; kk < kt; ++kk)
+                    acc[kk] = kfma<T>(cv, wide_stage_comb<T>(ls->lam, ls->sl, (int64_t)O * (k0 + kk) + o), acc[kk]);
+            }
+        } else {
 #pragma unroll 4
-        for (int o = threadIdx.x; o < O; o += kWOX) {
-            const T cv = row[o];
+            for (int o = threadIdx.x; o < O; o += kWOX) {
+                const T cv = row[o];
 #pragma unroll
-            for (int kk = 0; kk < kKT; ++kk)
-                if (kk < kt) acc[kk] = kfma<T>(cv, ybar[(int64_t)O * (k0 + kk) + o], acc[kk]);
+                for (int kk = 0; kk < kKT; ++kk)
+                    if (kk < kt) acc[kk] = kfma<T>(cv, ybar[(int64_t)O * (k0 + kk) + o], acc[kk]);
+            }
         }
 #pragma unroll
         for (int kk = 0; kk < kKT; ++kk) {
@@ -423,6 +434,33 @@ kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __re
     }
 }
 
+// x̄[i, k] of the wide-out layer from its dot products S (one element)
+template <typename T, int PATH>
+__device__ __forceinline__ T wideout_xfin_one(const Math<T>& M, const LayerConst& lc, const T* __restrict__ x,
+                                              const T* __restrict__ xslab, int nblk, const T* __restrict__ S,
+                                              int64_t K, int i, int64_t k) {
+    const int I = lc.I, G = lc.G;
+    const int R = G + (lc.use_base ? 1 : 0);
+    const T invh = T(lc.invh);
+    const T* __restrict__ Si = S + (int64_t)i * R * K + k;
+    const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k);
+    Basis1<T, PATH> bs;
+    bs.init(M, lc, xi);
+    T nbar = T(0);
+    for (int g = 0; g < G; ++g) {
+        T z, aux;
+        const T phi = bs.next(M, lc, g, z, aux);
+        nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, Si[(int64_t)g * K]) * invh;
+    }
+    T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
+    if (lc.use_base) {
+        T sw, dsw;
+        swish_and_grad<T>(M, xi, sw, dsw);
+        xb = xb + Si[(int64_t)G * K] * dsw;
+    }
+    return xb;
+}
+
 template <typename T, int PATH>
 __global__ void __launch_bounds__(kBlock)
 kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ x, const T* __restrict__ xslab,
@@ -430,30 +468,12 @@ kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restri
     KAN_EXP_TABLE_LDS(tab);   // G + 2 dependent exponentials per thread: the LDS copy pays here
     const Math<T> M{tab};
     const LayerConst& lc = *lcp;
-    const int I = lc.I, G = lc.G;
-    const int R = G + (lc.use_base ? 1 : 0);
-    const T invh = T(lc.invh);
+    const int I = lc.I;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < (int64_t)I * K;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t k = idx / I;
         const int i = (int)(idx - k * I);
-        const T* __restrict__ Si = S + (int64_t)i * R * K + k;
-        const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k);
-        Basis1<T, PATH> bs;
-        bs.init(M, lc, xi);
-        T nbar = T(0);
-        for (int g = 0; g < G; ++g) {
-            T z, aux;
-            const T phi = bs.next(M, lc, g, z, aux);
-            nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, Si[(int64_t)g * K]) * invh;
-        }
-        T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
-        if (lc.use_base) {
-            T sw, dsw;
-            swish_and_grad<T>(M, xi, sw, dsw);
-            xb = xb + Si[(int64_t)G * K] * dsw;
-        }
-        xbar[idx] = xb;
+        xbar[idx] = wideout_xfin_one<T, PATH>(M, lc, x, xslab, nblk, S, K, i, k);
     }
 }
 
@@ -465,30 +485,33 @@ kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restri
 //   blockIdx.y >= np: x̄ of the columns k ≡ y - np (mod nxg): the chunk's basis values in LDS,
 //          one thread per basis slot c = g + G i forms Σ_o C[o, c] ȳ[o, k] and its rrule term,
 //          then one thread per input sums them over g (the order of the reference pullback).
-template <typename T>
-__global__ void __launch_bounds__(256)
-kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
-                        const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
-                        int nsub, int nxg, int cw, int assign) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char wv_raw[];
-    T* L = reinterpret_cast<T*>(wv_raw);
+// The body of the wide-in pullback for block (bx, by) of the grid above.  yb_at(o, k) gives
+// ȳ[o, k]; prep_param(o) runs once, block-uniformly, before a parameter block's column loop (the
+// pair pullback forms that output's ȳ row there); yb_col(ybL, t, k) fills ybL[0, O) for an x̄
+// block's column k (thread t < O writes entry t).
+template <typename T, typename YB, typename PREP, typename YCOL>
+__device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
+                                                const T* __restrict__ x, YB yb_at, PREP prep_param, YCOL yb_col,
+                                                T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
+                                                int nsub, int nxg, int cw, int assign, int bx, int by, T* L) {
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
-    
-    const int i0 = blockIdx.x * cw;
+
+    const int i0 = bx * cw;
     const int ni = I - i0 < cw ? I - i0 : cw;
     const int t = threadIdx.x;
     const bool base = lc.use_base != 0;
     const T invh = T(lc.invh);
-    if ((int)blockIdx.y < np * nsub) {
-        // output o = blockIdx.y / nsub: dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k) for the basis slots c of
-        // sub-chunk blockIdx.y % nsub (spb consecutive slots of the chunk), basis by the direct
+    if (by < np * nsub) {
+        // output o = by / nsub: dC[o, c] += Σ_k ȳ[o, k] φ_c(x_k) for the basis slots c of
+        // sub-chunk by % nsub (spb consecutive slots of the chunk), basis by the direct
         // formula; dW[o, i] += Σ_k ȳ[o, k] swish(x_ik).  With spb <= 128 the block's threads are
         // nq = 256 / spb column lanes per slot (columns k ≡ q mod nq), summed over the lanes in order
         // through LDS; otherwise one lane, slots t, t + 256, ...  (nsub > 1 keeps spb <= 128 for a
         // wide chunk, so a thread evaluates ~K/nq bases instead of K·ncp/256.)
-        const int o = (int)blockIdx.y / nsub, sub = (int)blockIdx.y - o * nsub;
+        const int o = by / nsub, sub = by - o * nsub;
+        prep_param(o);
         const int ncp = cw * G, spb = (ncp + nsub - 1) / nsub;
         const int c0 = sub * spb, nc = ni * G;
         const int c1 = c0 + spb < nc ? c0 + spb : nc;
@@ -501,7 +524,7 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
         for (int m = 0; m < kS; ++m) dcv[m] = dwv[m] = T(0);
         if (q < nq) {
             for (int64_t k = q; k < K; k += nq) {
-                const T yb = ybar[(int64_t)O * k + o];
+                const T yb = yb_at(o, k);
 #pragma unroll
                 for (int m = 0; m < kS; ++m) {
                     const int c = c0 + cb + 256 * m;
@@ -564,7 +587,7 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
     T* dsL = dnL + cw;           // [cw] swish'(x_i)
     const T* __restrict__ C = p + lc.p_off + (int64_t)O * G * i0;
     const T* __restrict__ W = p + lc.w_off + (int64_t)O * i0;
-    for (int64_t k = (int64_t)blockIdx.y - np * nsub; k < K; k += nxg) {
+    for (int64_t k = (int64_t)by - np * nsub; k < K; k += nxg) {
         __syncthreads();
         for (int c = t; c < nc; c += blockDim.x) {
             const int i = c / G, g = c - i * G;
@@ -584,7 +607,7 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
                 }
             }
         }
-        if (t < O) ybL[t] = ybar[(int64_t)O * k + t];
+        yb_col(ybL, t, k);
         __syncthreads();
         for (int c = t; c < nc; c += blockDim.x) {
             const T* __restrict__ Cc = C + (int64_t)O * c;
@@ -605,6 +628,79 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
             xbar[(int64_t)I * k + i0 + t] = xb;
         }
     }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ p, const T* __restrict__ x,
+                        const T* __restrict__ ybar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
+                        int nsub, int nxg, int cw, int assign) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wv_raw[];
+    const int O = lcp->O;
+    widein_vjp_body<T>(
+        lcp, p, x, [&](int o, int64_t k) { return ybar[(int64_t)O * k + o]; }, [](int) {},
+        [&](T* ybL, int t, int64_t k) {
+            if (t < O) ybL[t] = ybar[(int64_t)O * k + t];
+        },
+        xbar, pbar, K, np, nsub, nxg, cw, assign, blockIdx.x, blockIdx.y, reinterpret_cast<T*>(wv_raw));
+}
+
+// ---------------------------------------------------------------------------
+// The surrogate pair's pullback in two launches (kanode_vjp / kanode_vjp_stage of a KAN [N, H, N],
+// Burgers_Surrogate.jl:85-97, Schrodinger_Surrogate.jl:93-104), instead of four:
+//   A: blocks [0, nF) the wide-in forward's chunk partials of the hidden layer h (with a stage: y and
+//      λs formed and written, WideStageIn); blocks [nF, nF + nD) the wide-out dot products
+//      S[i, r, k] = Σ_o row_{i,r}[o] ȳ[o, k] (ȳ = λs formed in place) -- they need ȳ and the
+//      parameters only, not h, so they run beside the forward;
+//   B: blocks [0, nP) the wide-out parameter cotangents (h summed from the partials, ȳ); the rest the
+//      wide-in pullback, whose cotangent (x̄ of the hidden layer) each block forms itself from S and h
+//      (wideout_xfin_one: a parameter block its output's K entries, an x̄ block its column's H),
+//      which removes the x̄ pass and its launch.
+// Every value is computed by the same arithmetic in the same order as on the four-launch path, so the
+// results are bitwise equal to it.
+template <typename T, int MV, int MW, bool STAGE>
+__global__ void __launch_bounds__(256)
+kd_vjp_pair_a_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
+                     const T* __restrict__ x, T* __restrict__ pslab, const T* __restrict__ ybar, T* __restrict__ S,
+                     int64_t K, int nF, int nblk, int gyF, int tiles, WideStageIn<T> si) {
+    const int b = blockIdx.x;
+    if (b < nF) {
+        widein_fwd_body<T, STAGE, MV, MW>(lc0, p, x, pslab, K, STAGE ? &si : nullptr, b % nblk, b / nblk, gyF);
+    } else {
+        const int q = b - nF;
+        const int ir = lc1->I * (lc1->G + (lc1->use_base ? 1 : 0));
+        wideout_dot_body<T>(lc1, p, ybar, S, K, q % ir, q / ir, tiles, STAGE ? &si : nullptr);
+    }
+}
+
+template <typename T, int PATH>
+__global__ void __launch_bounds__(256)
+kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
+                     const T* __restrict__ x, const T* __restrict__ pslab, int nblk, const T* __restrict__ ybar,
+                     const T* __restrict__ S, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int nP, int nrc,
+                     int np, int nxg, int cw, int nbx, int hb_off, int assign) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char pb_raw[];
+    T* L = reinterpret_cast<T*>(pb_raw);
+    const Math<T> M{kExp2Tab256};   // exp table from global memory (L1)
+    const int b = blockIdx.x;
+    if (b < nP) {
+        wideout_param_body<T, PATH>(M, lc1, (const T*)nullptr, pslab, nblk, ybar, pbar, K, b % nrc, b / nrc, assign);
+        return;
+    }
+    const int q = b - nP;
+    const LayerConst& l1 = *lc1;
+    T* hbL = L + hb_off;   // [K]: a parameter block's cotangent row
+    widein_vjp_body<T>(
+        lc0, p, x, [&](int, int64_t k) { return hbL[k]; },
+        [&](int o) {
+            for (int64_t k = threadIdx.x; k < K; k += blockDim.x)
+                hbL[k] = wideout_xfin_one<T, PATH>(M, l1, (const T*)nullptr, pslab, nblk, S, K, o, k);
+            __syncthreads();
+        },
+        [&](T* ybL, int t, int64_t k) {
+            if (t < l1.I) ybL[t] = wideout_xfin_one<T, PATH>(M, l1, (const T*)nullptr, pslab, nblk, S, K, t, k);
+        },
+        xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L);
 }
 
 // ---------------------------------------------------------------------------
@@ -708,6 +804,61 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
+                              const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
+                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign) {
+    if (K < 1 || K > kPairMaxK || !xb) return hipErrorNotSupported;
+    const int R1 = h1.G + (h1.use_base ? 1 : 0);
+    const int tiles = (int)col_tiles(K), nrc = (h1.O + kWOB - 1) / kWOB;
+    // B's LDS: the wide-in pullback's dynamic block (+ the K-row) beside the wide-out parameter
+    // body's static arrays; beyond 64 KB the four-launch path runs instead
+    const int cw = K > 8 ? (64 / h0.G > 1 ? 64 / h0.G : 1) : widein_cw(h0.O, h0.G, h0.I);
+    size_t lw = (size_t)4 * cw * h0.G + kOWide + 2 * (size_t)cw;
+    lw = lw > 512 ? lw : 512;
+    const size_t lds_b = sizeof(T) * (lw + (size_t)K);
+    const size_t static_b = sizeof(T) * ((size_t)(kMaxGrid + 1) * kWOPK + (size_t)kSW * kWOB);
+    if (lds_b + static_b > 65536) return hipErrorNotSupported;
+    // A
+    const int nblk = widein_chunks(h0);
+    const int gyF = (int)(K < 65535 ? K : 65535);
+    const int nF = nblk * gyF, nD = h1.I * R1 * tiles;
+    const int tn = (256 / h0.O) * h0.O, cwf = widein_cw(h0.O, h0.G, h0.I);
+    const int nv = (h0.O * h0.G * cwf + tn - 1) / tn, nw = (h0.O * cwf + tn - 1) / tn;
+    const WideStageIn<T> none{};
+    const WideStageIn<T>& sa = si ? *si : none;
+#define KAN_PA(MV, MW)                                                                                             \
+    do {                                                                                                           \
+        if (si) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(nF + nD), dim3(256), 0, st, lc,     \
+                                   lc + 1, p, x, pslab, ybar, S, K, nF, nblk, gyF, tiles, sa);                     \
+        else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(nF + nD), dim3(256), 0, st, lc,      \
+                                lc + 1, p, x, pslab, ybar, S, K, nF, nblk, gyF, tiles, sa);                        \
+    } while (0)
+    if (nv <= 8 && nw <= 2) KAN_PA(8, 2);
+    else if (nv <= 16 && nw <= 4) KAN_PA(16, 4);
+    else KAN_PA(kWIMaxV, kWIMaxW);
+#undef KAN_PA
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // B
+    const int nP = pbar ? nrc * h1.I : 0;
+    const int nbx = (h0.I + cw - 1) / cw;
+    const int np = pbar ? h0.O : 0;
+    const int nxg = (int)(K < 4096 ? K : 4096);
+    const int nW = nbx * (np + nxg);
+    const T* yb_b = si ? si->ls_out : ybar;   // ȳ of the wide-out parameter blocks: λs as A wrote it
+#define KAN_PB(PATH)                                                                                               \
+    hipLaunchKernelGGL((kd_vjp_pair_b_kernel<T, PATH>), dim3(nP + nW), dim3(256), lds_b, st, lc, lc + 1, p, xvjp,   \
+                       pslab, nblk, yb_b, S, xb, pbar, K, nP, nrc, np, nxg, cw, nbx, (int)lw, assign ? 1 : 0)
+    switch (h1.path) {
+    case PATH_REC_CORR: KAN_PB(PATH_REC_CORR); break;
+    case PATH_REC: KAN_PB(PATH_REC); break;
+    default: KAN_PB(PATH_DIRECT);
+    }
+#undef KAN_PB
+    return hipGetLastError();
+}
+
 #define KAN_WIDE_INST(T)                                                                                       \
     template hipError_t launch_kd_fwd_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*, T*, \
                                                 int64_t, hipStream_t, const WideStageIn<T>*);                   \
@@ -716,7 +867,10 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
     template hipError_t launch_kd_vjp_wideout<T>(const LayerConst&, const LayerConst*, const T*, const T*,       \
                                                  const T*, T*, T*, T*, int64_t, hipStream_t, const T*, int, bool); \
     template hipError_t launch_kd_vjp_widein<T>(const LayerConst&, const LayerConst*, const T*, const T*,        \
-                                                const T*, T*, T*, int64_t, hipStream_t, bool);
+                                                const T*, T*, T*, int64_t, hipStream_t, bool);                  \
+    template hipError_t launch_kd_vjp_pair<T>(const LayerConst&, const LayerConst&, const LayerConst*, const T*,  \
+                                              const T*, const WideStageIn<T>*, const T*, const T*, T*, T*, T*, T*, \
+                                              int64_t, hipStream_t, bool);
 KAN_WIDE_INST(double)
 KAN_WIDE_INST(float)
 #undef KAN_WIDE_INST

@@ -62,6 +62,7 @@ struct kanode_handle {
     // evaluation-strategy options (kanode_set_option; read here, never from the environment per launch)
     bool fused_step = true;           // KANODE_OPT_FUSED_STEP
     bool fused_solve = true;          // KANODE_OPT_FUSED_SOLVE
+    bool pair_vjp = true;             // KANODE_OPT_PAIR_VJP
     int fused_solve_cap = 0;          // KANODE_OPT_FUSED_SOLVE_CAP (0 = the kernel's block)
     kan::GridOverride grid_ovr{};     // KANODE_OPT_GRID_{RHS,VJP,ADJ_STEP} (0 = default)
     // the integrator's storage for solves without a dense output (kanode_solve.cpp)
@@ -436,11 +437,21 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
     T* ws = (T*)h->ws;
     const WsLayout wl = ws_layout(h, B);
     if (surrogate_pair(h)) {
-        // four launches: wide-in partials; the wide-out pullback's dot products and parameter
-        // cotangents in one launch; its input cotangent; the wide-in pullback
         T* ps = ws + wl.pslab;
         T* hbar = ws + wl.g0;
         const int nb = kan::widein_chunks(h->hlc[0]);
+        if (lamJ && h->pair_vjp) {
+            // two launches (launch_kd_vjp_pair): wide-in partials beside the wide-out dot products; the
+            // wide-out parameter cotangents beside the wide-in pullback (x̄ of the hidden layer formed
+            // per block)
+            const hipError_t e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, nullptr, lam, u, ps,
+                                                            ws + wl.wslab, lamJ, dp, B, st, false);
+            if (e == hipSuccess) return KANODE_OK;
+            if (e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
+        }
+        // four launches: wide-in partials; the wide-out pullback's dot products and parameter
+        // cotangents in one launch; its input cotangent; the wide-in pullback
         HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st));
         HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, lam, hbar, dp,
                                                   ws + wl.wslab, B, st, ps, nb));
@@ -686,10 +697,19 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         si.lam = lam;
         si.sl = sl;
         si.ls_out = ls;
-        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st, &si));
-        HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, ls, hbar, dp,
-                                                  ws + wl.wslab, B, st, ps, nb, dp_assign));
-        HIP_TRY(h, kan::launch_kd_vjp_widein<T>(h->hlc[0], h->dlc, p, y, hbar, lamJ, dp, B, st, dp_assign));
+        hipError_t e = hipErrorNotSupported;
+        if (h->pair_vjp) {   // two launches (see vjp_t)
+            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.wslab, lamJ,
+                                           dp, B, st, dp_assign);
+            if (e != hipSuccess && e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
+        }
+        if (e != hipSuccess) {
+            HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st, &si));
+            HIP_TRY(h, kan::launch_kd_vjp_wideout<T>(h->hlc[1], h->dlc + 1, p, (const T*)nullptr, ls, hbar, dp,
+                                                      ws + wl.wslab, B, st, ps, nb, dp_assign));
+            HIP_TRY(h, kan::launch_kd_vjp_widein<T>(h->hlc[0], h->dlc, p, y, hbar, lamJ, dp, B, st, dp_assign));
+        }
         if (adj->want_error)
             HIP_TRY(h, kan::launch_stage_error<T>(lam, ls, lamJ, sl, (double*)h->slab, kSlabBlocks,
                                                   (double*)adj->error_sumsq, n, st));
@@ -908,6 +928,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_GRID_VJP: return count(h->grid_ovr.vjp, "GRID_VJP", kSlabBlocks / 2);
     case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
     case KANODE_OPT_ADJ_STEP_ROWS: return flag(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS");
+    case KANODE_OPT_PAIR_VJP: return flag(h->pair_vjp, "PAIR_VJP");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -923,6 +944,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_GRID_VJP: return h->grid_ovr.vjp;
     case KANODE_OPT_GRID_ADJ_STEP: return h->grid_ovr.vstep;
     case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows ? 1 : 0;
+    case KANODE_OPT_PAIR_VJP: return h->pair_vjp ? 1 : 0;
     }
     return -1;
 }
@@ -1086,6 +1108,32 @@ kanode_status kanode_edge_activations(kanode_handle* h, int32_t layer, const voi
                                                   (const float*)x, (float*)act, K, st));
     }
     return KANODE_OK;
+}
+
+kanode_status kanode_adam_step(void* x, void* m, void* v, const void* g, int64_t n, int32_t dtype, double scale,
+                               double eta, double beta1, double beta2, double eps, double beta1_t, double beta2_t,
+                               void* stream) {
+    if (n < 0 || (dtype != KANODE_F32 && dtype != KANODE_F64)) return KANODE_ERR_INVALID_ARG;
+    if (n == 0) return KANODE_OK;
+    if (!x || !m || !v || !g) return KANODE_ERR_INVALID_ARG;
+    // 1 - β^t must stay positive (t >= 1 with 0 <= β < 1): the bias corrections divide by it
+    if (!(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && beta1_t < 1.0 && beta2_t < 1.0))
+        return KANODE_ERR_INVALID_ARG;
+    kan::AdamArgs a;
+    a.scale = scale;
+    a.beta1 = beta1;
+    a.beta2 = beta2;
+    a.omb1 = 1.0 - beta1;
+    a.omb2 = 1.0 - beta2;
+    a.c1 = 1.0 - beta1_t;
+    a.c2 = 1.0 - beta2_t;
+    a.eps = eps;
+    a.eta = eta;
+    const hipStream_t st = (hipStream_t)stream;
+    const hipError_t e = dtype == KANODE_F64
+        ? kan::launch_adam_step<double>((double*)x, (double*)m, (double*)v, (const double*)g, n, a, st)
+        : kan::launch_adam_step<float>((float*)x, (float*)m, (float*)v, (const float*)g, n, a, st);
+    return e == hipSuccess ? KANODE_OK : KANODE_ERR_HIP;
 }
 
 }  // extern "C"

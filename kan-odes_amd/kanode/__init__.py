@@ -11,7 +11,7 @@ from .layers import Chain, KDense, glorot_uniform, linrange_f32
 from .rhs import ChainRHS, FisherKPPRHS, fisher_kpp_laplacian, layer_apply, rhs_apply
 from .ode import Solution, Tsit5Options, solve
 from .adjoint import DenseRecord, interpolating_adjoint
-from .train import Adam, Trainer, mse_loss, reg_loss
+from .train import Adam, FusedAdam, Trainer, mse_loss, reg_loss
 from . import checkpoint, tp
 from .tp import GridShardedChainRHS
 
@@ -19,6 +19,6 @@ __all__ = [
     "DenseRecord", "interpolating_adjoint",
     "KanodeError", "LIB_PATH", "lib", "KanodeHandle", "LayerCfg", "Chain", "KDense", "glorot_uniform",
     "linrange_f32", "ChainRHS", "FisherKPPRHS", "fisher_kpp_laplacian", "layer_apply", "rhs_apply",
-    "Solution", "Tsit5Options", "solve", "Adam", "Trainer", "mse_loss", "reg_loss", "checkpoint", "tp",
+    "Solution", "Tsit5Options", "solve", "Adam", "FusedAdam", "Trainer", "mse_loss", "reg_loss", "checkpoint", "tp",
     "GridShardedChainRHS",
 ]

@@ -88,9 +88,10 @@ OPT_GRID_RHS = 5
 OPT_GRID_VJP = 6
 OPT_GRID_ADJ_STEP = 7
 OPT_ADJ_STEP_ROWS = 8
+OPT_PAIR_VJP = 9
 OPTIONS = {"pointwise_table": OPT_POINTWISE_TABLE, "fused_step": OPT_FUSED_STEP, "fused_solve": OPT_FUSED_SOLVE,
            "fused_solve_cap": OPT_FUSED_SOLVE_CAP, "grid_rhs": OPT_GRID_RHS, "grid_vjp": OPT_GRID_VJP,
-           "grid_adj_step": OPT_GRID_ADJ_STEP, "adj_step_rows": OPT_ADJ_STEP_ROWS}
+           "grid_adj_step": OPT_GRID_ADJ_STEP, "adj_step_rows": OPT_ADJ_STEP_ROWS, "pair_vjp": OPT_PAIR_VJP}
 
 SIGNATURES = [
     ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),
@@ -120,6 +121,8 @@ SIGNATURES = [
     ("kanode_layer_forward", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
     ("kanode_layer_vjp", C.c_int, [_H, C.c_int32, _P, _P, _P, _P, _P, C.c_int64, _P]),
     ("kanode_edge_activations", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_adam_step", C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_double,
+                                   C.c_double, C.c_double, C.c_double, C.c_double, _P]),
 ]
 
 _lib = None

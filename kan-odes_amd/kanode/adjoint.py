@@ -58,6 +58,14 @@ def _rms2(x):
     return float((x.double() * x.double()).sum())
 
 
+def _gsum(f, *vals: float) -> float:
+    """Σ of the given local sums over the shards of a grid-sharded RHS (kanode.tp: f.reduce_sum,
+    one scalar all-reduce), or their plain sum."""
+    tot = float(sum(vals))
+    red = getattr(f, "reduce_sum", None)
+    return red(tot) if red is not None else tot
+
+
 def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, grads, opt: Tsit5Options):
     """(dL/du0, dL/dp) for L with ∂L/∂u(saveat[j]) = grads[j] (tensors or None)."""
     t0, tf = float(tspan[0]), float(tspan[1])
@@ -75,6 +83,7 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
     # tstops in τ: the interior saveat times, then the end
     stops = sorted(tf - ts for ts in jumps if t0 + eps < ts < tf - eps) + [T]
     n_lam, n_mu = lam.numel(), mu.numel()
+    ntot = _gsum(f, n_lam + n_mu)          # every shard's λ and μ entries (the norm is over all of them)
 
     def fz(tau, lam_):
         return _adj_rhs(f, p, rec, tf, tau, lam_, [], [])
@@ -85,14 +94,13 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
     if opt.adaptive:
         sl = opt.abstol + lam.abs() * opt.reltol
         sm = opt.abstol + mu.abs() * opt.reltol
-        ntot = n_lam + n_mu
-        d0 = math.sqrt((_rms2(lam / sl) + _rms2(mu / sm)) / ntot)
-        d1 = math.sqrt((_rms2(k1l / sl) + _rms2(k1m / sm)) / ntot)
+        d0 = math.sqrt(_gsum(f, _rms2(lam / sl), _rms2(mu / sm)) / ntot)
+        d1 = math.sqrt(_gsum(f, _rms2(k1l / sl), _rms2(k1m / sm)) / ntot)
         h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
         h0 = min(h0, T)
         k2l, k2m = fz(h0, lam + h0 * k1l)
         nf += 1
-        d2 = math.sqrt((_rms2((k2l - k1l) / sl) + _rms2((k2m - k1m) / sm)) / ntot) / h0
+        d2 = math.sqrt(_gsum(f, _rms2((k2l - k1l) / sl), _rms2((k2m - k1m) / sm)) / ntot) / h0
         mx = max(d1, d2)
         h1 = max(1e-6, h0 * 1e-3) if mx <= 1e-15 else (0.01 / mx) ** (1.0 / 5.0)
         h = min(100 * h0, h1, T)
@@ -129,7 +137,7 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
         if opt.adaptive:
             emu = sum((h * b) * k.double() for b, k in zip(BTILDE, km))        # norms in double
             skm = opt.abstol + torch.maximum(mu.abs(), mu_new.abs()).double() * opt.reltol
-            EEst = math.sqrt((sumsq.item() + _rms2(emu / skm)) / (n_lam + n_mu))
+            EEst = math.sqrt(_gsum(f, sumsq.item(), _rms2(emu / skm)) / ntot)
             q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
             if EEst > 1.0 and h > opt.dtmin:
                 nreject += 1

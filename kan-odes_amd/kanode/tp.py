@@ -13,7 +13,11 @@ split over the R ranks of a process group, rank r owns the grid points [a_r, b_r
   * layer 2's output rows C2[a_r:b_r, :, :], W2[a_r:b_r, :] -> du[a_r:b_r] as a
     KDense(H -> n_r) launch.
 The pullback mirrors it: layer-2 VJP (local dC2/dW2 rows) -> all_reduce(SUM) of the [H, B]
-hidden cotangent partials -> layer-1 VJP (local dC1/dW1 columns, local ū slice).  Every
+hidden cotangent partials -> layer-1 VJP (local dC1/dW1 columns, local ū slice).  As an
+InterpolatingAdjoint stage (`vjp_stage`, the reference's NeuralODE default sensealg,
+Burgers_Surrogate.jl:97) that is: layer-1 forward at the interpolated state -> all_reduce of
+the [H, B] partials -> layer-2 VJP -> all_reduce of the [H, B] hidden cotangents -> layer-1 VJP,
+two 10·B-value collectives per adjoint stage and no layer-2 forward.  Every
 parameter gradient is therefore shard-local: d(Σ_r L_r)/dp_r lands on the rank owning p_r,
 and no gradient all-reduce is needed across the grid shards (a data-parallel group over
 trajectories, if any, still all-reduces its gradients in Trainer).  The adaptive step
@@ -140,3 +144,43 @@ class GridShardedChainRHS:
         hpart = self.layer_fn(0, p[:self.P1], u)                  # (B, H) partial pre-activation
         h = _AllReduceSum.apply(hpart, self._allreduce)           # one [H, B] all-reduce per RHS
         return self.layer_fn(1, p[self.P1:], h)                   # (B, n_r): own rows of du
+
+    def _layer_vjp(self, l: int, pl: torch.Tensor, x: torch.Tensor, g: torch.Tensor):
+        """(x̄, p̄_l) of one layer: kanode_layer_vjp on the default handle; through autograd on the
+        layer_fn override otherwise."""
+        if hasattr(self, "_hd"):
+            return self._hd.layer_vjp(l, pl.contiguous(), x.contiguous(), g.contiguous())
+        with torch.enable_grad():
+            x_ = x.detach().requires_grad_(True)
+            p_ = pl.detach().requires_grad_(True)
+            xb, pb = torch.autograd.grad(self.layer_fn(l, p_, x_), [x_, p_], g)
+        return xb, pb
+
+    def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
+        """InterpolatingAdjoint stage on the grid shard (kanode/adjoint.py; the statement of
+        kanode_vjp_stage): y = u + Σ c_j k_j, λs = λ + Σ lc_j lk_j (both local slices), returns this
+        rank's λsᵀ∂f/∂u rows and its parameters' λsᵀ∂f/∂p.  `error` receives this shard's Σ (e/sk)²;
+        the adjoint driver sums it over the shards (reduce_sum) with the μ part."""
+        y = u
+        for cj, kj in zip(c, ks):
+            y = torch.addcmul(y, kj, torch.full_like(kj, cj))
+        ls = lam
+        for cj, kj in zip(lc, lks):
+            ls = torch.addcmul(ls, kj, torch.full_like(kj, cj))
+        p1, p2 = p[:self.P1], p[self.P1:]
+        with torch.no_grad():
+            h = self._allreduce(self.layer_fn(0, p1, y).contiguous())            # forward to the hidden layer
+        hbar, dp2 = self._layer_vjp(1, p2, h, ls)
+        hbar = self._allreduce(hbar.contiguous())                                 # Σ over the output shards
+        lamJ, dp1 = self._layer_vjp(0, p1, y, hbar)
+        if lam_out is not None:
+            lam_out.copy_(ls)
+        if error is not None:
+            ec, abstol, reltol, sumsq = error
+            e = torch.zeros_like(lam)
+            for ej, kj in zip(ec[:-1], lks):
+                e = e + ej * kj
+            e = e + ec[-1] * lamJ
+            sk = abstol + reltol * torch.maximum(lam.abs(), ls.abs())
+            sumsq.fill_(float(((e / sk).double() ** 2).sum()))
+        return lamJ, torch.cat([dp1.reshape(-1), dp2.reshape(-1)])

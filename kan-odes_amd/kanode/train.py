@@ -2,7 +2,9 @@
 
     Adam        — Flux 0.14 legacy `Adam(η, β=(0.9,0.999), ϵ=1e-8)` + `update!`
                   (LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:167,201;
-                  Flux pinned at Lotka-Volterra/Manifest.toml:841)
+                  Flux pinned at Lotka-Volterra/Manifest.toml:841): the torch statement
+    FusedAdam   — the same step as ONE HIP launch (kanode_adam_step) with the post-all-reduce
+                  mean folded in; what Trainer uses on the GPU
     mse_loss    — `mean(abs2, X .- pred)` (LV_driver_KANODE.jl:197-203, Fisher-KPP_Source.jl:107-109)
     reg_loss    — L1 + entropy on the flat p (LV_driver_KANODE.jl:187-194)
     Trainer     — one iteration = forward Tsit5 solve, loss, discrete adjoint
@@ -43,6 +45,35 @@ class Adam:
         """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ)."""
         with torch.no_grad():
             x.sub_(self.apply(x, d))
+
+
+class FusedAdam(Adam):
+    """Adam whose step is one kanode_adam_step launch on x's device (m, v device-resident, Flux's
+    running powers βp kept on the host).  update(x, g, scale) applies Δ = scale·g: Trainer passes the
+    SUM all-reduced gradient with scale = 1/world_size, so the mean, both moments and x -= Δ are one
+    pass over the parameters instead of ~8 torch launches."""
+
+    def update(self, x: torch.Tensor, d: torch.Tensor, scale: float = 1.0) -> None:
+        from . import _lib as L
+        if not x.is_cuda:
+            raise L.KanodeError("FusedAdam runs on the GPU (kanode_adam_step); use kanode.Adam on the CPU")
+        if x.dtype not in (torch.float32, torch.float64) or d.dtype != x.dtype or d.numel() < x.numel():
+            raise L.KanodeError("FusedAdam: x and the gradient must share a float dtype and size")
+        if not (x.is_contiguous() and d.is_contiguous()):
+            raise L.KanodeError("FusedAdam: x and the gradient must be contiguous")
+        b1, b2 = self.beta
+        st = self.state.get(id(x))
+        if st is None:
+            st = [torch.zeros_like(x), torch.zeros_like(x), [b1, b2]]
+            self.state[id(x)] = st
+        mt, vt, bp = st
+        dt = L.F64 if x.dtype == torch.float64 else L.F32
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        L.check(L.lib().kanode_adam_step(x.data_ptr(), mt.data_ptr(), vt.data_ptr(), d.data_ptr(), x.numel(), dt,
+                                         float(scale), float(self.eta), float(b1), float(b2), float(self.eps),
+                                         float(bp[0]), float(bp[1]), stream), None, "kanode_adam_step")
+        bp[0] *= b1
+        bp[1] *= b2
 
 
 def mse_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
@@ -95,7 +126,7 @@ class Trainer:
         self.rhs, self.u0, self.tspan, self.saveat, self.target = rhs, u0, tspan, saveat, target
         self.tp = tp
         self.p = p0.detach().clone()
-        self.opt = Adam(eta)
+        self.opt = FusedAdam(eta) if self.p.is_cuda else Adam(eta)
         self.solver = solver or Tsit5Options()
         self.sparse_reg = sparse_reg
         self.group = group
@@ -123,14 +154,18 @@ class Trainer:
         loss, g, _ = self.loss_and_grad()
         if self.tp:
             loss = torch.as_tensor(self.rhs.reduce_sum(float(loss)), dtype=g.dtype)
+        scale = 1.0
         if self.group is not None:
             import torch.distributed as dist
             ws = dist.get_world_size(self.group)
-            buf = torch.cat([g.reshape(-1), loss.reshape(1).to(g.dtype)])   # one collective per step
+            buf = torch.cat([g.reshape(-1), loss.reshape(1).to(device=g.device, dtype=g.dtype)])   # one collective per step
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
-            buf /= ws
-            g, loss = buf[:-1].reshape(g.shape), buf[-1]
-        self.opt.update(self.p, g)
+            scale = 1.0 / ws
+            g, loss = buf[:-1].reshape(g.shape), buf[-1] * scale
+        if isinstance(self.opt, FusedAdam):
+            self.opt.update(self.p, g.contiguous(), scale)      # the mean is formed inside the launch
+        else:
+            self.opt.update(self.p, g * scale if scale != 1.0 else g)
         lv = float(loss)
         self.history.append(lv)
         return lv

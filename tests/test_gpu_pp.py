@@ -167,6 +167,100 @@ def test_table_vjp_matches_oracle(nx, normalizer, G):
     assert_close(lamJ, lamJ2.cpu().numpy(), vjp_scales(p, D, dx, u, lam), 2 * RTOL[torch.float64], "table vs rec")
 
 
+def kan_vjp_scales(spec, p, u, lam):
+    """Σ|terms| scales of the D = 0 pullback (utils.jl:15-21, kdense.jl:116-124), every factor taken
+    as the sum of the magnitudes of the terms it is computed from, so that a factor that cancels
+    (N' = 1 - tanh² at |u| = 6 is 2.5e-5, swish' = σ + uσ(1-σ) crosses zero at u = -1.28, 1 - tanh²(y)
+    of rswaf far from a knot) is scaled by its rounding floor rather than by its tiny value:
+      λᵀJ:  |λ|·(Σ_j |C_j|·S(∂φ_j/∂n)·S(N') + |W|·S(swish'))
+            S(∂φ_j/∂n) = 2(|n| + |g_j|)(1/h)²φ_j (rbf: -2yφ/h, y = (n - g_j)/h)
+                       = 2|tanh y|(1 + tanh² y)/h (rswaf)
+            S(N') = 1 + tanh² (tanh, tanh_fast), σ + σ² (sigmoid), 1/(1+|u|)² (softsign), 1 (identity)
+            S(swish') = σ + |u|σ(1 + σ)
+      dp_j: Σ_points |λ|·S(φ_j) with S = φ_j (rbf), 1 + tanh² y (rswaf); dp_W: Σ |λ||u|σ.
+    Where nothing cancels this is the KAN-derivative scale Σ|C_j ∂φ_j/∂u| + |W||swish'| itself."""
+    g = O.knots(spec).astype(np.float64)
+    ih = float(O.inv_h(spec))
+    x = u.ravel()
+    n = np.array([O.act(spec.normalizer, v) for v in x])
+    sig = 0.5 * (1.0 + np.tanh(0.5 * x))
+    if spec.normalizer in ("tanh", "tanh_fast"):
+        sN = 1.0 + n * n
+    elif spec.normalizer in ("sigmoid", "sigmoid_fast"):
+        sN = n + n * n
+    elif spec.normalizer == "softsign":
+        sN = 1.0 / (1.0 + np.abs(x)) ** 2
+    else:
+        sN = np.ones_like(x)
+    sSw = sig + np.abs(x) * sig * (1.0 + sig)
+    y = (n[:, None] - g[None, :]) * ih
+    if spec.basis == "rbf":
+        phi = np.exp(-y * y)
+        dphi = 2.0 * (np.abs(n)[:, None] + np.abs(g)[None, :]) * ih * ih * phi
+        sphi = phi
+    else:
+        th = np.tanh(y)
+        dphi = 2.0 * np.abs(th) * (1.0 + th * th) * ih
+        sphi = 1.0 + th * th
+    al = np.abs(lam).ravel()
+    sJ = al * (np.sum(np.abs(p[:-1])[None, :] * dphi, 1) * sN + abs(p[-1]) * sSw)
+    sdp = np.concatenate([al @ sphi, [al @ (np.abs(x) * sig)]])
+    return sJ.reshape(u.shape), sdp
+
+
+# The λᵀJ bar of VERDICT r2 #2: 1e-14 of the KAN-derivative scale (D = 0 removes the Laplacian
+# term that dominated the earlier D = 0.01 scales, so the φ'/swish' evaluation itself is pinned).
+# Measured r3 against |λ|(Σ|C_j ∂φ_j/∂u| + |W||swish'|) taken literally: ≤ 0.8 of the bar except at
+# the cancellations kan_vjp_scales lists (up to 80×: u = -6 under tanh, the zero of swish'),
+# tools/diag/vjp_sweep_diag.py, profiles/r03/parity/vjp_sweep_diag.txt.
+VJP_KAN_RTOL = 1e-14
+TABLE_VJP = [("softsign", "rbf", 10), ("tanh_fast", "rbf", 10), ("softsign", "rbf", 5), ("tanh_fast", "rbf", 5)]
+
+
+@pytest.mark.parametrize("G", [2, 5, 10, 32])
+@pytest.mark.parametrize("basis", ["rbf", "rswaf"])
+@pytest.mark.parametrize("normalizer", ["softsign", "tanh_fast", "tanh", "sigmoid", "sigmoid_fast", "identity"])
+def test_vjp_kan_part_dense_sweep(normalizer, basis, G):
+    """D = 0: λᵀJ = λ·φ'(u) exactly, over the sweep() points (every table interval edge and its
+    float neighbours, ±L, 0, ±1e-300, out-of-range values).  The table VJP
+    (fk_vjp_pp_wave_kernel: rbf, G = 5/10, softsign/tanh_fast) and the per-point kernel (every other
+    configuration) against the oracle pullback; dp against Σ|λ φ_j| at 1e-13."""
+    rng = np.random.default_rng(G * 7 + len(normalizer) * 3 + len(basis))
+    spec = O.LayerSpec(1, 1, G, normalizer, basis)
+    p = rng.uniform(-1, 1, G + 1)
+    u = sweep()
+    lam = rng.normal(size=u.shape)
+    rhs = rhs_for(256, normalizer, G, basis)
+    lamJ, dp = rhs.vjp(t(u), t(p), t(lam))
+    rJ, rdp = O.fk_vjp(spec, p, 0.0, 0.01, u, lam)
+    sJ, sdp = kan_vjp_scales(spec, p, u, lam)
+    assert_close(lamJ, rJ, sJ, VJP_KAN_RTOL, f"lamJ {normalizer}/{basis}/G={G}")
+    assert_close(dp, rdp, sdp, 1e-13, "dp")
+
+
+@pytest.mark.parametrize("normalizer,basis,G", TABLE_VJP)
+def test_vjp_stage_kan_part_dense_sweep(normalizer, basis, G):
+    """The adjoint-stage variant (fk_vjp_pp_wave_kernel<..., STG = true>: stage inputs formed in
+    registers, λ error fused) on a D = 0 handle over the same sweep, at the same bar.  The stage
+    arrays are zero, so y = u and λs = λ exactly and the oracle sees the same points."""
+    rng = np.random.default_rng(G + 3 * len(normalizer))
+    spec = O.LayerSpec(1, 1, G, normalizer, basis)
+    p = rng.uniform(-1, 1, G + 1)
+    u = sweep()
+    lam = rng.normal(size=u.shape)
+    rhs = rhs_for(256, normalizer, G, basis)
+    assert rhs.hd.pointwise_table
+    ut, lt = t(u), t(lam)
+    zeros = [torch.zeros_like(ut) for _ in range(4)]
+    lam_out = torch.empty_like(lt)
+    lamJ, dp = rhs.vjp_stage(ut, t(p), zeros, [0.1, 0.2, 0.3, 0.4], lt, zeros[:3], [0.5, 0.6, 0.7], lam_out)
+    assert torch.equal(lam_out, lt)
+    rJ, rdp = O.fk_vjp(spec, p, 0.0, 0.01, u, lam)
+    sJ, sdp = kan_vjp_scales(spec, p, u, lam)
+    assert_close(lamJ, rJ, sJ, VJP_KAN_RTOL, f"stage lamJ {normalizer}/G={G}")
+    assert_close(dp, rdp, sdp, 1e-13, "stage dp")
+
+
 def test_table_vjp_nonfinite_and_reproducible():
     rng = np.random.default_rng(21)
     nx, D, dx = 256, 0.01, 1.0 / 255
@@ -216,3 +310,33 @@ def test_table_stamp_tracks_parameter_changes_in_place():
     p.copy_(p_bit)
     d2 = rhs.rhs(ut, p)
     assert not torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("use_base", [True, False])
+def test_table_stamp_sees_a_change_of_w_alone(use_base):
+    """the stamp compares p[G] (W) only when the layer has the base term; an in-place change
+    of W alone must rebuild both tables, and a layer without the base term (P = G, stamp[G] compared
+    against 0) must still track changes of C."""
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", use_base_act=use_base))
+    rhs = kanode.FisherKPPRHS(kan1, nx=256, dx=1.0 / 255, D=0.01, device=device())
+    assert rhs.hd.pointwise_table
+    spec = O.LayerSpec(1, 1, 10, "softsign", use_base_act=use_base)
+    rng = np.random.default_rng(31)
+    u = rng.uniform(-1.5, 1.5, (4, 256))
+    lam = rng.normal(size=u.shape)
+    P = 11 if use_base else 10
+    p = t(rng.uniform(-1, 1, P))
+    p1 = p.clone()
+    p2 = p1.clone()
+    p2[P - 1] = p2[P - 1] * -1.7          # W alone (use_base) or the last C (no base term)
+    for pv in (p1, p2, p1):
+        p.copy_(pv)
+        du = rhs.rhs(t(u), p)
+        lamJ, dp = rhs.vjp(t(u), p, t(lam))
+        pn = pv.cpu().numpy()
+        ref = O.fk_rhs(spec, pn, 0.01, 1.0 / 255, u)
+        rJ, rdp = O.fk_vjp(spec, pn, 0.01, 1.0 / 255, u, lam)
+        scale = np.max(np.abs(ref)) + 4 * 0.01 * 255 ** 2
+        assert np.max(np.abs(du.cpu().numpy() - ref)) <= 1e-13 * scale
+        assert np.max(np.abs(lamJ.cpu().numpy() - rJ)) <= 1e-12 * (np.max(np.abs(rJ)) + 4 * 0.01 * 255 ** 2)
+        assert np.max(np.abs(dp.cpu().numpy() - rdp)) <= 1e-11 * np.max(np.abs(rdp))

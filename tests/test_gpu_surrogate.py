@@ -156,3 +156,41 @@ def test_surrogate_pair_stages_form_their_inputs_in_the_wide_in_kernel(N, G, B):
     dp0 = t(rng.normal(size=p.shape))
     _, dp2 = hd.vjp_stage(p, u, ks, c, lam, lks, lc, dp=dp0.clone())
     assert (dp2 - (dp0 + dp_ref)).abs().max().item() <= 1e-15 * (dp0.abs() + dp_ref.abs()).max().item()
+
+
+@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (2048, 10, 8), (300, 7, 11), (512, 5, 200), (41, 5, 2)])
+def test_pair_vjp_two_launches_equal_four(N, G, B):
+    """KANODE_OPT_PAIR_VJP: the surrogate pullback in two launches (the wide-out dot products beside
+    the wide-in forward; the wide-out parameter cotangents beside the wide-in pullback, which forms the
+    hidden layer's cotangent per block) is bitwise equal to the four-launch path, for the plain VJP and
+    for an adjoint stage (stage inputs formed in the kernels, dp assigned / accumulated)."""
+    rng = np.random.default_rng(7 * N + G + B)
+    specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+    p = t(_glorot_params(rng, specs))
+    hd = kanode.KanodeHandle(cfgs_from_specs(specs), dtype=torch.float64, rhs_kind="chain", device=device())
+    assert hd.get_option("pair_vjp") == 1
+    u = t(rng.uniform(-1, 1, (B, N)))
+    lam = t(rng.normal(size=(B, N)))
+    ks = [t(rng.normal(size=(B, N)) * 0.1) for _ in range(7)]
+    c = [0.01 * w for w in kanode.ode.interp_weights(0.4)]
+    lks = [t(rng.normal(size=(B, N))) for _ in range(5)]
+    lc = [0.02 * a for a in kanode.ode.A[4]]
+    dp0 = t(rng.normal(size=p.shape))
+    out = {}
+    for pair in (1, 0):
+        with hd.options(pair_vjp=pair):
+            lamJ, dp = hd.vjp(p, u, lam)
+            ls = torch.empty_like(u)
+            sJ, sdp = hd.vjp_stage(p, u, ks, c, lam, lks, lc, lam_out=ls)
+            _, sdp2 = hd.vjp_stage(p, u, ks, c, lam, lks, lc, dp=dp0.clone())
+            out[pair] = (lamJ, dp, sJ, sdp, ls, sdp2)
+    for a, b in zip(out[1], out[0]):
+        assert torch.equal(a, b)
+    # and against the oracle at the stage inputs (the four-launch path's own parity)
+    y = u.clone()
+    for cj, kj in zip(c, ks):
+        y = torch.addcmul(y, kj, torch.full_like(kj, cj))
+    rJ, rdp = O.chain_vjp(specs, p.cpu().numpy(), y.cpu().numpy(), out[1][4].cpu().numpy())
+    xs, ps = O.chain_vjp(specs, np.abs(p.cpu().numpy()), y.cpu().numpy(), np.abs(out[1][4].cpu().numpy()))
+    assert_close(out[1][2], rJ, np.abs(xs) * 1e2 + np.max(np.abs(xs)) * 1e-2, RTOL[torch.float64], "stage lamJ")
+    assert_close(out[1][3], rdp, np.abs(ps) * 1e2 + np.max(np.abs(ps)) * 1e-2, RTOL[torch.float64], "stage dp")

@@ -1,0 +1,103 @@
+"""The fused optimiser step (kanode_adam_step, kan_optim.hip) against Flux's Adam formula
+(LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:167,201; Flux 0.14 legacy Optimise.Adam, restated)
+and against kanode.Adam (the torch statement), and the Trainer that uses it."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import device, t
+
+import kanode
+
+pytestmark = pytest.mark.gpu
+
+
+def flux_adam(x, grads, eta, scale, dtype=np.float64, b1=0.9, b2=0.999, eps=1e-8):
+    """Flux's apply!/update! in float64 numpy (Float64 hyper-parameters promote a Float32 x; the
+    results are rounded on store)."""
+    x = x.astype(dtype).copy()
+    m = np.zeros_like(x)
+    v = np.zeros_like(x)
+    bp1, bp2 = b1, b2
+    for g in grads:
+        d = g.astype(dtype).astype(np.float64) * scale
+        m = (b1 * m.astype(np.float64) + (1 - b1) * d).astype(dtype)
+        v = (b2 * v.astype(np.float64) + ((1 - b2) * d) * d).astype(dtype)
+        step = m.astype(np.float64) / (1 - bp1) / (np.sqrt(v.astype(np.float64) / (1 - bp2)) + eps) * eta
+        x = (x.astype(np.float64) - step).astype(dtype)
+        bp1 *= b1
+        bp2 *= b2
+    return x
+
+
+@pytest.mark.parametrize("n", [11, 240, 450_561])      # FK, LV and the SC1024 parameter vector
+def test_fused_adam_matches_flux_formula_fp64(n):
+    rng = np.random.default_rng(n)
+    x0 = rng.normal(size=n)
+    grads = [rng.normal(size=n) * 10.0 ** rng.uniform(-6, 2, n) for _ in range(6)]
+    ref = flux_adam(x0, grads, 1e-2, 0.5)
+    x = t(x0)
+    opt = kanode.FusedAdam(1e-2)
+    for g in grads:
+        opt.update(x, t(g), 0.5)
+    got = x.cpu().numpy()
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)) <= 1e-15
+    # the torch statement of the same step (8 elementwise launches) on the same device
+    xs = t(x0)
+    slow = kanode.Adam(1e-2)
+    for g in grads:
+        slow.update(xs, t(g) * 0.5)
+    assert (x - xs).abs().max().item() <= 1e-15 * xs.abs().max().item()
+
+
+def test_fused_adam_fp32_promotes_like_flux():
+    """LV4k trains Float32 parameters: Flux's Float64 hyper-parameters promote each broadcast, which
+    is rounded to Float32 on store; the kernel does the same."""
+    rng = np.random.default_rng(3)
+    x0 = rng.normal(size=240).astype(np.float32)
+    grads = [rng.normal(size=240).astype(np.float32) for _ in range(4)]
+    ref = flux_adam(x0, grads, 1e-3, 1.0, dtype=np.float32)
+    x = t(x0, torch.float32)
+    opt = kanode.FusedAdam(1e-3)
+    for g in grads:
+        opt.update(x, t(g, torch.float32))
+    got = x.cpu().numpy()
+    assert np.max(np.abs(got.astype(np.float64) - ref) / np.abs(ref)) <= 1.2e-7     # one float32 ulp
+
+
+def test_fused_adam_rejects_bad_arguments():
+    opt = kanode.FusedAdam(1e-3)
+    with pytest.raises(kanode.KanodeError):
+        opt.update(torch.zeros(4, dtype=torch.float64), torch.zeros(4, dtype=torch.float64))   # CPU tensor
+    with pytest.raises(kanode.KanodeError):
+        opt.update(t(np.zeros(4)), t(np.zeros(4), torch.float32))
+    lib = kanode.lib()
+    x = t(np.zeros(4))
+    p = x.data_ptr()
+    assert lib.kanode_adam_step(p, p, p, p, -1, 1, 1.0, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, None) != 0
+    assert lib.kanode_adam_step(p, p, p, p, 4, 1, 1.0, 1e-3, 1.0, 0.999, 1e-8, 1.0, 0.999, None) != 0
+    assert lib.kanode_adam_step(p, p, p, p, 0, 1, 1.0, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, None) == 0
+
+
+def test_trainer_uses_fused_adam_and_matches_torch_adam():
+    """Trainer.step on the GPU (Fisher-KPP, native solve + InterpolatingAdjoint) takes the fused step;
+    three steps give the parameters the torch Adam statement gives."""
+    nx, B = 256, 4
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=1.0 / (nx - 1), D=0.01, device=device())
+    x = np.arange(nx) / (nx - 1)
+    u0 = t(np.stack([(np.tanh((x - c) / 0.02) - np.tanh((x - c - 0.2) / 0.02)) / 2 for c in (0.3, 0.35, 0.4, 0.45)]))
+    ts = [0.0, 0.05, 0.1]
+    opt = kanode.Tsit5Options(adaptive=False, dt=5e-4)
+    ptrue = t(np.random.default_rng(1).uniform(-0.5, 0.5, 11))
+    target = kanode.solve(rhs, u0, (0.0, 0.1), ptrue, ts, opt).u
+    p0 = ptrue * 1.2
+    fused = kanode.Trainer(rhs, u0, (0.0, 0.1), ts, target, p0, eta=1e-2, solver=opt)
+    assert isinstance(fused.opt, kanode.FusedAdam)
+    slow = kanode.Trainer(rhs, u0, (0.0, 0.1), ts, target, p0, eta=1e-2, solver=opt)
+    slow.opt = kanode.Adam(1e-2)
+    for _ in range(3):
+        la, lb = fused.step(), slow.step()
+        assert la == lb
+    assert (fused.p - slow.p).abs().max().item() <= 1e-15 * slow.p.abs().max().item()
+    assert fused.history[-1] < fused.history[0]

@@ -55,3 +55,85 @@ def test_mirrored_structs_match_the_header():
                 assert jt.startswith("NTuple{"), (jname, n, jt)
             else:
                 assert C2JL[ct] == jt, (jname, n, ct, jt)
+
+
+def _strip(src):
+    """Julia source without comments, docstrings and string literals (for structural checks)."""
+    src = re.sub(r'"""[\s\S]*?"""', '""', src)
+    src = re.sub(r'"(?:\\.|[^"\\])*"', '""', src)
+    return "\n".join(line.split("#", 1)[0] for line in src.splitlines())
+
+
+def _functions(src):
+    """name -> body of every `function name(...) ... end` block (top level, indentation 0)."""
+    out = {}
+    for m in re.finditer(r"^function ([\w.]+)\(.*?^end\b", src, flags=re.S | re.M):
+        out.setdefault(m.group(1), []).append(m.group(0))
+    return out
+
+
+def test_blocks_balance():
+    """Every block opener has its `end` (Julia is absent, so this stands in for the parser): `end`
+    inside an index expression (x[end]) is not counted."""
+    s = _strip(JL)
+    while True:
+        t = re.sub(r"\[[^\[\]]*\]", "[]", s)
+        if t == s:
+            break
+        s = t
+    s = re.sub(r"\bmutable struct\b", "struct", s)
+    # block keywords open a statement (line start); generator `for`s inside calls and short-circuit
+    # guards (`cond || throw(...)`) open nothing; `do` opens a block wherever it stands
+    openers = len(re.findall(r"^\s*(?:function|struct|module|if|for|while|let|begin|try|quote|macro)\b", s, re.M))
+    openers += len(re.findall(r"\bdo\b", s))
+    assert openers == len(re.findall(r"\bend\b", s))
+    assert s.count("(") == s.count(")")
+
+
+def test_enum_values_match_the_header():
+    def enum(prefix):
+        return {m.group(1).lower(): int(m.group(2)) for m in re.finditer(prefix + r"(\w+)\s*=\s*(\d+)", HDR)}
+    norm, basis = enum("KANODE_NORM_"), enum("KANODE_BASIS_")
+    jl_norm = dict(re.findall(r":(\w+) => (\d+)", re.search(r"const NORM = Dict\((.*?)\)\n", JL, re.S).group(1)))
+    jl_basis = dict(re.findall(r":(\w+) => (\d+)", re.search(r"const BASIS = Dict\((.*?)\)\n", JL, re.S).group(1)))
+    for k, v in norm.items():
+        assert int(jl_norm[k]) == v, k
+    for k, v in basis.items():
+        assert int(jl_basis[k]) == v, k
+    assert "Float32 => Int32(0)" in JL and "Float64 => Int32(1)" in JL     # kanode_dtype
+
+
+def test_lux_and_chainrules_surface():
+    """Lux.setup on the layer must give the reference axes (initialparameters /
+    initialstates / parameterlength / statelength), and the layer, the Fisher-KPP RHS and the device
+    solve must each carry an rrule."""
+    s = _strip(JL)
+    for pat in (r"function LuxCore\.initialparameters\(rng::AbstractRNG, l::KANChainHip\)",
+                r"function LuxCore\.initialstates\(::AbstractRNG, l::KANChainHip\)",
+                r"LuxCore\.parameterlength\(l::KANChainHip\)",
+                r"LuxCore\.statelength\(l::KANChainHip\)",
+                r"ChainRulesCore\.rrule\(l::KANChainHip,",
+                r"ChainRulesCore\.rrule\(f::RCKanodeHip,",
+                r"ChainRulesCore\.rrule\(::typeof\(solve_tsit5\),",
+                r"glorot_uniform\(rng, Int\(s\.out_dims\), Int\(s\.grid_len\) \* Int\(s\.in_dims\)\)",
+                r"Symbol\(\"layer_\", i\)"):
+        assert re.search(pat, JL), pat
+    # layerspec passes every kanode_layer_spec choice through, and the handle takes Float32
+    m = re.search(r"function layerspec\((.*?)\)\n", s, re.S)
+    for kw in ("normalizer", "basis_func", "use_base_act", "grid_lims", "denominator", "iqf_reference_quirk"):
+        assert kw in m.group(1), kw
+    assert re.search(r"function Handle\(ls::Vector\{LayerSpec\}; T::Type", s)
+
+
+def test_every_kernel_call_checks_its_sizes():
+    """The C side trusts the sizes it is given: each Julia entry that hands host arrays to the
+    library checks length(p) == kanode_param_length and the state rows before the ccall."""
+    fns = _functions(_strip(JL))
+    for name, sym in (("rhs", "kanode_rhs_host"), ("vjp", "kanode_vjp_host"), ("solve_impl", None)):
+        body = fns[name][0]
+        assert "checkp(h, p)" in body and "checku(h, " in body, name
+        if sym:
+            assert body.index("checkp(h, p)") < body.index(sym), name
+    assert "solve_impl(" in fns["solve_tsit5"][0]
+    checkp = fns["checkp"][0]
+    assert "length(p) == h.P" in checkp and "DimensionMismatch" in checkp

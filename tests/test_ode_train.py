@@ -98,3 +98,40 @@ def test_checkpoint_roundtrip(tmp_path):
     d = kanode.checkpoint.load(path)
     assert np.array_equal(d["p"], P[-1]) and len(d["p_list"]) == 3
     assert d["loss"].tolist() == [3.0, 2.0, 1.0] and d["size_KAN"].tolist() == [2.0, 10.0, 5.0]
+
+
+def test_reg_loss_matches_driver_formula():
+    """reg_loss (LV_driver_KANODE.jl:187-194): L1 activation loss + entropy of |p|/Σ|p|, and the
+    driver's call shape reg_loss(p, 5e-4, 0) (:200, sparse_on = 1) that adds only the scaled L1 term."""
+    rng = np.random.default_rng(0)
+    p = rng.normal(size=240)
+    l1 = np.abs(p)
+    a = l1.sum()
+    e = l1 / a
+    ref = a * 0.7 + (-(e * np.log(e)).sum()) * 0.3
+    assert abs(kanode.reg_loss(torch.as_tensor(p), 0.7, 0.3).item() - ref) <= 1e-13 * abs(ref)
+    assert abs(kanode.reg_loss(torch.as_tensor(p)).item() - (a + -(e * np.log(e)).sum())) <= 1e-13 * a
+    pt = torch.as_tensor(p).requires_grad_(True)
+    r = kanode.reg_loss(pt, 5e-4, 0)
+    assert abs(r.item() - 5e-4 * a) <= 1e-15 * a
+    (g,) = torch.autograd.grad(r, [pt])
+    assert torch.equal(g, 5e-4 * torch.sign(torch.as_tensor(p)))
+    # an exact zero in p: 0·log(0) is NaN in Julia and in torch alike, and ·0 keeps it NaN
+    p[3] = 0.0
+    assert np.isnan(kanode.reg_loss(torch.as_tensor(p), 5e-4, 0).item())
+
+
+def test_trainer_sparse_reg_adds_the_l1_term():
+    """Trainer(sparse_reg = 5e-4) is the driver's loss(p) with sparse_on = 1 (:196-201): its gradient
+    is the plain loss gradient plus 5e-4·sign(p)."""
+    ptrue = torch.tensor([1.5, 1.0, 1.0, 3.0], dtype=torch.float64)
+    u0 = torch.tensor([1.0, 1.0], dtype=torch.float64)
+    ts = [0.1 * i for i in range(35)]
+    target = kanode.solve(lotka, u0, (0.0, 3.5), ptrue, saveat=ts,
+                          opt=kanode.Tsit5Options(abstol=1e-10, reltol=1e-10)).u
+    plain = kanode.Trainer(lotka, u0, (0.0, 3.5), ts, target, ptrue * 1.1)
+    reg = kanode.Trainer(lotka, u0, (0.0, 3.5), ts, target, ptrue * 1.1, sparse_reg=5e-4)
+    l0, g0, _ = plain.loss_and_grad()
+    l1, g1, _ = reg.loss_and_grad()
+    assert abs((l1 - l0).item() - 5e-4 * (ptrue * 1.1).abs().sum().item()) <= 1e-15
+    assert torch.allclose(g1 - g0, 5e-4 * torch.sign(ptrue), rtol=0, atol=1e-13)   # differences of O(1) gradients
