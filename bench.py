@@ -68,11 +68,30 @@ def load_traffic(workload: str, alg_bytes: float):
     return None
 
 
+def host_cpu():
+    """(model name, CPUs this process may run on, threads used).  The GPU box gives one GPU's job a
+    16-core share and exports OMP_NUM_THREADS=16 (nproc shows the whole machine), so the OpenMP
+    comparator uses OMP_NUM_THREADS when it is set and the affinity mask otherwise."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else visible
+    return model, visible, max(1, min(threads, visible))
+
+
 def cpu_baseline(nx, dx, D, p_np, target_s: float):
     """The faithful CPU restatement (oracle/cpu_bench.c) timed on this host."""
     from oracle import oracle as O
     spec = O.LayerSpec(1, 1, 10, "softsign")
-    threads = max(1, min(16, os.cpu_count() or 1))
+    model, visible, threads = host_cpu()
     rng = np.random.default_rng(123)
     B = 256
     x = np.arange(nx) * dx
@@ -90,7 +109,30 @@ def cpu_baseline(nx, dx, D, p_np, target_s: float):
         "sample": f"{B} trajectories x {reps} RHS evals, Nx={nx}, dense (D*lap)*u matvec + per-point "
                   f"KDense(1,1,10) (oracle/cpu_bench.c, OpenMP {threads} threads, {tm:.1f} s)",
         "single_core_value": 32 * 2 / t1s,
+        "cpu_model": model,
+        "cpus_visible": visible,
+        "threads_from": "OMP_NUM_THREADS (the box's 16-core share per GPU)" if os.environ.get("OMP_NUM_THREADS")
+                        else "sched_getaffinity",
     }
+
+
+def cpu_epoch(p_np, nx, dx, D, B_cpu, T, saveat, seed, eta, adaptive, dt, gpu_s, B_gpu):
+    """The epoch on the host, in C on one core (oracle/cpu_epoch.c): Tsit5 with dense output, MSE loss,
+    InterpolatingAdjoint, Adam, with the reference's dense Laplacian matvec in the RHS and its
+    transpose in the VJP.  No interpreter in the loop (tests/test_cpu_epoch.py pins it to the Python
+    statement of the same epoch)."""
+    from oracle import oracle as O
+    u0 = fk_ics(B_cpu, nx, dx, seed=seed, device="cpu").numpy()
+    target = 0.9 * np.broadcast_to(u0, (len(saveat), B_cpu, nx))
+    _, _, _, st, secs = O.fk_epoch(O.LayerSpec(1, 1, 10, "softsign"), p_np, D, dx, u0, T, saveat, target,
+                                   adaptive=adaptive, dt=dt, eta=eta)
+    model, _, _ = host_cpu()
+    return {"cpu": secs, "cpu_batch": B_cpu, "cpu_cores": 1, "cpu_model": model,
+            "cpu_kind": "port (oracle/cpu_epoch.c: C Tsit5 + InterpolatingAdjoint + Adam, dense Laplacian matvec "
+                        "+ scalar KAN, one core)",
+            "cpu_steps": [st["naccept"], st["adjoint_naccept"]],
+            "gpu_per_trajectory": gpu_s / B_gpu, "cpu_per_trajectory": secs / B_cpu,
+            "speedup_per_trajectory": (secs / B_cpu) / (gpu_s / B_gpu)}
 
 
 def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: float, reps: int, group=None,
@@ -133,19 +175,39 @@ def epoch_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, steps: int, dt: fl
                     "trajectories_per_s": B_gpu * world / gpu_s,
                     "collective": "one all_reduce(SUM) of [dL/dp ; L] (12 doubles) per epoch"})
     if B_cpu > 0:
-        from oracle import oracle as O
-        from oracle.oracle_rhs import OracleFKRHS
-        cpu_rhs = OracleFKRHS(O.LayerSpec(1, 1, 10, "softsign"), D, dx, dense=True)
-        u0c = fk_ics(B_cpu, nx, dx, seed=7, device="cpu")
-        tc = kanode.Trainer(cpu_rhs, u0c, (0.0, T), saveat, (0.9 * u0c).unsqueeze(0).expand(len(saveat), -1, -1)
-                            .contiguous(), torch.as_tensor(p_np), eta=1e-3, solver=solver)
-        t0 = time.perf_counter()
-        tc.step()
-        cpu_s = time.perf_counter() - t0
-        out.update({"cpu": cpu_s, "cpu_batch": B_cpu, "cpu_cores": 1,
-                    "cpu_kind": "port (oracle: dense Laplacian matvec + scalar KAN, C; torch CPU Tsit5 driver)",
-                    "gpu_per_trajectory": gpu_s / B_gpu, "cpu_per_trajectory": cpu_s / B_cpu,
-                    "speedup_per_trajectory": (cpu_s / B_cpu) / (gpu_s / B_gpu)})
+        out.update(cpu_epoch(p_np, nx, dx, D, B_cpu, T, saveat, 7, 1e-3, False, dt, gpu_s, B_gpu))
+    return out
+
+
+def epoch_adaptive_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, reps: int = 1):
+    """The reference's Fisher-KPP training epoch as written (Fisher-KPP_Source.jl:38-44,101-109,198-201):
+    T = 5, saveat every 0.5 (11 points), solve(prob, Tsit5()) at the default tolerances (abstol 1e-6,
+    reltol 1e-3, adaptive), the gradient by the InterpolatingAdjoint, one Adam step; here at Nx = 256
+    (the configs[2] grid) over B_gpu trajectories on the GPU (native solve + adjoint: one launch per
+    forward / adjoint step) and B_cpu on the CPU (cpu_epoch: C, one core)."""
+    T = 5.0
+    saveat = [0.5 * i for i in range(11)]
+    solver = kanode.Tsit5Options()
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev)
+    u0 = fk_ics(B_gpu, nx, dx, seed=17, device=dev)
+    target = (0.9 * u0).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+    tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, target, torch.as_tensor(p_np, device=dev), eta=1e-2, solver=solver)
+    tr.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    gpu_s = (time.perf_counter() - t0) / reps
+    _, _, sol = tr.loss_and_grad()
+    out = {"unit": "s/epoch", "gpu": gpu_s, "gpu_batch": B_gpu, "T": T, "saveat": 0.5, "abstol": 1e-6, "reltol": 1e-3,
+           "forward_steps": sol.stats["naccept"], "forward_rejects": sol.stats["nreject"],
+           "adjoint_steps": sol.stats["adjoint"]["naccept"], "adjoint_rejects": sol.stats["adjoint"]["nreject"],
+           "what": "adaptive Tsit5 solve (T=5, saveat 0.5, default tolerances) + InterpolatingAdjoint + Adam, "
+                   "FK256 fp64 (native kanode_solve_tsit5 + kanode_adjoint_tsit5)"}
+    if B_cpu > 0:
+        out.update(cpu_epoch(p_np, nx, dx, D, B_cpu, T, saveat, 17, 1e-2, True, 0.0, gpu_s, B_gpu))
     return out
 
 
@@ -202,9 +264,11 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     integrator statement in Python (kind "port"); Julia is not available to time the reference."""
     from scipy.integrate import solve_ivp
     ts = [0.1 * i for i in range(35)]
+    ts_test = [0.1 * i for i in range(141)]
     f = lambda t, x: [1.5 * x[0] - x[0] * x[1], x[0] * x[1] - 3.0 * x[1]]   # noqa: E731
-    target = solve_ivp(f, (0.0, 3.5), [1.0, 1.0], t_eval=ts, method="DOP853", rtol=1e-10,
-                       atol=1e-12).y.T[:, None, :]
+    full = solve_ivp(f, (0.0, 14.0), [1.0, 1.0], t_eval=ts_test, method="DOP853", rtol=1e-10,
+                     atol=1e-12).y.T[:, None, :]
+    target = full[:35]
     chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
     p0 = chain.setup(np.random.default_rng(0))[0].astype(np.float64) / 1e5 * 1e4   # a mid-training scale
     legs = [("gpu", dev, kanode.ChainRHS(chain, device=dev), reps)]
@@ -214,17 +278,28 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
         legs.append(("cpu", "cpu", OracleChainRHS([O.LayerSpec(2, 10, 5, "tanh_fast"),
                                                    O.LayerSpec(10, 2, 5, "tanh_fast")]), 2))
     out = {"unit": "ms/iteration", "batch": 1, "dtype": "f64",
-           "what": "adaptive Tsit5 solve + InterpolatingAdjoint + Adam, LV KAN [2,10,2] G=5, one trajectory"}
+           "what": "one LV_driver_KANODE.jl iteration (:283-291): adaptive Tsit5 solve + InterpolatingAdjoint "
+                   "+ Adam, then the loss_train (tspan_train, 35 saveat) and loss_test (tspan (0, 14), 141 "
+                   "saveat) forward solves, LV KAN [2,10,2] G=5, one trajectory"}
     for name, d, rhs, n in legs:
-        tr = kanode.Trainer(rhs, torch.tensor([[1.0, 1.0]], dtype=torch.float64, device=d), (0.0, 3.5), ts,
-                            torch.as_tensor(target, device=d), torch.as_tensor(p0, device=d), eta=1e-3,
-                            sensealg="interpolating_adjoint")
-        tr.step()
+        u0 = torch.tensor([[1.0, 1.0]], dtype=torch.float64, device=d)
+        tr = kanode.Trainer(rhs, u0, (0.0, 3.5), ts, torch.as_tensor(target, device=d), torch.as_tensor(p0, device=d),
+                            eta=1e-3, sensealg="interpolating_adjoint")
+        tgt_test = torch.as_tensor(full, device=d)
+
+        def iteration():
+            tr.step()
+            with torch.no_grad():
+                l_tr = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 3.5), tr.p, ts).u, tr.target)
+                l_te = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 14.0), tr.p, ts_test).u, tgt_test)
+            return float(l_tr), float(l_te)
+
+        iteration()
         if name == "gpu":
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(n):
-            tr.step()
+            iteration()
         if name == "gpu":
             torch.cuda.synchronize()
         out[name] = (time.perf_counter() - t0) / n * 1e3
@@ -425,6 +500,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vjp", action="store_true")
     ap.add_argument("--no-epoch", action="store_true")
+    ap.add_argument("--no-epoch-adaptive", action="store_true",
+                    help="skip the adaptive reference-problem epoch (T = 5, default tolerances)")
     ap.add_argument("--no-dist-surrogates", action="store_true",
                     help="skip the multi-rank configs[3]/[4] training legs (N > 1 only)")
     ap.add_argument("--epoch-batch", type=int, default=4096, help="trajectories in the training-epoch leg")
@@ -577,11 +654,14 @@ def main() -> None:
         out["surrogates"] = surrogate_bench(dev, world == 1 and not args.no_cpu_baseline)
 
     if not args.no_epoch:
-        ep = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch, 0 if (args.no_cpu_baseline or world > 1) else 8,
+        ep = epoch_bench(dev, p_np, nx, dx, D, args.epoch_batch, 0 if (args.no_cpu_baseline or world > 1) else 16,
                          args.epoch_steps, 1e-3, 3, group=tdist.group.WORLD if dist else None, rank=rank,
                          world=world)
         if rank == 0:
             out["epoch"] = ep
+        if rank == 0 and not args.no_epoch_adaptive:
+            out["epoch_adaptive"] = epoch_adaptive_bench(dev, p_np, nx, dx, D, args.epoch_batch,
+                                                         0 if (args.no_cpu_baseline or world > 1) else 2)
 
     if dist and not args.no_dist_surrogates:
         sd = surrogate_dist_bench(dev, rank, world, args.dist_backend)

@@ -38,7 +38,9 @@
  * batch, so they can be captured into a hipGraph.  *_host variants take host
  * pointers, stage through handle-owned device buffers and return after the
  * stream synchronises.  A handle is bound to one device, is NOT thread-safe,
- * and separate handles are independent.  `dp`/`pbar` ACCUMULATE (+=): the adjoint
+ * and separate handles are independent.  A handle's device calls must be stream-ordered: issue
+ * them on one stream at a time (the Fisher-KPP table kernels keep per-handle build state in device
+ * memory; kanode_reserve resets it).  `dp`/`pbar` ACCUMULATE (+=): the adjoint
  * integrates μ across stages, so zeroing is the caller's job.
  */
 #ifndef KANODE_H

@@ -570,6 +570,9 @@ constexpr int kChainMaxLayers = 4;
 template <typename T, int NORM, int PATH, class S = ChainShapeAny>
 __device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps,
                                             T* __restrict__ row, int j, T yj, T lj) {
+    // layer 0's basis cache (omc0) is filled by the forward loop below only when layer 0 is not the
+    // last layer: a one-layer output-major shape would read it uninitialised
+    static_assert(!(S::NL == 1 && out_major<S>(0)), "an output-major layer must not be the only layer");
     // forward: the input activation of every layer (lane j holds entry j)
     T act[kChainMaxLayers];
     act[0] = yj;

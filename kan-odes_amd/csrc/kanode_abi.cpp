@@ -896,6 +896,15 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch) {
             h->ws_bytes = need;
         }
     }
+    // Reset the table stamps: the build's skip protocol assumes each slot's arrival counter
+    // is 0 when a launch starts, which holds for stream-ordered launches of one handle; re-zeroing the
+    // stamp region here (the call before graph capture / a new batch) also clears what an aborted
+    // launch could have left, and invalidates the stamps, so the next launch rebuilds every table.
+    if (h->dtable) {
+        const int64_t off = (int64_t)kan::kPPMaxFns * kan::kPPCoef * h->hpc.ni;
+        HIP_TRY(h, hipDeviceSynchronize());
+        HIP_TRY(h, hipMemset(h->dtable + off, 0, sizeof(double) * (size_t)(kan::pp_tables_doubles(h->hpc.ni) - off)));
+    }
     h->reserved_batch = std::max(h->reserved_batch, max_batch);
     return KANODE_OK;
 }

@@ -908,7 +908,11 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         hstep = std::min(hstep, stops[si] - tau);
         const int nxt = cur ^ 1;
         bool fused_step = false;   // Fisher-KPP table path, Q-form dense output: the six stages in one launch
-        bool combined = false;     // fixed step: km[1] holds Σ_{j>=1} h·a6_j·kμ_{j+1} (kanode_internal_fk_adjoint_step)
+        // combined (fixed step, kanode_internal_fk_adjoint_step): the step's reduction launch reduces the
+        // stage moments through the combinations the step consumes and writes μ_new itself (AdjMuUpdate)
+        // and the FSAL kμ_7 into km[6]; km[1..5] are NOT written on such a step and hold stale values,
+        // so nothing may read them when `combined` is set
+        bool combined = false;
         if (s->qform) {
             kan::AdjStepArgs a{};
             for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];

@@ -1,0 +1,384 @@
+/*
+ * cpu_epoch.c — CPU BASELINE of one Fisher-KPP training epoch (test infrastructure only; called
+ * only by bench.py's epoch legs and tests/test_cpu_epoch.py).
+ *
+ * One iteration of the reference's training loop (PDE examples/Fisher-KPP_Source.jl:101-109,
+ * 195-201): predict(p) = solve(ODEProblem(rc_kanode, u0, (0, T), p), Tsit5(); saveat), the MSE loss,
+ * its gradient by SciMLSensitivity's InterpolatingAdjoint, and one Flux Adam update — all in C on one
+ * core, so the "reference CPU path" of the epoch metric is timed without an interpreter in the loop.
+ *   RHS: D*lap*u as the reference's DENSE Nx x Nx matvec (:55-59,97) + kan1_.(u) per point (:96);
+ *   VJP: (D*lap)^T λ as the dense transposed matvec (what Zygote's pullback of the matvec does) +
+ *        the per-point KAN pullback (kref_fk_vjp_f64 with D = 0);
+ *   Tsit5 / controller / dense output / adjoint: the statements of kan-odes_amd/kanode/ode.py and
+ *   kanode/adjoint.py (OrdinaryDiffEqTsit5 1.1.0 and SciMLSensitivity 7.69, restated there):
+ *   Hairer-Wanner initial step, PI controller (beta1 7/50, beta2 2/25, gamma 9/10, qmin 1/5, qmax 10,
+ *   qoldinit 1e-4), RMS error norm over the whole state ([λ; μ] in the adjoint), saveat from the
+ *   free interpolant, λ jumps at the saveat times with FSAL re-evaluated.
+ * u, targets: [Nx, B] column-major (trajectory contiguous); targets [n_save][Nx*B].
+ */
+#include "kanode_ref.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+static const double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
+static const double TA[6][6] = {
+    {0.161},
+    {-0.008480655492356989, 0.335480655492357},
+    {2.897153057105493, -6.359448489975075, 4.3622954328695815},
+    {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525},
+    {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383},
+    {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774}};
+static const double TB[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
+                             -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
+                             0.015151515151515152};
+static const double RI[7][4] = {{1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
+                                {0.0, 0.13169999999999998, -0.2234, 0.1017},
+                                {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
+                                {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
+                                {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
+                                {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
+                                {0.0, 1.5, -4.0, 2.5}};
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+typedef struct {
+    const kref_layer* L;
+    const double* p;
+    int64_t Nx, B, n, P;
+    double D, dx;
+    double* A;      /* dense D*lap, column-major */
+    double* tmp;    /* [n] */
+    int64_t nf_fwd, nf_adj;
+} fk_ctx;
+
+static void rhs(fk_ctx* c, const double* u, double* du) {
+    kref_fk_rhs_f64(c->L, c->p, 0.0, c->dx, c->Nx, u, c->B, du, 0);   /* kan1_.(u) (D = 0: no stencil) */
+    for (int64_t b = 0; b < c->B; ++b) {                                /* + (D*lap) u, dense gemv 'N' */
+        const double* ub = u + c->Nx * b;
+        double* db = c->tmp;
+        memset(db, 0, sizeof(double) * (size_t)c->Nx);
+        for (int64_t j = 0; j < c->Nx; ++j) {
+            const double uj = ub[j];
+            const double* Aj = c->A + c->Nx * j;
+            for (int64_t i = 0; i < c->Nx; ++i) db[i] += Aj[i] * uj;
+        }
+        for (int64_t i = 0; i < c->Nx; ++i) du[c->Nx * b + i] += db[i];
+    }
+    c->nf_fwd++;
+}
+
+/* lamJ = (∂f/∂u)^T lam ; dp = Σ lam ∂f/∂p (overwritten) */
+static void vjp(fk_ctx* c, const double* u, const double* lam, double* lamJ, double* dp) {
+    memset(dp, 0, sizeof(double) * (size_t)c->P);
+    kref_fk_vjp_f64(c->L, c->p, 0.0, c->dx, c->Nx, u, lam, c->B, lamJ, dp);
+    for (int64_t b = 0; b < c->B; ++b) {                                /* + (D*lap)^T λ, dense gemv 'T' */
+        const double* lb = lam + c->Nx * b;
+        for (int64_t j = 0; j < c->Nx; ++j) {
+            const double* Aj = c->A + c->Nx * j;
+            double s = 0.0;
+            for (int64_t i = 0; i < c->Nx; ++i) s += Aj[i] * lb[i];
+            lamJ[c->Nx * b + j] += s;
+        }
+    }
+    c->nf_adj++;
+}
+
+static void interp_w(double th, double* w) {
+    for (int i = 0; i < 7; ++i) {
+        double s = 0.0, tp = th;
+        for (int m = 0; m < 4; ++m) { s += RI[i][m] * tp; tp *= th; }
+        w[i] = s;
+    }
+}
+
+typedef struct {   /* the forward dense output: accepted steps */
+    int64_t n, cap;
+    double *t, *dt, *u, *k;    /* u: [cap][n]; k: [cap][7][n] */
+} dense_rec;
+
+static int rec_add(dense_rec* r, int64_t n, double t, double dt, const double* u, double* const* ks) {
+    if (r->n == r->cap) {
+        int64_t cap = r->cap ? 2 * r->cap : 256;
+        double* nt = realloc(r->t, sizeof(double) * cap);
+        double* nd = realloc(r->dt, sizeof(double) * cap);
+        double* nu = realloc(r->u, sizeof(double) * cap * n);
+        double* nk = realloc(r->k, sizeof(double) * cap * n * 7);
+        if (!nt || !nd || !nu || !nk) return -1;
+        r->t = nt; r->dt = nd; r->u = nu; r->k = nk; r->cap = cap;
+    }
+    r->t[r->n] = t;
+    r->dt[r->n] = dt;
+    memcpy(r->u + r->n * n, u, sizeof(double) * n);
+    for (int i = 0; i < 7; ++i) memcpy(r->k + (r->n * 7 + i) * n, ks[i], sizeof(double) * n);
+    r->n++;
+    return 0;
+}
+
+/* u(t) from the dense record (DenseRecord.locate: the step with t_s <= t, θ clamped to [0, 1]) */
+static void rec_eval(const dense_rec* r, int64_t n, double t, double* out) {
+    int64_t lo = 0, hi = r->n;          /* bisect_right(t_list, t) - 1 */
+    while (lo < hi) { int64_t mid = (lo + hi) / 2; if (t < r->t[mid]) hi = mid; else lo = mid + 1; }
+    int64_t s = lo - 1;
+    if (s < 0) s = 0;
+    if (s > r->n - 1) s = r->n - 1;
+    const double dt = r->dt[s];
+    double th = (t - r->t[s]) / dt;
+    th = th < 0.0 ? 0.0 : (th > 1.0 ? 1.0 : th);
+    double w[7];
+    interp_w(th, w);
+    const double* u = r->u + s * n;
+    for (int64_t e = 0; e < n; ++e) {
+        double acc = 0.0;
+        for (int i = 0; i < 7; ++i) acc += (dt * w[i]) * r->k[(s * 7 + i) * n + e];
+        out[e] = u[e] + acc;
+    }
+}
+
+static double sumsq_scaled(const double* x, const double* sk, int64_t n) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) { const double v = x[i] / sk[i]; s += v * v; }
+    return s;
+}
+
+/* One epoch.  Returns 0 on success; loss, grad[P] (dL/dp) and the stats out. */
+int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0, int64_t B,
+                      double T, const double* saveat, int32_t n_save, const double* target, double abstol,
+                      double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
+                      int64_t* stats /* [4]: fwd accept, fwd reject, adj accept, adj reject */, double* seconds) {
+    const double t_start = now_s();
+    fk_ctx c = {L, p, Nx, B, Nx * B, kref_layer_param_length(L), D, dx, NULL, NULL, 0, 0};
+    const int64_t n = c.n, P = c.P;
+    c.A = calloc((size_t)(Nx * Nx), sizeof(double));
+    c.tmp = malloc(sizeof(double) * Nx);
+    const double dx2 = dx * dx, cd = D * (-2.0 / dx2), co = D * (1.0 / dx2);
+    for (int64_t i = 0; i < Nx; ++i) {
+        c.A[i + Nx * i] = cd;
+        if (i + 1 < Nx) { c.A[i + Nx * (i + 1)] = co; c.A[(i + 1) + Nx * i] = co; }
+    }
+    c.A[0 + Nx * (Nx - 1)] = co;
+    c.A[(Nx - 1) + Nx * 0] = co;
+    double* buf = malloc(sizeof(double) * n * 24);
+    double *u = buf, *unew = buf + n, *y = buf + 2 * n, *sk = buf + 3 * n, *e = buf + 4 * n;
+    double* ks[7];
+    for (int i = 0; i < 7; ++i) ks[i] = buf + (5 + i) * n;
+    double* pred = malloc(sizeof(double) * n * n_save);
+    dense_rec rec = {0, 0, NULL, NULL, NULL, NULL};
+    const double beta1 = 7.0 / 50.0, beta2 = 2.0 / 25.0, gamma = 0.9, qmin = 0.2, qmax = 10.0, qoldinit = 1e-4;
+
+    /* ---- forward: solve(prob, Tsit5(); saveat) with the dense output kept ---- */
+    memcpy(u, u0, sizeof(double) * n);
+    int32_t si = 0;
+    while (si < n_save && saveat[si] <= 1e-14) { memcpy(pred + si * n, u0, sizeof(double) * n); ++si; }
+    double t = 0.0, dt;
+    rhs(&c, u, ks[0]);
+    if (adaptive) {   /* _initdt */
+        for (int64_t i = 0; i < n; ++i) sk[i] = abstol + fabs(u[i]) * reltol;
+        const double d0 = sqrt(sumsq_scaled(u, sk, n) / n), d1 = sqrt(sumsq_scaled(ks[0], sk, n) / n);
+        double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        if (dt0 > T) dt0 = T;
+        for (int64_t i = 0; i < n; ++i) y[i] = u[i] + dt0 * ks[0][i];
+        rhs(&c, y, ks[1]);
+        for (int64_t i = 0; i < n; ++i) e[i] = ks[1][i] - ks[0][i];
+        const double d2 = sqrt(sumsq_scaled(e, sk, n) / n) / dt0;
+        const double mx = d1 > d2 ? d1 : d2;
+        const double dt1 = mx <= 1e-15 ? fmax(1e-6, dt0 * 1e-3) : pow(0.01 / mx, 1.0 / 5.0);
+        dt = fmin(fmin(100 * dt0, dt1), T);
+    } else {
+        dt = dt_fixed;
+    }
+    double qold = qoldinit;
+    int64_t nacc = 0, nrej = 0;
+    while (t < T - 1e-14 * fmax(1.0, T)) {
+        if (dt > T - t) dt = T - t;
+        for (int s = 0; s < 6; ++s) {
+            for (int64_t i = 0; i < n; ++i) {
+                double acc = u[i];
+                for (int j = 0; j <= s; ++j) acc = acc + (dt * TA[s][j]) * ks[j][i];
+                y[i] = acc;
+            }
+            if (s == 5) memcpy(unew, y, sizeof(double) * n);
+            rhs(&c, y, ks[s + 1]);
+        }
+        double dtnew = dt;
+        if (adaptive) {
+            for (int64_t i = 0; i < n; ++i) {
+                double acc = 0.0;
+                for (int j = 0; j < 7; ++j) acc += TB[j] * ks[j][i];
+                e[i] = dt * acc;
+                sk[i] = abstol + fmax(fabs(u[i]), fabs(unew[i])) * reltol;
+            }
+            const double EEst = sqrt(sumsq_scaled(e, sk, n) / n);
+            const double q11 = EEst > 0 ? pow(EEst, beta1) : 0.0;
+            if (EEst > 1.0) { ++nrej; dt = dt / fmin(1.0 / qmin, q11 / gamma); continue; }
+            double q = q11 / pow(qold, beta2);
+            q = fmax(1.0 / qmax, fmin(1.0 / qmin, q / gamma));
+            dtnew = q > 0 ? dt / q : dt * qmax;
+            qold = fmax(EEst, qoldinit);
+        }
+        const double tn = t + dt;
+        while (si < n_save && saveat[si] <= tn + 1e-12 * fmax(1.0, fabs(tn))) {
+            const double ts = saveat[si];
+            if (fabs(ts - tn) <= 1e-12 * fmax(1.0, fabs(tn))) {
+                memcpy(pred + si * n, unew, sizeof(double) * n);
+            } else {
+                double w[7];
+                interp_w((ts - t) / dt, w);
+                for (int64_t i = 0; i < n; ++i) {
+                    double acc = 0.0;
+                    for (int j = 0; j < 7; ++j) acc += (dt * w[j]) * ks[j][i];
+                    pred[si * n + i] = u[i] + acc;
+                }
+            }
+            ++si;
+        }
+        if (rec_add(&rec, n, t, dt, u, ks)) return -1;
+        t = tn;
+        memcpy(u, unew, sizeof(double) * n);
+        memcpy(ks[0], ks[6], sizeof(double) * n);
+        ++nacc;
+        dt = dtnew;
+    }
+    /* ---- loss = mean(abs2, target - pred); ∂L/∂u(t_j) = -2 (target - pred) / numel ---- */
+    const double numel = (double)n * n_save;
+    double loss = 0.0;
+    double* g = malloc(sizeof(double) * n * n_save);
+    for (int64_t i = 0; i < n * n_save; ++i) {
+        const double r = target[i] - pred[i];
+        loss += r * r;
+        g[i] = -2.0 * r / numel;
+    }
+    loss /= numel;
+
+    /* ---- InterpolatingAdjoint (kanode/adjoint.py, statement for statement) ---- */
+    double *lam = buf + 12 * n, *ls = buf + 13 * n, *lnew = buf + 14 * n;
+    double* kl[7];
+    for (int i = 0; i < 7; ++i) kl[i] = buf + (15 + i) * n;
+    double* km = malloc(sizeof(double) * P * 7);
+    double* mu = calloc(P, sizeof(double));
+    double* munew = malloc(sizeof(double) * P);
+    double* emu = malloc(sizeof(double) * P);
+    double* skm = malloc(sizeof(double) * P);
+    memset(lam, 0, sizeof(double) * n);
+    int32_t used[64] = {0};
+    if (n_save > 64) return -2;
+    const double eps = 1e-12 * fmax(1.0, fabs(T));
+    for (int32_t j = 0; j < n_save; ++j)
+        if (fabs(saveat[j] - T) <= 0.0 && !used[j]) {   /* the jump at tf sets the initial λ */
+            for (int64_t i = 0; i < n; ++i) lam[i] += g[j * n + i];
+            used[j] = 1;
+        }
+    double stops[65];
+    int nst = 0;
+    for (int32_t j = n_save - 1; j >= 0; --j)     /* interior saveat times in τ = T - t, ascending */
+        if (!used[j] && saveat[j] > eps && saveat[j] < T - eps) {
+            const double s = T - saveat[j];
+            if (nst == 0 || s > stops[nst - 1]) stops[nst++] = s;
+        }
+    stops[nst++] = T;
+    double tau = 0.0, h;
+    rec_eval(&rec, n, T - 0.0, y);
+    vjp(&c, y, lam, kl[0], km);
+    const double ntot = (double)(n + P);
+    if (adaptive) {
+        for (int64_t i = 0; i < n; ++i) sk[i] = abstol + fabs(lam[i]) * reltol;
+        for (int64_t q = 0; q < P; ++q) skm[q] = abstol + fabs(mu[q]) * reltol;
+        const double d0 = sqrt((sumsq_scaled(lam, sk, n) + sumsq_scaled(mu, skm, P)) / ntot);
+        const double d1 = sqrt((sumsq_scaled(kl[0], sk, n) + sumsq_scaled(km, skm, P)) / ntot);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        if (h0 > T) h0 = T;
+        for (int64_t i = 0; i < n; ++i) ls[i] = lam[i] + h0 * kl[0][i];
+        rec_eval(&rec, n, T - h0, y);
+        vjp(&c, y, ls, kl[1], km + P);
+        for (int64_t i = 0; i < n; ++i) e[i] = kl[1][i] - kl[0][i];
+        for (int64_t q = 0; q < P; ++q) emu[q] = km[P + q] - km[q];
+        const double d2 = sqrt((sumsq_scaled(e, sk, n) + sumsq_scaled(emu, skm, P)) / ntot) / h0;
+        const double mx = d1 > d2 ? d1 : d2;
+        const double h1 = mx <= 1e-15 ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / mx, 1.0 / 5.0);
+        h = fmin(fmin(100 * h0, h1), T);
+    } else {
+        h = dt_fixed;
+    }
+    qold = qoldinit;
+    int32_t sti = 0;
+    int64_t aacc = 0, arej = 0;
+    while (tau < T - 1e-14 * fmax(1.0, T)) {
+        if (h > stops[sti] - tau) h = stops[sti] - tau;
+        for (int s = 0; s < 6; ++s) {
+            for (int64_t i = 0; i < n; ++i) {
+                double acc = lam[i];
+                for (int j = 0; j <= s; ++j) acc = acc + (h * TA[s][j]) * kl[j][i];
+                ls[i] = acc;
+            }
+            if (s == 5) memcpy(lnew, ls, sizeof(double) * n);
+            rec_eval(&rec, n, T - (tau + TC[s] * h), y);
+            vjp(&c, y, ls, kl[s + 1], km + (s + 1) * P);
+        }
+        for (int64_t q = 0; q < P; ++q) {
+            double acc = 0.0;
+            for (int j = 0; j < 6; ++j) acc += (h * TA[5][j]) * km[j * P + q];
+            munew[q] = mu[q] + acc;
+        }
+        double hnew = h;
+        if (adaptive) {
+            for (int64_t i = 0; i < n; ++i) {
+                double acc = 0.0;
+                for (int j = 0; j < 7; ++j) acc += (h * TB[j]) * kl[j][i];
+                e[i] = acc;
+                sk[i] = abstol + reltol * fmax(fabs(lam[i]), fabs(lnew[i]));
+            }
+            for (int64_t q = 0; q < P; ++q) {
+                double acc = 0.0;
+                for (int j = 0; j < 7; ++j) acc += (h * TB[j]) * km[j * P + q];
+                emu[q] = acc;
+                skm[q] = abstol + fmax(fabs(mu[q]), fabs(munew[q])) * reltol;
+            }
+            const double EEst = sqrt((sumsq_scaled(e, sk, n) + sumsq_scaled(emu, skm, P)) / ntot);
+            const double q11 = EEst > 0 ? pow(EEst, beta1) : 0.0;
+            if (EEst > 1.0) { ++arej; h = h / fmin(1.0 / qmin, q11 / gamma); continue; }
+            double q = q11 / pow(qold, beta2);
+            q = fmax(1.0 / qmax, fmin(1.0 / qmin, q / gamma));
+            hnew = q > 0 ? h / q : h * qmax;
+            qold = fmax(EEst, qoldinit);
+        }
+        tau = tau + h;
+        memcpy(lam, lnew, sizeof(double) * n);
+        memcpy(mu, munew, sizeof(double) * P);
+        memcpy(kl[0], kl[6], sizeof(double) * n);
+        memcpy(km, km + 6 * P, sizeof(double) * P);
+        ++aacc;
+        if (fabs(tau - stops[sti]) <= 1e-12 * fmax(1.0, T)) {
+            tau = stops[sti];
+            const double ts = T - tau;
+            if (sti < nst - 1) {
+                for (int32_t j = 0; j < n_save; ++j)   /* λ += ∂L/∂u(t_j) at every saveat equal to ts */
+                    if (!used[j] && fabs(saveat[j] - ts) <= eps) {
+                        for (int64_t i = 0; i < n; ++i) lam[i] += g[j * n + i];
+                        used[j] = 1;
+                    }
+                rec_eval(&rec, n, T - tau, y);           /* u_modified!: FSAL re-evaluated */
+                vjp(&c, y, lam, kl[0], km);
+            }
+            sti = sti + 1 < nst ? sti + 1 : nst - 1;
+        }
+        h = hnew;
+    }
+    /* dL/dp = μ(t0); a saveat at t0 adds to dL/du0 only */
+    memcpy(grad, mu, sizeof(double) * P);
+    /* ---- Flux Adam step (first step of a fresh optimiser: βp = β) ---- */
+    for (int64_t q = 0; q < P; ++q) {
+        const double m = 0.1 * grad[q], v = 0.001 * grad[q] * grad[q];
+        p[q] -= m / (1 - 0.9) / (sqrt(v / (1 - 0.999)) + 1e-8) * eta;
+    }
+    *loss_out = loss;
+    stats[0] = nacc; stats[1] = nrej; stats[2] = aacc; stats[3] = arej;
+    free(c.A); free(c.tmp); free(buf); free(pred); free(g); free(km); free(mu); free(munew); free(emu); free(skm);
+    free(rec.t); free(rec.dt); free(rec.u); free(rec.k);
+    *seconds = now_s() - t_start;
+    return 0;
+}

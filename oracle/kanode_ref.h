@@ -90,6 +90,13 @@ void kref_fk_rhs_f64(const kref_layer* L, const double* p, double D, double dx, 
 void kref_fk_vjp_f64(const kref_layer* L, const double* p, double D, double dx, int64_t Nx,
                      const double* u, const double* lam, int64_t B, double* lamJ, double* dp);
 
+/* One Fisher-KPP training epoch on one core (cpu_epoch.c; bench comparator): solve + loss +
+ * InterpolatingAdjoint gradient + Adam, u0 [Nx, B], target [n_save][Nx, B]; p updated in place. */
+int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0, int64_t B,
+                      double T, const double* saveat, int32_t n_save, const double* target, double abstol,
+                      double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
+                      int64_t* stats, double* seconds);
+
 /* per-edge activations (Activation_getter.jl:3-63): act [O, I, K] (o fastest) */
 void kref_edge_act_f64(const kref_layer* L, const double* p, const double* x, int64_t K, double* act);
 

@@ -99,6 +99,10 @@ def lib() -> C.CDLL:
         L.kref_bench_chain_f64.restype = C.c_double
         L.kref_bench_chain_f64.argtypes = [C.c_int32, LP, P, P, C.c_int64, P, C.c_int32, C.c_int32]
         L.kref_omp_max_threads.restype = C.c_int32
+        L.kref_fk_epoch_f64.restype = C.c_int
+        L.kref_fk_epoch_f64.argtypes = [LP, P, C.c_double, C.c_double, C.c_int64, P, C.c_int64, C.c_double, P,
+                                        C.c_int32, P, C.c_double, C.c_double, C.c_int32, C.c_double, C.c_double,
+                                        P, P, P, P]
         _lib = L
     return _lib
 
@@ -228,6 +232,30 @@ def bench_chain(specs, p, x, reps: int, threads: int) -> float:
     K = x.shape[0]
     y = np.zeros((K, specs[-1].out_dims), np.float64)
     return lib().kref_bench_chain_f64(len(specs), _layers(specs), _ptr(p), _ptr(x), K, _ptr(y), reps, threads)
+
+
+def fk_epoch(spec: LayerSpec, p: np.ndarray, D: float, dx: float, u0: np.ndarray, T: float, saveat, target,
+             abstol=1e-6, reltol=1e-3, adaptive=True, dt=0.0, eta=1e-2):
+    """One Fisher-KPP training epoch in C on one core (oracle/cpu_epoch.c): Tsit5 solve with dense
+    output, MSE loss, InterpolatingAdjoint gradient, one Adam step (first step of a fresh optimiser).
+    u0 (B, Nx); target (n_save, B, Nx).  Returns (loss, grad, p_new, stats dict, seconds)."""
+    u0 = np.ascontiguousarray(u0, dtype=np.float64)
+    B, Nx = u0.shape
+    sv = np.ascontiguousarray(saveat, dtype=np.float64)
+    tg = np.ascontiguousarray(target, dtype=np.float64)
+    assert tg.shape == (sv.size, B, Nx)
+    pn = np.ascontiguousarray(p, dtype=np.float64).copy()
+    grad = np.zeros_like(pn)
+    loss = C.c_double()
+    secs = C.c_double()
+    st = np.zeros(4, np.int64)
+    rc = lib().kref_fk_epoch_f64(C.byref(spec.to_c()), _ptr(pn), D, dx, Nx, _ptr(u0), B, T, _ptr(sv), sv.size,
+                                 _ptr(tg), abstol, reltol, int(adaptive), dt, eta, C.byref(loss), _ptr(grad),
+                                 _ptr(st), C.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"kref_fk_epoch_f64 failed ({rc})")
+    stats = dict(naccept=int(st[0]), nreject=int(st[1]), adjoint_naccept=int(st[2]), adjoint_nreject=int(st[3]))
+    return loss.value, grad, pn, stats, secs.value
 
 
 def omp_max_threads() -> int:

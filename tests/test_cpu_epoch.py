@@ -1,0 +1,46 @@
+"""The C epoch comparator (oracle/cpu_epoch.c, bench.py's CPU epoch legs) against the Python statement
+of the same epoch (kanode.solve + InterpolatingAdjoint + Adam on the oracle RHS, dense Laplacian):
+Fisher-KPP_Source.jl:101-109,195-201.  Both are CPU restatements; this pins the comparator to the
+driver the GPU path is checked against."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle.oracle_rhs import OracleFKRHS
+
+import kanode
+
+
+def _ics(B, nx, seed):
+    rng = np.random.default_rng(seed)
+    x = np.arange(nx) / (nx - 1)
+    c, d, a = rng.uniform(0.3, 0.7, (B, 1)), rng.uniform(0.1, 0.3, (B, 1)), rng.uniform(0.5, 1, (B, 1))
+    return a * (np.tanh((x - (c - d / 2)) / (d / 10)) - np.tanh((x - (c + d / 2)) / (d / 10))) / 2
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_c_epoch_matches_python_driver(adaptive):
+    nx, B, D = 32, 3, 0.01
+    dx = 1.0 / (nx - 1)
+    spec = O.LayerSpec(1, 1, 10, "softsign")
+    u0 = _ics(B, nx, 1)
+    p0 = np.random.default_rng(2).uniform(-1, 1, 11)
+    T = 0.5
+    saveat = [0.0, 0.1, 0.25, 0.25, 0.4, 0.5]
+    target = 0.9 * np.broadcast_to(u0, (len(saveat), B, nx))
+    dt = 2e-3
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8) if adaptive else kanode.Tsit5Options(adaptive=False, dt=dt)
+    loss, grad, p_new, st, secs = O.fk_epoch(spec, p0, D, dx, u0, T, saveat, target, abstol=1e-8, reltol=1e-8,
+                                             adaptive=adaptive, dt=dt, eta=1e-2)
+    tr = kanode.Trainer(OracleFKRHS(spec, D, dx, dense=True), torch.as_tensor(u0), (0.0, T), saveat,
+                        torch.as_tensor(np.ascontiguousarray(target)), torch.as_tensor(p0), eta=1e-2, solver=opt,
+                        sensealg="interpolating_adjoint")
+    lt, gt, sol = tr.loss_and_grad()
+    assert st["naccept"] == sol.stats["naccept"] and st["nreject"] == sol.stats["nreject"]
+    assert st["adjoint_naccept"] == sol.stats["adjoint"]["naccept"]
+    assert abs(loss - lt.item()) <= 1e-12 * abs(loss)
+    assert np.max(np.abs(grad - gt.numpy())) <= 1e-10 * np.max(np.abs(gt.numpy()))
+    tr.step()
+    assert np.max(np.abs(p_new - tr.p.numpy())) <= 1e-12 * np.max(np.abs(p0))
+    assert secs > 0
