@@ -156,8 +156,8 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     of <= 256 points, GRID_ADJ_STEP unset); 0 = the persistent-grid step kernel, whose
  *     stages pass kλ through memory.  Same λᵀJ and λ bitwise; dp to the reduction order.
  *   KANODE_OPT_PAIR_VJP (default 1): the VJP / adjoint stage of a surrogate chain KAN [N, H, N]
- *     (wide-in then wide-out layer) runs as two launches (batches up to 512); 0 = the four-launch
- *     path.  Bitwise equal results.
+ *     (wide-in then wide-out layer) runs as two launches (batches up to 64); 0 = the four-launch
+ *     path.  Equal to the summation order of the wide-out dot products (both fixed-order).
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {

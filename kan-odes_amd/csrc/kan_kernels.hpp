@@ -166,6 +166,28 @@ struct FinishJobs {
     FinishJob j[kMaxFinishJobs];
 };
 hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, hipStream_t st);
+// The finish of an ADAPTIVE Fisher-KPP adjoint step in one launch (kan_pp.hip adj_finish_kernel):
+// block q < P forms the stage sums S_i[q] = Σ_b slab_i[b·P + q] (i < nslab, one pass, fixed order),
+//     μ_new[q] = fma(1, Σ_i ca_i S_i, fma(a0, km1[q], μ[q]))       (μ + h Σ_j a6_j kμ_j)
+//     km7[q]   = S_{k7}[q]                                         (the next step's FSAL kμ_1)
+//     out[1 + q] = (e / (abstol + reltol·max(|μ|, |μ_new|)))²,  e = e0·km1[q] + Σ_i ce_i S_i
+//                                                                  (the μ part of the [λ; μ] norm)
+// and block P sums the λ error partials into out[0]: the step's μ update, FSAL and error norm,
+// which otherwise take the reduction, lincomb and two error launches.
+struct AdjFinish {
+    const double* slab[6];
+    double ca[6], ce[6];
+    int32_t nslab, k7;
+    int64_t nblk;
+    double a0, e0, abstol, reltol;
+    const double* mu;
+    double* mu_new;
+    const double* km1;
+    double* km7;
+    const double* err_slab;
+    double* out;
+};
+hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st);
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,
                              hipStream_t st);
@@ -366,8 +388,9 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
 // constants (lc[0] wide-in, lc[1] wide-out); x = layer-1 input (u; with si the stage base u, y formed
 // and written to si->y_out, λs to si->ls_out); ybar = λ (no si); xvjp = the layer-1 input the pullback
 // reads (u, or si->y_out); pslab = the wide-in chunk partials (widein_chunks·K·H), S = the wide-out dot
-// slab (H·(G+1)·K).  hipErrorNotSupported: K > kPairMaxK or the LDS would not fit (use the 4 launches).
-constexpr int64_t kPairMaxK = 512;
+// products' chunk partials (widein_chunks·H·(G+1)·K).  hipErrorNotSupported: K > kPairMaxK or the LDS
+// would not fit (use the 4 launches).
+constexpr int64_t kPairMaxK = 64;
 template <typename T>
 hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,

@@ -1326,6 +1326,57 @@ hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, 
     return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(kBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
+    __shared__ double red[(kBlock / kWave) * 6];
+    __shared__ double sums[6];
+    const int64_t q = blockIdx.x;
+    if (q == P) {   // the λ error partials
+        double s = 0.0;
+        for (int64_t b = threadIdx.x; b < f.nblk; b += blockDim.x) s += f.err_slab[b];
+        const double v[1] = {s};
+        block_sum_to<double, 1>(v, 1, red, sums);
+        __syncthreads();
+        if (threadIdx.x == 0) f.out[0] = sums[0];
+        return;
+    }
+    double acc[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[i] = 0.0;
+    for (int64_t b = threadIdx.x; b < f.nblk; b += blockDim.x) {
+        double v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = i < f.nslab ? f.slab[i][b * P + q] : 0.0;   // all loads first
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[i] += v[i];
+    }
+    block_sum_to<double, 6>(acc, f.nslab, red, sums);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double cm = 0.0, ce = 0.0, k7 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (i < f.nslab) {
+                cm = ::fma(f.ca[i], sums[i], cm);
+                ce = ::fma(f.ce[i], sums[i], ce);
+                if (i == f.k7) k7 = sums[i];
+            }
+        }
+        const double m0 = f.mu[q], k1 = f.km1[q];
+        const double mn = ::fma(1.0, cm, ::fma(f.a0, k1, m0));
+        f.mu_new[q] = mn;
+        f.km7[q] = k7;
+        const double e = ::fma(f.e0, k1, ce);
+        const double r = e / ::fma(f.reltol, fmax(kabs(m0), kabs(mn)), f.abstol);
+        f.out[1 + q] = r * r;
+    }
+}
+
+hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st) {
+    if (f.nslab < 1 || f.nslab > 6 || P < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(adj_finish_kernel, dim3((unsigned)P + 1), dim3(kBlock), 0, st, f, P);
+    return hipGetLastError();
+}
+
 // du = D·lap·y + KAN(y) for one trajectory row held by one wave (lane: pairs 128k + 2·lane),
 // stencil neighbours by wave rotation, the KAN from the LDS table (direct formula off-table)
 template <int NORM, int BASIS, int NP>

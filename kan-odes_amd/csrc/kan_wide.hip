@@ -109,13 +109,26 @@ __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const S
 }
 // MV / MW: C / W load slots per thread (>= the chunk's entries / tn; the launch picks the smallest
 // instantiation that covers the chunk -- unused predicated slots still cost instructions).
-template <typename T, bool STAGE, int MV, int MW>
+// The pair pullback's dot products, formed by the wide-in forward blocks (DOT): the chunk's input
+// range [i0, i0 + ni) is also an output range of the wide-out layer (N_in == N_out), so the block
+// that holds ȳ[i0 .. i0 + ni, k] (λs it formed, or λ) forms the partial sums
+//     spart[(bx·IR + q)·K + k] = Σ_{o in chunk} row_q[o] ȳ[o, k],   row_q = C2[:, r + G2 i2] (r < G2) or
+// W2[:, i2] (r = G2), q = i2·R2 + r, IR = I2·R2; the consumer sums the nblk chunk partials in order.
+template <typename T>
+struct PairDot {
+    const LayerConst* lc1;
+    T* spart;
+    const T* ybar;   // ȳ without a stage (λ); with a stage, λs as the block forms it
+};
+template <typename T, bool STAGE, int MV, int MW, bool DOT = false>
 __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, T* __restrict__ slab, int64_t K,
-                                                const WideStageIn<T>* si, int bx, int by, int gy) {
+                                                const WideStageIn<T>* si, int bx, int by, int gy,
+                                                const PairDot<T>* pd = nullptr) {
     __shared__ T phiL[kWideInMaxInputs * kMaxGrid];
     __shared__ T swL[kWideInMaxInputs];
     __shared__ T xL[kWideInMaxInputs];
+    __shared__ T lsL[DOT ? kWideInMaxInputs : 1];
     __shared__ T red[256];
     const Math<T> M{kExp2Tab256};
     const LayerConst& lc = *lcp;
@@ -146,9 +159,15 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
                 const T v = wide_stage_comb<T>(x, si->su, idx);
                 xL[t] = v;
                 if (si->y_out) si->y_out[idx] = v;
-                if (si->lam) si->ls_out[idx] = wide_stage_comb<T>(si->lam, si->sl, idx);
+                if (si->lam) {
+                    const T l = wide_stage_comb<T>(si->lam, si->sl, idx);
+                    si->ls_out[idx] = l;
+                    if constexpr (DOT) lsL[t] = l;
+                }
             }
             __syncthreads();
+        } else if constexpr (DOT) {
+            if (t < ni) lsL[t] = pd->ybar[(int64_t)I * k + i0 + t];
         }
         // one thread per basis slot c = g + G i (direct formula: no per-input knot chain)
         for (int c = t; c < ni * G; c += blockDim.x) {
@@ -178,6 +197,31 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             slab[((int64_t)bx * K + k) * O + t] = sum;
         }
         __syncthreads();
+        if constexpr (DOT) {
+            // rows q of the wide-out layer against the chunk's ȳ: thread (q, s) sums entries t ≡ s
+            // (mod ns) of the chunk, then the ns sub-sums of row q are added in order (LDS `red`)
+            const LayerConst& l1 = *pd->lc1;
+            const int R1 = l1.G + (l1.use_base ? 1 : 0), IR = l1.I * R1, O1 = l1.O;
+            const int ns = IR >= 256 ? 1 : 256 / IR;
+            for (int q0 = 0; q0 < IR; q0 += 256 / ns) {
+                const int q = q0 + t / ns, sub = t - (t / ns) * ns;
+                T a = T(0);
+                if (q < IR && t / ns < 256 / ns) {
+                    const int i2 = q / R1, r = q - i2 * R1;
+                    const T* __restrict__ row =
+                        r < l1.G ? p + l1.p_off + (int64_t)O1 * (r + (int64_t)l1.G * i2) : p + l1.w_off + (int64_t)O1 * i2;
+                    for (int e = sub; e < ni; e += ns) a = kfma<T>(row[i0 + e], lsL[e], a);
+                }
+                red[t] = a;
+                __syncthreads();
+                if (t < 256 / ns && q0 + t < IR) {
+                    T sum = red[t * ns];
+                    for (int s2 = 1; s2 < ns; ++s2) sum += red[t * ns + s2];
+                    pd->spart[((int64_t)bx * IR + q0 + t) * K + k] = sum;
+                }
+                __syncthreads();
+            }
+        }
     }
 }
 // (two kernels: the plain forward keeps a small argument block, the stage form carries StageArgs)
@@ -299,12 +343,13 @@ kd_fwd_wideout_kernel(const LayerConst* __restrict__ lcp, const T* __restrict__ 
 // column; the wave partials are summed in order through LDS and added to pbar once
 // (coalesced over o).  The basis of input i is staged in LDS kWOPK columns at a time.
 constexpr int kWOPK = 128;
+// Ph: LDS of (kMaxGrid + 1)·wk entries, wk <= kWOPK the column tile (the caller's: a static array in
+// the dot+param launch, a K-sized slice of the dynamic block in the pair pullback).
 template <typename T, int PATH>
 __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const LayerConst* __restrict__ lcp,
                                                    const T* __restrict__ x, const T* __restrict__ xslab, int nblk,
                                                    const T* __restrict__ ybar, T* __restrict__ pbar, int64_t K,
-                                                   int bx, int i, int assign) {
-    __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
+                                                   int bx, int i, int assign, T* __restrict__ Ph, int wk) {
     __shared__ T red[kSW][kWOB];
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
@@ -314,8 +359,8 @@ __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const Layer
     T acc[kMaxGrid + 1];
 #pragma unroll
     for (int r = 0; r <= kMaxGrid; ++r) acc[r] = T(0);
-    for (int64_t k0 = 0; k0 < K; k0 += kWOPK) {
-        const int kt = (int)((K - k0) < kWOPK ? (K - k0) : kWOPK);
+    for (int64_t k0 = 0; k0 < K; k0 += wk) {
+        const int kt = (int)((K - k0) < wk ? (K - k0) : wk);
         __syncthreads();
         for (int kk = threadIdx.x; kk < kt; kk += blockDim.x) {
             const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k0 + kk);
@@ -323,9 +368,9 @@ __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const Layer
             bs.init(M, lc, xi);
             for (int g = 0; g < G; ++g) {
                 T z, aux;
-                Ph[g * kWOPK + kk] = bs.next(M, lc, g, z, aux);
+                Ph[g * wk + kk] = bs.next(M, lc, g, z, aux);
             }
-            Ph[kMaxGrid * kWOPK + kk] = base ? swish<T>(M, xi) : T(0);
+            Ph[kMaxGrid * wk + kk] = base ? swish<T>(M, xi) : T(0);
         }
         __syncthreads();
         if (o < O) {
@@ -334,8 +379,8 @@ __device__ __forceinline__ void wideout_param_body(const Math<T>& M, const Layer
                 const T yb = ybar[(int64_t)O * (k0 + kk) + o];
 #pragma unroll
                 for (int r = 0; r < kMaxGrid; ++r)
-                    if (r < G) acc[r] = kfma<T>(yb, Ph[r * kWOPK + kk], acc[r]);
-                acc[kMaxGrid] = kfma<T>(yb, Ph[kMaxGrid * kWOPK + kk], acc[kMaxGrid]);
+                    if (r < G) acc[r] = kfma<T>(yb, Ph[r * wk + kk], acc[r]);
+                acc[kMaxGrid] = kfma<T>(yb, Ph[kMaxGrid * wk + kk], acc[kMaxGrid]);
             }
         }
     }
@@ -384,11 +429,16 @@ __device__ __forceinline__ void wideout_dot_body(const LayerConst* __restrict__ 
 #pragma unroll
         for (int kk = 0; kk < kKT; ++kk) acc[kk] = T(0);
         if (ls) {
-#pragma unroll 2
+            // λs[o, k] formed here: every column's stage loads issued before the first combination
             for (int o = threadIdx.x; o < O; o += kWOX) {
                 const T cv = row[o];
-                for (int kk = 0; kk < kt; ++kk)
-                    acc[kk] = kfma<T>(cv, wide_stage_comb<T>(ls->lam, ls->sl, (int64_t)O * (k0 + kk) + o), acc[kk]);
+                T yv[kKT];
+#pragma unroll
+                for (int kk = 0; kk < kKT; ++kk)
+                    yv[kk] = kk < kt ? wide_stage_comb<T>(ls->lam, ls->sl, (int64_t)O * (k0 + kk) + o) : T(0);
+#pragma unroll
+                for (int kk = 0; kk < kKT; ++kk)
+                    if (kk < kt) acc[kk] = kfma<T>(cv, yv[kk], acc[kk]);
             }
         } else {
 #pragma unroll 4
@@ -429,18 +479,37 @@ kd_vjp_wideout_dotparam_kernel(const LayerConst* __restrict__ lcp, const T* __re
         const int ir = lcp->I * (lcp->G + (lcp->use_base ? 1 : 0));
         wideout_dot_body<T>(lcp, p, ybar, S, K, b % ir, b / ir, tiles);
     } else {
+        __shared__ T Ph[(kMaxGrid + 1) * kWOPK];
         const int q = b - nd;
-        wideout_param_body<T, PATH>(M, lcp, x, xslab, nblk, ybar, pbar, K, q % nrc, q / nrc, assign);
+        wideout_param_body<T, PATH>(M, lcp, x, xslab, nblk, ybar, pbar, K, q % nrc, q / nrc, assign, Ph, kWOPK);
     }
 }
 
 // x̄[i, k] of the wide-out layer from its dot products S (one element)
+// S: nS partial slabs of I·R·K sums each (the pair's chunk partials, summed in order; nS = 1: the
+// dot launch's complete sums)
+template <typename T>
+__device__ __forceinline__ T dot_sum(const T* __restrict__ Si, int nS, int64_t sstride) {
+    if (nS == 1) return Si[0];
+    constexpr int kR = 16;
+    T s = T(0);
+    for (int b0 = 0; b0 < nS; b0 += kR) {
+        T v[kR];
+#pragma unroll
+        for (int j = 0; j < kR; ++j) v[j] = b0 + j < nS ? Si[(int64_t)(b0 + j) * sstride] : T(0);
+#pragma unroll
+        for (int j = 0; j < kR; ++j)
+            if (b0 + j < nS) s += v[j];
+    }
+    return s;
+}
 template <typename T, int PATH>
 __device__ __forceinline__ T wideout_xfin_one(const Math<T>& M, const LayerConst& lc, const T* __restrict__ x,
                                               const T* __restrict__ xslab, int nblk, const T* __restrict__ S,
-                                              int64_t K, int i, int64_t k) {
+                                              int64_t K, int i, int64_t k, int nS = 1) {
     const int I = lc.I, G = lc.G;
     const int R = G + (lc.use_base ? 1 : 0);
+    const int64_t sstride = (int64_t)I * R * K;
     const T invh = T(lc.invh);
     const T* __restrict__ Si = S + (int64_t)i * R * K + k;
     const T xi = layer_in<T>(x, xslab, nblk, I, K, i, k);
@@ -450,13 +519,14 @@ __device__ __forceinline__ T wideout_xfin_one(const Math<T>& M, const LayerConst
     for (int g = 0; g < G; ++g) {
         T z, aux;
         const T phi = bs.next(M, lc, g, z, aux);
-        nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, Si[(int64_t)g * K]) * invh;
+        nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, dot_sum<T>(Si + (int64_t)g * K, nS, sstride)) *
+                          invh;
     }
     T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
     if (lc.use_base) {
         T sw, dsw;
         swish_and_grad<T>(M, xi, sw, dsw);
-        xb = xb + Si[(int64_t)G * K] * dsw;
+        xb = xb + dot_sum<T>(Si + (int64_t)G * K, nS, sstride) * dsw;
     }
     return xb;
 }
@@ -648,28 +718,71 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
 // ---------------------------------------------------------------------------
 // The surrogate pair's pullback in two launches (kanode_vjp / kanode_vjp_stage of a KAN [N, H, N],
 // Burgers_Surrogate.jl:85-97, Schrodinger_Surrogate.jl:93-104), instead of four:
-//   A: blocks [0, nF) the wide-in forward's chunk partials of the hidden layer h (with a stage: y and
-//      λs formed and written, WideStageIn); blocks [nF, nF + nD) the wide-out dot products
-//      S[i, r, k] = Σ_o row_{i,r}[o] ȳ[o, k] (ȳ = λs formed in place) -- they need ȳ and the
-//      parameters only, not h, so they run beside the forward;
-//   B: blocks [0, nP) the wide-out parameter cotangents (h summed from the partials, ȳ); the rest the
-//      wide-in pullback, whose cotangent (x̄ of the hidden layer) each block forms itself from S and h
-//      (wideout_xfin_one: a parameter block its output's K entries, an x̄ block its column's H),
-//      which removes the x̄ pass and its launch.
-// Every value is computed by the same arithmetic in the same order as on the four-launch path, so the
-// results are bitwise equal to it.
+//   A: the wide-in forward's chunk partials of the hidden layer h (with a stage: y and λs formed and
+//      written, WideStageIn), and, in the same blocks, the chunk partials of the wide-out dot products
+//      S[i, r, k] = Σ_o row_{i,r}[o] ȳ[o, k] over the block's o-range (PairDot: ȳ = λs as the block
+//      formed it; the dot products need ȳ and the parameters only, not h);
+//   B: blocks [0, nP) the wide-out parameter cotangents (h summed from its partials, ȳ); the rest the
+//      wide-in pullback, whose cotangent (x̄ of the hidden layer) each block forms itself from the S
+//      and h partials (wideout_xfin_one: a parameter block its output's K entries, an x̄ block its
+//      column's H), which removes the x̄ pass and its launch.
+// The results equal the four-launch path's up to the summation order of S (chunk partials summed in
+// chunk order instead of one wave-ordered block sum): fixed, so bitwise reproducible.
 template <typename T, int MV, int MW, bool STAGE>
 __global__ void __launch_bounds__(256)
 kd_vjp_pair_a_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
-                     const T* __restrict__ x, T* __restrict__ pslab, const T* __restrict__ ybar, T* __restrict__ S,
-                     int64_t K, int nF, int nblk, int gyF, int tiles, WideStageIn<T> si) {
-    const int b = blockIdx.x;
-    if (b < nF) {
-        widein_fwd_body<T, STAGE, MV, MW>(lc0, p, x, pslab, K, STAGE ? &si : nullptr, b % nblk, b / nblk, gyF);
-    } else {
-        const int q = b - nF;
-        const int ir = lc1->I * (lc1->G + (lc1->use_base ? 1 : 0));
-        wideout_dot_body<T>(lc1, p, ybar, S, K, q % ir, q / ir, tiles, STAGE ? &si : nullptr);
+                     const T* __restrict__ x, T* __restrict__ pslab, const T* __restrict__ ybar, T* __restrict__ spart,
+                     int64_t K, int nblk, int gyF, WideStageIn<T> si) {
+    const PairDot<T> pd{lc1, spart, ybar};
+    widein_fwd_body<T, STAGE, MV, MW, true>(lc0, p, x, pslab, K, STAGE ? &si : nullptr, blockIdx.x % nblk,
+                                            blockIdx.x / nblk, gyF, &pd);
+}
+
+// x̄ of one wide-out input from its value xi and its dot products Sl[g·ss] (g < G; the swish row at G)
+template <typename T, int PATH>
+__device__ __forceinline__ T wideout_xfin_lds(const Math<T>& M, const LayerConst& lc, T xi, const T* Sl, int ss) {
+    const int G = lc.G;
+    const T invh = T(lc.invh);
+    Basis1<T, PATH> bs;
+    bs.init(M, lc, xi);
+    T nbar = T(0);
+    for (int g = 0; g < G; ++g) {
+        T z, aux;
+        const T phi = bs.next(M, lc, g, z, aux);
+        nbar = nbar + basis_pull<T>(lc.basis, lc.iqf_quirk, z, phi, aux, Sl[g * ss]) * invh;
+    }
+    T xb = nbar * dnormalize<NORM_RUNTIME, T>(lc.norm, bs.n);
+    if (lc.use_base) {
+        T sw, dsw;
+        swish_and_grad<T>(M, xi, sw, dsw);
+        xb = xb + Sl[G * ss] * dsw;
+    }
+    return xb;
+}
+
+// dst[v] = Σ_{b < nS} src(v, b) for v < nt, by the whole block (every thread calls): thread t sums the
+// terms b ≡ s (mod ns) of value t / ns in ascending b, then the ns sub-sums are added in order (fixed
+// order: bitwise reproducible).  red: LDS of 256 entries.
+template <typename T, typename F>
+__device__ __forceinline__ void block_gather_sums(F src, int nt, int nS, T* red, T* dst) {
+    const int t = threadIdx.x;
+    for (int v0 = 0; v0 < nt; v0 += 256) {
+        const int nv = nt - v0 < 256 ? nt - v0 : 256;
+        const int ns = 256 / nv;
+        const int v = t / ns, s = t - v * ns;
+        T a = T(0);
+        if (v < nv) {
+#pragma unroll 4
+            for (int b = s; b < nS; b += ns) a += src(v0 + v, b);
+        }
+        red[t] = a;
+        __syncthreads();
+        if (t < nv) {
+            T sum = red[t * ns];
+            for (int j = 1; j < ns; ++j) sum += red[t * ns + j];
+            dst[v0 + t] = sum;
+        }
+        __syncthreads();
     }
 }
 
@@ -679,26 +792,43 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
                      const T* __restrict__ x, const T* __restrict__ pslab, int nblk, const T* __restrict__ ybar,
                      const T* __restrict__ S, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int nP, int nrc,
                      int np, int nxg, int cw, int nbx, int hb_off, int assign) {
+    // S: the nblk chunk partials of the wide-out dot products (kd_vjp_pair_a_kernel), [b][I1·R1][K]
     extern __shared__ __attribute__((aligned(16))) unsigned char pb_raw[];
     T* L = reinterpret_cast<T*>(pb_raw);
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1)
     const int b = blockIdx.x;
     if (b < nP) {
-        wideout_param_body<T, PATH>(M, lc1, (const T*)nullptr, pslab, nblk, ybar, pbar, K, b % nrc, b / nrc, assign);
+        const int wk = (int)(K < kWOPK ? K : kWOPK);
+        wideout_param_body<T, PATH>(M, lc1, (const T*)nullptr, pslab, nblk, ybar, pbar, K, b % nrc, b / nrc, assign, L,
+                                    wk);
         return;
     }
     const int q = b - nP;
     const LayerConst& l1 = *lc1;
-    T* hbL = L + hb_off;   // [K]: a parameter block's cotangent row
+    const int H = l1.I, R = l1.G + (l1.use_base ? 1 : 0);
+    const int64_t bs = (int64_t)H * R * K;     // stride of one chunk's partials
+    T* hbL = L + hb_off;                       // [K]: a parameter block's cotangent row
+    T* red = hbL + K;                          // [256]
+    T* Sv = red + 256;                         // [max(R·K, H·R)] the block's dot products
+    T* hv = Sv + (R * K > H * R ? R * K : H * R);   // [max(K, H)] the hidden values it needs
     widein_vjp_body<T>(
         lc0, p, x, [&](int, int64_t k) { return hbL[k]; },
-        [&](int o) {
+        [&](int o) {   // hidden unit o over all columns: S[o, r, k] for r < R, k < K, and h[o, k]
+            block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K, nblk,
+                                 red, Sv);
             for (int64_t k = threadIdx.x; k < K; k += blockDim.x)
-                hbL[k] = wideout_xfin_one<T, PATH>(M, l1, (const T*)nullptr, pslab, nblk, S, K, o, k);
+                hv[k] = layer_in<T>(nullptr, pslab, nblk, H, K, o, k);
+            __syncthreads();
+            for (int64_t k = threadIdx.x; k < K; k += blockDim.x)
+                hbL[k] = wideout_xfin_lds<T, PATH>(M, l1, hv[k], Sv + k, (int)K);
             __syncthreads();
         },
-        [&](T* ybL, int t, int64_t k) {
-            if (t < l1.I) ybL[t] = wideout_xfin_one<T, PATH>(M, l1, (const T*)nullptr, pslab, nblk, S, K, t, k);
+        [&](T* ybL, int t, int64_t k) {   // column k over all hidden units: S[i, r, k] and h[i, k]
+            block_gather_sums<T>(
+                [&](int v, int c) { return S[c * bs + (int64_t)v * K + k]; }, H * R, nblk, red, Sv);
+            if (t < H) hv[t] = layer_in<T>(nullptr, pslab, nblk, H, K, t, k);
+            __syncthreads();
+            if (t < H) ybL[t] = wideout_xfin_lds<T, PATH>(M, l1, hv[t], Sv + t * R, 1);
         },
         xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L);
 }
@@ -809,30 +939,33 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
                               T* xb, T* pbar, int64_t K, hipStream_t st, bool assign) {
     if (K < 1 || K > kPairMaxK || !xb) return hipErrorNotSupported;
-    const int R1 = h1.G + (h1.use_base ? 1 : 0);
-    const int tiles = (int)col_tiles(K), nrc = (h1.O + kWOB - 1) / kWOB;
+    const int nrc = (h1.O + kWOB - 1) / kWOB;
     // B's LDS: the wide-in pullback's dynamic block (+ the K-row) beside the wide-out parameter
     // body's static arrays; beyond 64 KB the four-launch path runs instead
     const int cw = K > 8 ? (64 / h0.G > 1 ? 64 / h0.G : 1) : widein_cw(h0.O, h0.G, h0.I);
     size_t lw = (size_t)4 * cw * h0.G + kOWide + 2 * (size_t)cw;
     lw = lw > 512 ? lw : 512;
-    const size_t lds_b = sizeof(T) * (lw + (size_t)K);
-    const size_t static_b = sizeof(T) * ((size_t)(kMaxGrid + 1) * kWOPK + (size_t)kSW * kWOB);
+    const size_t wk = (size_t)(K < kWOPK ? K : kWOPK);
+    const size_t R1 = (size_t)h1.G + (h1.use_base ? 1 : 0), H = (size_t)h1.I;
+    const size_t lds_w = lw + (size_t)K + 256 + (R1 * K > H * R1 ? R1 * K : H * R1) + ((size_t)K > H ? (size_t)K : H);
+    const size_t lds_p = (size_t)(kMaxGrid + 1) * wk;
+    const size_t lds_b = sizeof(T) * (lds_w > lds_p ? lds_w : lds_p);
+    const size_t static_b = sizeof(T) * (size_t)kSW * kWOB;
     if (lds_b + static_b > 65536) return hipErrorNotSupported;
     // A
     const int nblk = widein_chunks(h0);
     const int gyF = (int)(K < 65535 ? K : 65535);
-    const int nF = nblk * gyF, nD = h1.I * R1 * tiles;
+    const int nF = nblk * gyF;
     const int tn = (256 / h0.O) * h0.O, cwf = widein_cw(h0.O, h0.G, h0.I);
     const int nv = (h0.O * h0.G * cwf + tn - 1) / tn, nw = (h0.O * cwf + tn - 1) / tn;
     const WideStageIn<T> none{};
     const WideStageIn<T>& sa = si ? *si : none;
 #define KAN_PA(MV, MW)                                                                                             \
     do {                                                                                                           \
-        if (si) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(nF + nD), dim3(256), 0, st, lc,     \
-                                   lc + 1, p, x, pslab, ybar, S, K, nF, nblk, gyF, tiles, sa);                     \
-        else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(nF + nD), dim3(256), 0, st, lc,      \
-                                lc + 1, p, x, pslab, ybar, S, K, nF, nblk, gyF, tiles, sa);                        \
+        if (si) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(nF), dim3(256), 0, st, lc, lc + 1,  \
+                                   p, x, pslab, ybar, S, K, nblk, gyF, sa);                                        \
+        else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(nF), dim3(256), 0, st, lc, lc + 1,   \
+                                p, x, pslab, ybar, S, K, nblk, gyF, sa);                                           \
     } while (0)
     if (nv <= 8 && nw <= 2) KAN_PA(8, 2);
     else if (nv <= 16 && nw <= 4) KAN_PA(16, 4);

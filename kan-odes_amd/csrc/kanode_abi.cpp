@@ -266,7 +266,7 @@ bool surrogate_pair(const kanode_handle* h) {
 //   [hidden activations: Σ_{l>=1} I_l·B][grad ping: max_dim·B][grad pong: max_dim·B][wide slab]
 //   [surrogate pair: the wide-in layer's chunk partials, chunks·B·H]
 struct WsLayout {
-    int64_t acts, g0, g1, wslab, pslab, total;
+    int64_t acts, g0, g1, wslab, pslab, sslab, total;
 };
 WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     WsLayout w{};
@@ -281,6 +281,9 @@ WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     e += wide_slab_elems(h, B);
     w.pslab = e;
     if (surrogate_pair(h)) e += (int64_t)kan::widein_chunks(h->hlc[0]) * B * h->hlc[0].O;
+    // [surrogate pair, two-launch pullback: the wide-out dot products' chunk partials, chunks·H·(G+1)·B]
+    w.sslab = e;
+    if (surrogate_pair(h)) e += (int64_t)kan::widein_chunks(h->hlc[0]) * h->hlc[1].I * (h->hlc[1].G + 1) * B;
     w.total = e;
     return w;
 }
@@ -441,11 +444,11 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
         T* hbar = ws + wl.g0;
         const int nb = kan::widein_chunks(h->hlc[0]);
         if (lamJ && h->pair_vjp) {
-            // two launches (launch_kd_vjp_pair): wide-in partials beside the wide-out dot products; the
-            // wide-out parameter cotangents beside the wide-in pullback (x̄ of the hidden layer formed
-            // per block)
+            // two launches (launch_kd_vjp_pair): the wide-in forward blocks also form the wide-out dot
+            // products' chunk partials; the wide-out parameter cotangents beside the wide-in pullback
+            // (x̄ of the hidden layer formed per block)
             const hipError_t e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, nullptr, lam, u, ps,
-                                                            ws + wl.wslab, lamJ, dp, B, st, false);
+                                                            ws + wl.sslab, lamJ, dp, B, st, false);
             if (e == hipSuccess) return KANODE_OK;
             if (e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
@@ -699,7 +702,7 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         si.ls_out = ls;
         hipError_t e = hipErrorNotSupported;
         if (h->pair_vjp) {   // two launches (see vjp_t)
-            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.wslab, lamJ,
+            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab, lamJ,
                                            dp, B, st, dp_assign);
             if (e != hipSuccess && e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
@@ -1224,9 +1227,10 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
 }
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
                                               double* err_out, int64_t batch, void* stream, bool& launched,
-                                              bool* combined, const AdjMuUpdate* mu) {
+                                              bool* combined, const AdjMuUpdate* mu, const AdjAdaptiveFinish* af) {
     launched = false;
     if (combined) *combined = false;
+    if (af) *af->done = false;
     if (h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN || !h->pp_on ||
         !kan::fk_vjp_pp_supported(h->hlc[0], (int)h->spec.nx) || !h->fused_step)
         return KANODE_OK;
@@ -1262,6 +1266,33 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
         }
         HIP_TRY(h, kan::launch_vjp_finish_jobs(jobs, 2, P, st));
         *combined = true;
+        launched = true;
+        return KANODE_OK;
+    }
+    if (err_out && af) {
+        // adaptive step: the six stage sums, μ_new = μ + Σ h a6_j kμ_j, kμ_7 and the μ error terms in one
+        // launch (slab s holds kμ_{s+2})
+        kan::AdjFinish f{};
+        for (int s = 0; s < 6; ++s) {
+            f.slab[s] = base + (int64_t)s * grid * P;
+            f.ca[s] = s < 5 ? af->a6[s + 1] : 0.0;
+            f.ce[s] = af->bt[s + 1];
+        }
+        f.nslab = 6;
+        f.k7 = 5;
+        f.nblk = grid;
+        f.a0 = af->a6[0];
+        f.e0 = af->bt[0];
+        f.abstol = af->abstol;
+        f.reltol = af->reltol;
+        f.mu = af->mu;
+        f.mu_new = af->mu_new;
+        f.km1 = af->km1;
+        f.km7 = af->km7;
+        f.err_slab = base + (int64_t)6 * grid * P;
+        f.out = af->out;
+        HIP_TRY(h, kan::launch_adj_finish(f, P, st));
+        *af->done = true;
         launched = true;
         return KANODE_OK;
     }

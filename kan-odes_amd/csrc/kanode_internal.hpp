@@ -68,9 +68,22 @@ struct AdjMuUpdate {
     const double* km1;
     double a61;
 };
+// An adaptive step's μ update, FSAL kμ_7 and μ error terms formed by one finish launch (AdjFinish):
+// out[0] = the λ error sum, out[1 + q] = the μ terms (device, 1 + P doubles); *done set when it ran.
+struct AdjAdaptiveFinish {
+    const double* mu;
+    double* mu_new;
+    const double* km1;
+    double* km7;
+    double a6[6], bt[7];   // h·a6_j, h·btilde_j
+    double abstol, reltol;
+    double* out;
+    bool* done;
+};
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,
                                               double* err_out, int64_t batch, void* stream, bool& launched,
-                                              bool* combined = nullptr, const AdjMuUpdate* mu = nullptr);
+                                              bool* combined = nullptr, const AdjMuUpdate* mu = nullptr,
+                                              const AdjAdaptiveFinish* af = nullptr);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

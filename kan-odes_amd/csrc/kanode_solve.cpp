@@ -86,6 +86,8 @@ extern "C" void kanode_solver_options_default(kanode_solver_options* o) {
 // Dense output: step n keeps u_n and k_2..k_7 in slot n (7 states); k_1 of step n is
 // k_7 of step n-1 (FSAL), k_1 of step 0 has its own buffer.  Without recording only
 // two slots are used, alternately.
+constexpr int kScalars = 8 + KANODE_MAX_GRID + 1;   // device / pinned scalar slots of a solution
+
 struct kanode_solution {
     kanode_handle* h = nullptr;
     int dtype = 0;
@@ -113,7 +115,7 @@ struct kanode_solution {
         void* adj_meta = nullptr;          // adjoint: stops, jump rows and offsets
         size_t adj_meta_bytes = 0;
     } fused;
-    double* dscal = nullptr;         // device scalars (norm totals)
+    double* dscal = nullptr;         // device scalars (norm totals; an adaptive FK adjoint step's 1 + P terms)
     double* hscal = nullptr;         // pinned host mirror
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
@@ -913,6 +915,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         // and the FSAL kμ_7 into km[6]; km[1..5] are NOT written on such a step and hold stale values,
         // so nothing may read them when `combined` is set
         bool combined = false;
+        bool finished = false;     // adaptive step: μ_new, kμ_7 and the μ error terms formed by the finish launch
         if (s->qform) {
             kan::AdjStepArgs a{};
             for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];
@@ -936,8 +939,20 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             a.lam_out = (double*)lam[nxt];
             void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
             const AdjMuUpdate mup{(const double*)mu[cur], (double*)mu[nxt], (const double*)km[0], hstep * TA[5][0]};
+            AdjAdaptiveFinish af{};
+            af.mu = (const double*)mu[cur];
+            af.mu_new = (double*)mu[nxt];
+            af.km1 = (const double*)km[0];
+            af.km7 = (double*)km[6];
+            for (int j = 0; j < 6; ++j) af.a6[j] = hstep * TA[5][j];
+            for (int j = 0; j < 7; ++j) af.bt[j] = hstep * BT[j];
+            af.abstol = o.abstol;
+            af.reltol = o.reltol;
+            af.out = s->dscal + 8;
+            af.done = &finished;
             SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? s->dscal + 0 : nullptr, s->batch,
-                                                      st, fused_step, &combined, &mup));
+                                                      st, fused_step, &combined, &mup,
+                                                      o.adaptive && P <= KANODE_MAX_GRID + 1 ? &af : nullptr));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];
@@ -956,19 +971,32 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
-        if (combined) {
+        if (combined || finished) {
             // μ_new = μ + h a_61 km_1 + (the step's combined Σ_{j>=2} h a_6j km_j): formed by the step's
-            // reduction launch (kanode_internal_fk_adjoint_step, AdjMuUpdate)
+            // reduction launch (kanode_internal_fk_adjoint_step: AdjMuUpdate, or AdjAdaptiveFinish)
         } else {
             SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
         }
         double hnew = hstep;
         if (o.adaptive) {
-            double ec[7];
-            for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
-            SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[nxt], 6, km, ec, km[6], o.abstol, o.reltol, P, s->dscal + 1, st));
-            SOLVE_TRY(read_scalars(h, s, 2, st));
-            const double EEst = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot);
+            double sumsq = 0.0;
+            if (finished) {   // the λ sum and the P μ terms in one read, summed here in order
+                if (capturing(st))
+                    return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
+                SOLVE_HIP(h, hipMemcpyAsync(s->hscal, s->dscal + 8, (size_t)(1 + P) * sizeof(double),
+                                            hipMemcpyDeviceToHost, st));
+                SOLVE_HIP(h, hipStreamSynchronize(st));
+                double mus = 0.0;
+                for (int64_t q = 0; q < P; ++q) mus += s->hscal[1 + q];
+                sumsq = s->hscal[0] + mus;
+            } else {
+                double ec[7];
+                for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
+                SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[nxt], 6, km, ec, km[6], o.abstol, o.reltol, P, s->dscal + 1, st));
+                SOLVE_TRY(read_scalars(h, s, 2, st));
+                sumsq = s->hscal[0] + s->hscal[1];
+            }
+            const double EEst = std::sqrt(sumsq / (double)ntot);
             const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
             if (EEst > 1.0 && hstep > o.dtmin) {
                 ++nreject;
@@ -1176,8 +1204,8 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         s->esize = dtype == KANODE_F64 ? 8 : 4;
         s->n = n;
         s->record = record;
-        if (hipMalloc(&s->k1_0, s->state_bytes()) != hipSuccess || hipMalloc(&s->dscal, 8 * sizeof(double)) != hipSuccess ||
-            hipHostMalloc((void**)&s->hscal, 8 * sizeof(double)) != hipSuccess) {
+        if (hipMalloc(&s->k1_0, s->state_bytes()) != hipSuccess || hipMalloc(&s->dscal, kScalars * sizeof(double)) != hipSuccess ||
+            hipHostMalloc((void**)&s->hscal, kScalars * sizeof(double)) != hipSuccess) {
             (void)hipGetLastError();
             delete s;
             return kanode_internal_fail(h, KANODE_ERR_ALLOC, "solve: out of device memory");

@@ -195,10 +195,12 @@ def test_native_surrogate_pair_solve_and_gradient_match_cpu_oracle():
     # 1e-15-level per RHS, carried through the steps)
     assert (ug - uc).abs().max().item() <= 1e-10 * max(1.0, uc.abs().max().item())
     # the same step sequences; the GPU and CPU sums of the 41-wide layers differ at the rounding
-    # level and the adjoint carries that over ~100 stages to 1.2e-8 of the largest dp (measured with
-    # this round's and the previous library alike): 50 reltol, as for differing step sequences
-    assert (gg - gc).abs().max().item() <= 50 * opt.reltol * gc.abs().max().item()
-    assert (gug - guc).abs().max().item() <= 50 * opt.reltol * guc.abs().max().item()
+    # level, and this problem amplifies rounding: moving p by ONE ulp moves dp by 4.2e-8 and du0 by
+    # 9.5e-8 of their largest entries on the GPU (tools/diag/burgers41_spread.py,
+    # profiles/r03/parity/burgers41_spread.txt; the four- and two-launch pullbacks sit at 1.2e-8 /
+    # 2.5e-8 and 2.8e-8 / 6e-8 from the CPU).  The bar is that spread: 200 reltol
+    assert (gg - gc).abs().max().item() <= 200 * opt.reltol * gc.abs().max().item()
+    assert (gug - guc).abs().max().item() <= 200 * opt.reltol * guc.abs().max().item()
 
 
 def test_native_saveat_edges():
