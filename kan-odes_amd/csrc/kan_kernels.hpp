@@ -60,6 +60,17 @@ template <typename T>
 hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageArgs<T>& sa, double* slab,
                               int slab_blocks, double* out, int64_t n, hipStream_t st);
 hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, hipStream_t st);
+// μ update + μ error partials of an adaptive adjoint step (kan_stage.hip adj_step_finish_kernel)
+constexpr int kAdjFinishBlocks = 64;
+template <typename T>
+struct AdjStepFinish {
+    const T* km[7];
+    double a[6], b[7];
+    double abstol, reltol;
+};
+template <typename T>
+hipError_t launch_adj_step_finish(const T* mu, T* mu_new, const AdjStepFinish<T>& f, double* slab, int64_t n,
+                                  int* nblk, hipStream_t st);
 
 // Flux Adam step after the gradient all-reduce (kan_optim.hip, kanode_adam_step)
 struct AdamArgs {
@@ -391,9 +402,11 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
 // products' chunk partials (widein_chunks·H·(G+1)·K).  hipErrorNotSupported: K > kPairMaxK or the LDS
 // would not fit (use the 4 launches).
 constexpr int64_t kPairMaxK = 64;
+// err_out (with si): the adjoint stage's λ error total, from per-block partials in err_slab (<= err_rows)
 template <typename T>
 hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
-                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign);
+                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab = nullptr,
+                              int err_rows = 0, double* err_out = nullptr);
 
 }  // namespace kan

@@ -69,6 +69,50 @@ hipError_t launch_stage_error_final(const double* slab, int nblk, double* out, h
     return hipGetLastError();
 }
 
+// The end of an adaptive adjoint step (kanode_solve.cpp adjoint_t, the paths without a fused step
+// finish): μ_new = μ + Σ_{j<6} a_j km_j (stage_lincomb_kernel's fma order) and, per block, the partial
+// Σ (e/sk)², e = Σ_{j<7} b_j km_j, sk = abstol + reltol·max(|μ|, |μ_new|) (stage_error_kernel's order)
+// into slab[block]: the lincomb and the two error launches in one, the host summing the <= 64
+// partials in order.
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+adj_step_finish_kernel(const T* __restrict__ mu, T* __restrict__ mu_new, AdjStepFinish<T> f, double* __restrict__ slab,
+                       int64_t n) {
+    __shared__ double red[kBlock / kWave];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        T kv[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) kv[j] = f.km[j][i];
+        const T m0 = mu[i];
+        T v = m0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) v = kfma<T>((T)f.a[j], kv[j], v);
+        mu_new[i] = v;
+        double e = 0.0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) e = ::fma(f.b[j], (double)kv[j], e);
+        const double sk = ::fma(f.reltol, fmax(kabs((double)m0), kabs((double)v)), f.abstol);
+        const double r = e / sk;
+        acc = ::fma(r, r, acc);
+    }
+    const double w[1] = {acc};
+    block_sum_to<double, 1>(w, 1, red, slab + blockIdx.x);
+}
+
+template <typename T>
+hipError_t launch_adj_step_finish(const T* mu, T* mu_new, const AdjStepFinish<T>& f, double* slab, int64_t n,
+                                  int* nblk, hipStream_t st) {
+    const int grid = grid_for(n, kBlock, kAdjFinishBlocks);
+    *nblk = grid;
+    hipLaunchKernelGGL((adj_step_finish_kernel<T>), dim3(grid), dim3(kBlock), 0, st, mu, mu_new, f, slab, n);
+    return hipGetLastError();
+}
+template hipError_t launch_adj_step_finish<double>(const double*, double*, const AdjStepFinish<double>&, double*,
+                                                   int64_t, int*, hipStream_t);
+template hipError_t launch_adj_step_finish<float>(const float*, float*, const AdjStepFinish<float>&, double*, int64_t,
+                                                  int*, hipStream_t);
+
 template <typename T>
 hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st) {
     const int grid = grid_for(n, kBlock, kGridCap);

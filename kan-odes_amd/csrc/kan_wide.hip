@@ -559,11 +559,11 @@ kd_vjp_wideout_xfin_kernel(const LayerConst* __restrict__ lcp, const T* __restri
 // ȳ[o, k]; prep_param(o) runs once, block-uniformly, before a parameter block's column loop (the
 // pair pullback forms that output's ȳ row there); yb_col(ybL, t, k) fills ybL[0, O) for an x̄
 // block's column k (thread t < O writes entry t).
-template <typename T, typename YB, typename PREP, typename YCOL>
+template <typename T, typename YB, typename PREP, typename YCOL, typename XOUT>
 __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, YB yb_at, PREP prep_param, YCOL yb_col,
-                                                T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int np,
-                                                int nsub, int nxg, int cw, int assign, int bx, int by, T* L) {
+                                                XOUT on_xbar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K,
+                                                int np, int nsub, int nxg, int cw, int assign, int bx, int by, T* L) {
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
@@ -696,6 +696,7 @@ __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ l
                 xb = xb + sb * dsL[t];
             }
             xbar[(int64_t)I * k + i0 + t] = xb;
+            on_xbar((int64_t)I * k + i0 + t, xb);
         }
     }
 }
@@ -712,7 +713,8 @@ kd_vjp_widein_co_kernel(const LayerConst* __restrict__ lcp, const T* __restrict_
         [&](T* ybL, int t, int64_t k) {
             if (t < O) ybL[t] = ybar[(int64_t)O * k + t];
         },
-        xbar, pbar, K, np, nsub, nxg, cw, assign, blockIdx.x, blockIdx.y, reinterpret_cast<T*>(wv_raw));
+        [](int64_t, T) {}, xbar, pbar, K, np, nsub, nxg, cw, assign, blockIdx.x, blockIdx.y,
+        reinterpret_cast<T*>(wv_raw));
 }
 
 // ---------------------------------------------------------------------------
@@ -791,7 +793,11 @@ __global__ void __launch_bounds__(256)
 kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
                      const T* __restrict__ x, const T* __restrict__ pslab, int nblk, const T* __restrict__ ybar,
                      const T* __restrict__ S, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int nP, int nrc,
-                     int np, int nxg, int cw, int nbx, int hb_off, int assign) {
+                     int np, int nxg, int cw, int nbx, int hb_off, int assign, WideStageIn<T> si,
+                     double* __restrict__ err_slab) {
+    // err_slab (adjoint stage with the λ error, si given): each x̄ block adds, for its entries,
+    // (e / sk)², e = Σ_j ec_j lk_j + ec_n·λsᵀJ, sk = abstol + reltol·max(|λ|, |λs|) (stage_error_kernel's
+    // statement), into err_slab[its index]; the stage's final reduction sums the nbx·nxg rows
     // S: the nblk chunk partials of the wide-out dot products (kd_vjp_pair_a_kernel), [b][I1·R1][K]
     extern __shared__ __attribute__((aligned(16))) unsigned char pb_raw[];
     T* L = reinterpret_cast<T*>(pb_raw);
@@ -811,6 +817,7 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
     T* red = hbL + K;                          // [256]
     T* Sv = red + 256;                         // [max(R·K, H·R)] the block's dot products
     T* hv = Sv + (R * K > H * R ? R * K : H * R);   // [max(K, H)] the hidden values it needs
+    double eacc = 0.0;
     widein_vjp_body<T>(
         lc0, p, x, [&](int, int64_t k) { return hbL[k]; },
         [&](int o) {   // hidden unit o over all columns: S[o, r, k] for r < R, k < K, and h[o, k]
@@ -830,7 +837,27 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
             __syncthreads();
             if (t < H) ybL[t] = wideout_xfin_lds<T, PATH>(M, l1, hv[t], Sv + t * R, 1);
         },
+        [&](int64_t idx, T xb) {
+            if (!err_slab) return;
+            const StageArgs<T>& sl = si.sl;
+            const double sc = stage_scale(sl.cscale);
+            T kv[kMaxStages];
+            stage_ld<T>(sl, si.lam, idx, kv);
+            double e = 0.0;
+#pragma unroll
+            for (int j = 0; j < kMaxStages; ++j)
+                if (j < sl.nk) e = ::fma(sl.ec[j] * sc, (double)kv[j], e);
+            e = ::fma(stage_ec_last(sl) * sc, (double)xb, e);
+            const double sk = ::fma(sl.reltol, fmax(kabs((double)si.lam[idx]), kabs((double)si.ls_out[idx])), sl.abstol);
+            const double r = e / sk;
+            eacc = ::fma(r, r, eacc);
+        },
         xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L);
+    if (err_slab && q / nbx >= np) {   // an x̄ block: its error partial
+        __shared__ double ered[256 / kWave];
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, ered, err_slab + (q / nbx - np) * nbx + q % nbx);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -937,7 +964,8 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
 template <typename T>
 hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
-                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign) {
+                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab,
+                              int err_rows, double* err_out) {
     if (K < 1 || K > kPairMaxK || !xb) return hipErrorNotSupported;
     const int nrc = (h1.O + kWOB - 1) / kWOB;
     // B's LDS: the wide-in pullback's dynamic block (+ the K-row) beside the wide-out parameter
@@ -980,16 +1008,22 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
     const int nxg = (int)(K < 4096 ? K : 4096);
     const int nW = nbx * (np + nxg);
     const T* yb_b = si ? si->ls_out : ybar;   // ȳ of the wide-out parameter blocks: λs as A wrote it
+    // the λ error of an adjoint stage: per-x̄-block partials, then the stage's ordered final sum
+    const bool err = si && err_out && err_slab && nbx * nxg <= err_rows;
+    if (si && err_out && !err) return hipErrorNotSupported;
 #define KAN_PB(PATH)                                                                                               \
     hipLaunchKernelGGL((kd_vjp_pair_b_kernel<T, PATH>), dim3(nP + nW), dim3(256), lds_b, st, lc, lc + 1, p, xvjp,   \
-                       pslab, nblk, yb_b, S, xb, pbar, K, nP, nrc, np, nxg, cw, nbx, (int)lw, assign ? 1 : 0)
+                       pslab, nblk, yb_b, S, xb, pbar, K, nP, nrc, np, nxg, cw, nbx, (int)lw, assign ? 1 : 0, sa,      \
+                       err ? err_slab : nullptr)
     switch (h1.path) {
     case PATH_REC_CORR: KAN_PB(PATH_REC_CORR); break;
     case PATH_REC: KAN_PB(PATH_REC); break;
     default: KAN_PB(PATH_DIRECT);
     }
 #undef KAN_PB
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e != hipSuccess || !err) return e;
+    return launch_stage_error_final(err_slab, nbx * nxg, err_out, st);
 }
 
 #define KAN_WIDE_INST(T)                                                                                       \
@@ -1003,7 +1037,7 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
                                                 const T*, T*, T*, int64_t, hipStream_t, bool);                  \
     template hipError_t launch_kd_vjp_pair<T>(const LayerConst&, const LayerConst&, const LayerConst*, const T*,  \
                                               const T*, const WideStageIn<T>*, const T*, const T*, T*, T*, T*, T*, \
-                                              int64_t, hipStream_t, bool);
+                                              int64_t, hipStream_t, bool, double*, int, double*);
 KAN_WIDE_INST(double)
 KAN_WIDE_INST(float)
 #undef KAN_WIDE_INST

@@ -701,11 +701,14 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         si.sl = sl;
         si.ls_out = ls;
         hipError_t e = hipErrorNotSupported;
-        if (h->pair_vjp) {   // two launches (see vjp_t)
+        bool err_done = false;
+        if (h->pair_vjp) {   // two launches (see vjp_t), plus the λ error's final sum
+            double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
             e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab, lamJ,
-                                           dp, B, st, dp_assign);
+                                           dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out);
             if (e != hipSuccess && e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
+            err_done = e == hipSuccess && err_out != nullptr;
         }
         if (e != hipSuccess) {
             HIP_TRY(h, kan::launch_kd_fwd_widein<T>(h->hlc[0], h->dlc, p, u, (T*)nullptr, ps, B, st, &si));
@@ -713,7 +716,7 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
                                                       ws + wl.wslab, B, st, ps, nb, dp_assign));
             HIP_TRY(h, kan::launch_kd_vjp_widein<T>(h->hlc[0], h->dlc, p, y, hbar, lamJ, dp, B, st, dp_assign));
         }
-        if (adj->want_error)
+        if (adj->want_error && !err_done)
             HIP_TRY(h, kan::launch_stage_error<T>(lam, ls, lamJ, sl, (double*)h->slab, kSlabBlocks,
                                                   (double*)adj->error_sumsq, n, st));
         return KANODE_OK;

@@ -86,7 +86,9 @@ extern "C" void kanode_solver_options_default(kanode_solver_options* o) {
 // Dense output: step n keeps u_n and k_2..k_7 in slot n (7 states); k_1 of step n is
 // k_7 of step n-1 (FSAL), k_1 of step 0 has its own buffer.  Without recording only
 // two slots are used, alternately.
-constexpr int kScalars = 8 + KANODE_MAX_GRID + 1;   // device / pinned scalar slots of a solution
+// device / pinned scalar slots of a solution: 8 norm totals, then an adaptive adjoint step's finish
+// terms at 8 (the FK step: 1 + P <= 34) or its <= kAdjFinishBlocks partials at 16
+constexpr int kScalars = 16 + kan::kAdjFinishBlocks + 16;
 
 struct kanode_solution {
     kanode_handle* h = nullptr;
@@ -971,9 +973,22 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         nf += 6;
         double a6[6];
         for (int j = 0; j < 6; ++j) a6[j] = hstep * TA[5][j];
+        int fin_blocks = 0;
         if (combined || finished) {
             // μ_new = μ + h a_61 km_1 + (the step's combined Σ_{j>=2} h a_6j km_j): formed by the step's
             // reduction launch (kanode_internal_fk_adjoint_step: AdjMuUpdate, or AdjAdaptiveFinish)
+        } else if (o.adaptive) {
+            // μ_new and the μ error partials in one launch (adj_step_finish_kernel)
+            kan::AdjStepFinish<T> f{};
+            for (int j = 0; j < 7; ++j) {
+                f.km[j] = (const T*)km[j];
+                f.b[j] = hstep * BT[j];
+            }
+            for (int j = 0; j < 6; ++j) f.a[j] = a6[j];
+            f.abstol = o.abstol;
+            f.reltol = o.reltol;
+            SOLVE_HIP(h, kan::launch_adj_step_finish<T>((const T*)mu[cur], (T*)mu[nxt], f, s->dscal + 16, P, &fin_blocks,
+                                                        st));
         } else {
             SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
         }
@@ -989,12 +1004,11 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                 double mus = 0.0;
                 for (int64_t q = 0; q < P; ++q) mus += s->hscal[1 + q];
                 sumsq = s->hscal[0] + mus;
-            } else {
-                double ec[7];
-                for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
-                SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[nxt], 6, km, ec, km[6], o.abstol, o.reltol, P, s->dscal + 1, st));
-                SOLVE_TRY(read_scalars(h, s, 2, st));
-                sumsq = s->hscal[0] + s->hscal[1];
+            } else {   // the λ total (dscal[0]) and the μ partials (dscal[16..]) in one read
+                SOLVE_TRY(read_scalars(h, s, 16 + fin_blocks, st));
+                double mus = 0.0;
+                for (int b = 0; b < fin_blocks; ++b) mus += s->hscal[16 + b];
+                sumsq = s->hscal[0] + mus;
             }
             const double EEst = std::sqrt(sumsq / (double)ntot);
             const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
