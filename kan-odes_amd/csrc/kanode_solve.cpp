@@ -872,30 +872,30 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                                          defer);
     };
     const int64_t ntot = n + P;
-    int cur = 0;   // lam[cur], mu[cur] hold λ, μ
-    SOLVE_TRY(adj_rhs(0.0, lam[cur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
+    int lcur = 0, mcur = 0;   // lam[lcur], mu[mcur] hold λ, μ (a saveat jump flips λ alone)
+    SOLVE_TRY(adj_rhs(0.0, lam[lcur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
     int64_t nf = 1;
     double hstep = o.dt;
     if (o.adaptive && !(o.dt > 0)) {
         // Hairer-Wanner on the augmented state [λ; μ] (kanode/adjoint.py)
         const double one = 1.0;
-        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 0, nullptr, &one, lam[cur], o.abstol, o.reltol, n, s->dscal + 0, st));
-        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 0, nullptr, &one, mu[cur], o.abstol, o.reltol, P, s->dscal + 1, st));
-        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 0, nullptr, &one, kl[0], o.abstol, o.reltol, n, s->dscal + 2, st));
-        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 0, nullptr, &one, km[0], o.abstol, o.reltol, P, s->dscal + 3, st));
+        SOLVE_TRY(wsumsq<T>(h, lam[lcur], lam[lcur], 0, nullptr, &one, lam[lcur], o.abstol, o.reltol, n, s->dscal + 0, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[mcur], mu[mcur], 0, nullptr, &one, mu[mcur], o.abstol, o.reltol, P, s->dscal + 1, st));
+        SOLVE_TRY(wsumsq<T>(h, lam[lcur], lam[lcur], 0, nullptr, &one, kl[0], o.abstol, o.reltol, n, s->dscal + 2, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[mcur], mu[mcur], 0, nullptr, &one, km[0], o.abstol, o.reltol, P, s->dscal + 3, st));
         SOLVE_TRY(read_scalars(h, s, 4, st));
         const double d0 = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot);
         const double d1 = std::sqrt((s->hscal[2] + s->hscal[3]) / (double)ntot);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         h0 = std::min(h0, TT);
         void* k1l[1] = {kl[0]};
-        SOLVE_TRY(adj_rhs(h0, lam[cur], 1, k1l, &h0, kl[1], km[1], nullptr, nullptr, nullptr));
+        SOLVE_TRY(adj_rhs(h0, lam[lcur], 1, k1l, &h0, kl[1], km[1], nullptr, nullptr, nullptr));
         ++nf;
         const double e2[2] = {1.0, -1.0};
         const void* a1[1] = {kl[1]};
         const void* b1[1] = {km[1]};
-        SOLVE_TRY(wsumsq<T>(h, lam[cur], lam[cur], 1, a1, e2, kl[0], o.abstol, o.reltol, n, s->dscal + 0, st));
-        SOLVE_TRY(wsumsq<T>(h, mu[cur], mu[cur], 1, b1, e2, km[0], o.abstol, o.reltol, P, s->dscal + 1, st));
+        SOLVE_TRY(wsumsq<T>(h, lam[lcur], lam[lcur], 1, a1, e2, kl[0], o.abstol, o.reltol, n, s->dscal + 0, st));
+        SOLVE_TRY(wsumsq<T>(h, mu[mcur], mu[mcur], 1, b1, e2, km[0], o.abstol, o.reltol, P, s->dscal + 1, st));
         SOLVE_TRY(read_scalars(h, s, 2, st));
         const double d2 = std::sqrt((s->hscal[0] + s->hscal[1]) / (double)ntot) / h0;
         const double mx = std::max(d1, d2);
@@ -910,7 +910,6 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     for (; it < o.maxiters; ++it) {
         if (tau >= TT - 1e-14 * std::max(1.0, TT)) break;
         hstep = std::min(hstep, stops[si] - tau);
-        const int nxt = cur ^ 1;
         bool fused_step = false;   // Fisher-KPP table path, Q-form dense output: the six stages in one launch
         // combined (fixed step, kanode_internal_fk_adjoint_step): the step's reduction launch reduces the
         // stage moments through the combinations the step consumes and writes μ_new itself (AdjMuUpdate)
@@ -937,13 +936,13 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             for (int j = 0; j < 7; ++j) a.ec[j] = hstep * BT[j];
             a.abstol = o.abstol;
             a.reltol = o.reltol;
-            a.lam = (const double*)lam[cur];
-            a.lam_out = (double*)lam[nxt];
+            a.lam = (const double*)lam[lcur];
+            a.lam_out = (double*)lam[lcur ^ 1];
             void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
-            const AdjMuUpdate mup{(const double*)mu[cur], (double*)mu[nxt], (const double*)km[0], hstep * TA[5][0]};
+            const AdjMuUpdate mup{(const double*)mu[mcur], (double*)mu[mcur ^ 1], (const double*)km[0], hstep * TA[5][0]};
             AdjAdaptiveFinish af{};
-            af.mu = (const double*)mu[cur];
-            af.mu_new = (double*)mu[nxt];
+            af.mu = (const double*)mu[mcur];
+            af.mu_new = (double*)mu[mcur ^ 1];
             af.km1 = (const double*)km[0];
             af.km7 = (double*)km[6];
             for (int j = 0; j < 6; ++j) af.a6[j] = hstep * TA[5][j];
@@ -962,10 +961,10 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             if (i == 5) {
                 double ec[7];
                 for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
-                SOLVE_TRY(adj_rhs(tau + hstep, lam[cur], 6, kl, lc, kl[6], km[6], lam[nxt], o.adaptive ? ec : nullptr,
+                SOLVE_TRY(adj_rhs(tau + hstep, lam[lcur], 6, kl, lc, kl[6], km[6], lam[lcur ^ 1], o.adaptive ? ec : nullptr,
                                   s->dscal + 0, true));
             } else {
-                SOLVE_TRY(adj_rhs(tau + TC[i] * hstep, lam[cur], i + 1, kl, lc, kl[i + 1], km[i + 1], nullptr,
+                SOLVE_TRY(adj_rhs(tau + TC[i] * hstep, lam[lcur], i + 1, kl, lc, kl[i + 1], km[i + 1], nullptr,
                                   nullptr, nullptr, true));
             }
         }
@@ -987,10 +986,10 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             for (int j = 0; j < 6; ++j) f.a[j] = a6[j];
             f.abstol = o.abstol;
             f.reltol = o.reltol;
-            SOLVE_HIP(h, kan::launch_adj_step_finish<T>((const T*)mu[cur], (T*)mu[nxt], f, s->dscal + 16, P, &fin_blocks,
+            SOLVE_HIP(h, kan::launch_adj_step_finish<T>((const T*)mu[mcur], (T*)mu[mcur ^ 1], f, s->dscal + 16, P, &fin_blocks,
                                                         st));
         } else {
-            SOLVE_TRY(lincomb<T>(h, mu[cur], 6, km, a6, mu[nxt], P, st));   // μ_new = μ + h Σ a_6j km_j
+            SOLVE_TRY(lincomb<T>(h, mu[mcur], 6, km, a6, mu[mcur ^ 1], P, st));   // μ_new = μ + h Σ a_6j km_j
         }
         double hnew = hstep;
         if (o.adaptive) {
@@ -1023,7 +1022,8 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             qold = std::max(EEst, o.qoldinit);
         }
         tau = tau + hstep;
-        cur = nxt;
+        lcur ^= 1;
+        mcur ^= 1;
         std::swap(kl[0], kl[6]);   // FSAL
         std::swap(km[0], km[6]);
         ++naccept;
@@ -1034,8 +1034,23 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             for (auto& jm : jumps)
                 if (jm.live && (!key || std::fabs(jm.ts - tsv) < std::fabs(key->ts - tsv))) key = &jm;
             if (key && std::fabs(key->ts - tsv) <= eps && si + 1 < stops.size()) {
-                SOLVE_TRY(add_jump(*key, lam[cur]));                       // callback: λ += ∂L/∂u(t_j)
-                SOLVE_TRY(adj_rhs(tau, lam[cur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
+                if (key->rows.size() <= (size_t)KANODE_MAX_STAGES) {
+                    // callback λ += ∂L/∂u(t_j) and the FSAL re-evaluation (u_modified!) as ONE adjoint
+                    // stage: λs = λ + Σ_r 1·g_r (the lincombs' fma order) -> λ_new, kλ_1 = λsᵀJ at λs
+                    void* g[KANODE_MAX_STAGES];
+                    double ones[KANODE_MAX_STAGES];
+                    int ng = 0;
+                    for (int64_t r : key->rows) {
+                        g[ng] = (char*)dl_du + r * sb;
+                        ones[ng++] = 1.0;
+                    }
+                    key->live = false;
+                    SOLVE_TRY(adj_rhs(tau, lam[lcur], ng, g, ones, kl[0], km[0], lam[lcur ^ 1], nullptr, nullptr));
+                    lcur ^= 1;
+                } else {
+                    SOLVE_TRY(add_jump(*key, lam[lcur]));                   // callback: λ += ∂L/∂u(t_j)
+                    SOLVE_TRY(adj_rhs(tau, lam[lcur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
+                }
                 ++nf;                                                      // u_modified!: FSAL re-evaluated
             }
             si = std::min(si + 1, stops.size() - 1);
@@ -1045,9 +1060,9 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     if (it == o.maxiters && !(tau >= TT - 1e-14 * std::max(1.0, TT)))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
     for (auto& jm : jumps)   // a saveat at t0 adds to dL/du0 only
-        if (jm.live && std::fabs(jm.ts - t0) <= eps) SOLVE_TRY(add_jump(jm, lam[cur]));
-    if (du0) SOLVE_HIP(h, hipMemcpyAsync(du0, lam[cur], sb, hipMemcpyDeviceToDevice, st));
-    if (dp) SOLVE_HIP(h, hipMemcpyAsync(dp, mu[cur], pb, hipMemcpyDeviceToDevice, st));
+        if (jm.live && std::fabs(jm.ts - t0) <= eps) SOLVE_TRY(add_jump(jm, lam[lcur]));
+    if (du0) SOLVE_HIP(h, hipMemcpyAsync(du0, lam[lcur], sb, hipMemcpyDeviceToDevice, st));
+    if (dp) SOLVE_HIP(h, hipMemcpyAsync(dp, mu[mcur], pb, hipMemcpyDeviceToDevice, st));
     if (stats) {
         stats->naccept = naccept;
         stats->nreject = nreject;

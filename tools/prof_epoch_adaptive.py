@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""bench.py's adaptive reference-problem epoch (FK256, T = 5, saveat 0.5, default tolerances) for
+rocprofv3 traces:  python3 tools/prof_epoch_adaptive.py [--batch 4096] [--reps 1]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kan-odes_amd")]
+import kanode  # noqa: E402
+import bench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=4096)
+ap.add_argument("--reps", type=int, default=1)
+a = ap.parse_args()
+kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
+p_np = kan1.setup(np.random.default_rng(0))[0].astype(np.float64)
+out = bench.epoch_adaptive_bench(torch.device("cuda:0"), p_np, 256, 1 / 255, 0.01, a.batch, 0, reps=a.reps)
+print(out, flush=True)
