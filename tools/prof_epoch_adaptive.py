@@ -17,7 +17,6 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--reps", type=int, default=1)
 a = ap.parse_args()
-kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
-p_np = kan1.setup(np.random.default_rng(0))[0].astype(np.float64)
+p_np = bench.fk_trained_like_params()
 out = bench.epoch_adaptive_bench(torch.device("cuda:0"), p_np, 256, 1 / 255, 0.01, a.batch, 0, reps=a.reps)
 print(out, flush=True)
