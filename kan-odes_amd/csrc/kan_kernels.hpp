@@ -403,10 +403,13 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
 // would not fit (use the 4 launches).
 constexpr int64_t kPairMaxK = 64;
 // err_out (with si): the adjoint stage's λ error total, from per-block partials in err_slab (<= err_rows)
+// bas (nullable): the wide-in basis store the forward blocks fill and the pullback blocks read
 template <typename T>
 hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
                               T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab = nullptr,
-                              int err_rows = 0, double* err_out = nullptr);
+                              int err_rows = 0, double* err_out = nullptr, T* bas = nullptr);
+// elements of the pair's wide-in basis store (bas above: φ [K][I][G], swish and swish' [K][I])
+inline int64_t pair_basis_elems(const LayerConst& h0, int64_t K) { return K * h0.I * (h0.G + 2); }
 
 }  // namespace kan

@@ -28,6 +28,15 @@
 
 namespace kan {
 
+// KAN_ABL (timing experiments only, tools/surr_ablate.sh; results are wrong when set): 1 the wide-in
+// parameter blocks' column loop, 3 the dot-product gathers, 7 the pair forward's dot products skipped;
+// 4 / 5 / 6 the pair pullback's wide-out parameter / x̄ / wide-in parameter blocks exit at once; 8 / 9
+// the pair's first / second launch exits at once
+#ifndef KAN_ABL
+#define KAN_ABL 0
+#endif
+
+
 constexpr int kKT = 8;        // column tile (trajectories per pass)
 constexpr int kOWide = 16;    // max out_dims of a wide-in layer
 
@@ -114,11 +123,22 @@ __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const S
 // that holds ȳ[i0 .. i0 + ni, k] (λs it formed, or λ) forms the partial sums
 //     spart[(bx·IR + q)·K + k] = Σ_{o in chunk} row_q[o] ȳ[o, k],   row_q = C2[:, r + G2 i2] (r < G2) or
 // W2[:, i2] (r = G2), q = i2·R2 + r, IR = I2·R2; the consumer sums the nblk chunk partials in order.
+// The pair's forward blocks also store the wide-in layer's basis values, which the pullback's
+// parameter and x̄ blocks would otherwise recompute (one exponential each, ten times over for the
+// ten parameter blocks of a chunk): phi[(k·I + i)·G + g] = φ_g(x_ik), sw / dsw[k·I + i] = swish(x_ik)
+// and its rrule derivative.  Bitwise the values the recomputation gives (same statements).
+template <typename T>
+struct WideBasisG {
+    T* phi;
+    T* sw;
+    T* dsw;
+};
 template <typename T>
 struct PairDot {
     const LayerConst* lc1;
     T* spart;
     const T* ybar;   // ȳ without a stage (λ); with a stage, λs as the block forms it
+    WideBasisG<T> bg;   // basis store (bg.phi == nullptr: none)
 };
 template <typename T, bool STAGE, int MV, int MW, bool DOT = false>
 __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
@@ -175,8 +195,23 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             const T xi = STAGE ? xL[i] : x[(int64_t)I * k + i0 + i];
             const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
             T aux = T(0);
-            phiL[c] = basis_direct<T>(M, lc.basis, (n - T(lc.grid[g])) * T(lc.invh), aux);
-            if (g == 0) swL[i] = lc.use_base ? swish<T>(M, xi) : T(0);
+            const T ph = basis_direct<T>(M, lc.basis, (n - T(lc.grid[g])) * T(lc.invh), aux);
+            phiL[c] = ph;
+            bool stored = false;
+            if constexpr (DOT) {
+                if (pd->bg.phi) {
+                    pd->bg.phi[((int64_t)I * k + i0) * G + c] = ph;
+                    if (g == 0) {
+                        T sw = T(0), dsw = T(0);
+                        if (lc.use_base) swish_and_grad<T>(M, xi, sw, dsw);
+                        swL[i] = sw;
+                        pd->bg.sw[(int64_t)I * k + i0 + i] = sw;
+                        pd->bg.dsw[(int64_t)I * k + i0 + i] = dsw;
+                    }
+                    stored = true;
+                }
+            }
+            if (g == 0 && !stored) swL[i] = lc.use_base ? swish<T>(M, xi) : T(0);
         }
         __syncthreads();
         T acc = T(0);
@@ -203,13 +238,15 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             const LayerConst& l1 = *pd->lc1;
             const int R1 = l1.G + (l1.use_base ? 1 : 0), IR = l1.I * R1, O1 = l1.O;
             const int ns = IR >= 256 ? 1 : 256 / IR;
-            for (int q0 = 0; q0 < IR; q0 += 256 / ns) {
+            for (int q0 = 0; q0 < (KAN_ABL == 7 ? 0 : IR); q0 += 256 / ns) {
                 const int q = q0 + t / ns, sub = t - (t / ns) * ns;
                 T a = T(0);
                 if (q < IR && t / ns < 256 / ns) {
                     const int i2 = q / R1, r = q - i2 * R1;
                     const T* __restrict__ row =
                         r < l1.G ? p + l1.p_off + (int64_t)O1 * (r + (int64_t)l1.G * i2) : p + l1.w_off + (int64_t)O1 * i2;
+                    // (eight row loads in flight before the fma chain measured slower: Burgers VJP
+                    // 15.9 -> 17.1 us)
                     for (int e = sub; e < ni; e += ns) a = kfma<T>(row[i0 + e], lsL[e], a);
                 }
                 red[t] = a;
@@ -563,7 +600,8 @@ template <typename T, typename YB, typename PREP, typename YCOL, typename XOUT>
 __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, YB yb_at, PREP prep_param, YCOL yb_col,
                                                 XOUT on_xbar, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K,
-                                                int np, int nsub, int nxg, int cw, int assign, int bx, int by, T* L) {
+                                                int np, int nsub, int nxg, int cw, int assign, int bx, int by, T* L,
+                                                const WideBasisG<T>* bg = nullptr) {
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1): no staging round trip
     const LayerConst& lc = *lcp;
     const int I = lc.I, O = lc.O, G = lc.G;
@@ -592,7 +630,39 @@ __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ l
         T dcv[kS], dwv[kS];
 #pragma unroll
         for (int m = 0; m < kS; ++m) dcv[m] = dwv[m] = T(0);
-        if (q < nq) {
+        if (q < nq && KAN_ABL != 1 && bg) {
+            // the basis values the pair's forward blocks stored (WideBasisG): per slot, eight columns'
+            // loads in flight, accumulated in ascending k (the per-slot order of the loop below)
+            const int64_t ps = (int64_t)I * G;
+#pragma unroll
+            for (int m = 0; m < kS; ++m) {
+                const int c = c0 + cb + 256 * m;
+                if ((nq == 1 || m == 0) && c < c1) {
+                    const int i = c / G, g = c - i * G;
+                    const bool wsl = base && g == 0;
+                    const T* __restrict__ ph = bg->phi + (int64_t)i0 * G + c;
+                    const T* __restrict__ sw = bg->sw + i0 + i;
+                    for (int64_t k0 = q; k0 < K; k0 += 8 * nq) {
+                        T pv[8], sv[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int64_t k = k0 + j * nq;
+                            pv[j] = k < K ? ph[k * ps] : T(0);
+                            sv[j] = k < K && wsl ? sw[k * I] : T(0);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int64_t k = k0 + j * nq;
+                            if (k < K) {
+                                const T yb = yb_at(o, k);
+                                dcv[m] = kfma<T>(yb, pv[j], dcv[m]);
+                                if (wsl) dwv[m] = kfma<T>(yb, sv[j], dwv[m]);
+                            }
+                        }
+                    }
+                }
+            }
+        } else if (q < nq && KAN_ABL != 1) {
             for (int64_t k = q; k < K; k += nq) {
                 const T yb = yb_at(o, k);
 #pragma unroll
@@ -659,21 +729,28 @@ __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ l
     const T* __restrict__ W = p + lc.w_off + (int64_t)O * i0;
     for (int64_t k = (int64_t)by - np * nsub; k < K; k += nxg) {
         __syncthreads();
+        const bool stored = bg && lc.basis == BASIS_RBF;   // the rbf rrule needs φ and z only
         for (int c = t; c < nc; c += blockDim.x) {
             const int i = c / G, g = c - i * G;
+            const T pst = stored ? bg->phi[((int64_t)I * k + i0) * G + c] : T(0);
+            const T dst = stored && base && g == 0 ? bg->dsw[(int64_t)I * k + i0 + i] : T(0);
             const T xi = x[(int64_t)I * k + i0 + i];
             const T n = normalize<NORM_RUNTIME, T>(M, lc.norm, xi);
             const T z = (n - T(lc.grid[g])) * invh;
             T aux = T(0);
-            phL[c] = basis_direct<T>(M, lc.basis, z, aux);
+            phL[c] = stored ? pst : basis_direct<T>(M, lc.basis, z, aux);
             zL[c] = z;
             auL[c] = aux;
             if (g == 0) {
                 dnL[i] = dnormalize<NORM_RUNTIME, T>(lc.norm, n);
                 if (base) {
-                    T sw, dsw;
-                    swish_and_grad<T>(M, xi, sw, dsw);
-                    dsL[i] = dsw;
+                    if (stored) {
+                        dsL[i] = dst;
+                    } else {
+                        T sw, dsw;
+                        swish_and_grad<T>(M, xi, sw, dsw);
+                        dsL[i] = dsw;
+                    }
                 }
             }
         }
@@ -734,10 +811,75 @@ template <typename T, int MV, int MW, bool STAGE>
 __global__ void __launch_bounds__(256)
 kd_vjp_pair_a_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
                      const T* __restrict__ x, T* __restrict__ pslab, const T* __restrict__ ybar, T* __restrict__ spart,
-                     int64_t K, int nblk, int gyF, WideStageIn<T> si) {
-    const PairDot<T> pd{lc1, spart, ybar};
+                     int64_t K, int nblk, int gyF, WideStageIn<T> si, WideBasisG<T> bg) {
+    if (KAN_ABL == 8) return;
+    const PairDot<T> pd{lc1, spart, ybar, bg};
     widein_fwd_body<T, STAGE, MV, MW, true>(lc0, p, x, pslab, K, STAGE ? &si : nullptr, blockIdx.x % nblk,
                                             blockIdx.x / nblk, gyF, &pd);
+}
+
+// Wide-out parameter cotangents in the pair pullback: one wave per unit (row chunk bx, hidden input i),
+// four units per block.  Lanes k < K stage the basis of input i for every column in the wave's LDS block
+// Ph [(G + 1)][K] (the hidden value summed from the wide-in chunk partials), then lane o accumulates
+// dC[o, g + G i] = Σ_k ȳ[o, k] φ_g(h_ik) and dW[o, i] = Σ_k ȳ[o, k] swish(h_ik) over the columns in
+// ascending k (eight ȳ loads in flight) and writes them: no cross-wave partial sums, one barrier.
+// (The four-launch path's wideout_param_body splits the columns over the block's four waves and sums
+// their partials through LDS: eleven rounds of two barriers for G = 10.)
+template <typename T, int PATH>
+__device__ __forceinline__ void wideout_param_wave(const Math<T>& M, const LayerConst& lc, const T* __restrict__ xslab,
+                                                   int nblk, const T* __restrict__ ybar, T* __restrict__ pbar,
+                                                   int64_t K, int unit, int nunits, int nrc, int assign,
+                                                   T* __restrict__ Ph) {
+    const int I = lc.I, O = lc.O, G = lc.G;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool live = unit < nunits;
+    const int bx = live ? unit % nrc : 0, i = live ? unit / nrc : 0;
+    const bool base = lc.use_base != 0;
+    if (live) {
+        for (int64_t kk = lane; kk < K; kk += kWave) {
+            const T xi = layer_in<T>(nullptr, xslab, nblk, I, K, i, kk);
+            Basis1<T, PATH> bs;
+            bs.init(M, lc, xi);
+            for (int g = 0; g < G; ++g) {
+                T z, aux;
+                Ph[g * K + kk] = bs.next(M, lc, g, z, aux);
+            }
+            Ph[(int64_t)G * K + kk] = base ? swish<T>(M, xi) : T(0);
+        }
+    }
+    __syncthreads();   // (every wave of the block is a parameter wave: uniform)
+    const int o = bx * kWOB + lane;
+    if (!live || o >= O) return;
+    T acc[kMaxGrid + 1];
+#pragma unroll
+    for (int r = 0; r <= kMaxGrid; ++r) acc[r] = T(0);
+    for (int64_t k0 = 0; k0 < K; k0 += 8) {
+        T yv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) yv[j] = k0 + j < K ? ybar[(int64_t)O * (k0 + j) + o] : T(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (k0 + j < K) {
+                const int64_t k = k0 + j;
+#pragma unroll
+                for (int r = 0; r < kMaxGrid; ++r)
+                    if (r < G) acc[r] = kfma<T>(yv[j], Ph[r * K + k], acc[r]);
+                acc[kMaxGrid] = kfma<T>(yv[j], Ph[(int64_t)G * K + k], acc[kMaxGrid]);
+            }
+        }
+    }
+    T* __restrict__ dC = pbar + lc.p_off + o + (int64_t)O * G * i;
+#pragma unroll
+    for (int r = 0; r < kMaxGrid; ++r) {
+        if (r < G) {
+            T* d = dC + (int64_t)O * r;
+            *d = assign ? acc[r] : *d + acc[r];
+        }
+    }
+    if (base) {
+        T* d = pbar + lc.w_off + o + (int64_t)O * i;
+        *d = assign ? acc[kMaxGrid] : *d + acc[kMaxGrid];
+    }
 }
 
 // x̄ of one wide-out input from its value xi and its dot products Sl[g·ss] (g < G; the swish row at G)
@@ -794,7 +936,7 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
                      const T* __restrict__ x, const T* __restrict__ pslab, int nblk, const T* __restrict__ ybar,
                      const T* __restrict__ S, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int nP, int nrc,
                      int np, int nxg, int cw, int nbx, int hb_off, int assign, WideStageIn<T> si,
-                     double* __restrict__ err_slab) {
+                     double* __restrict__ err_slab, WideBasisG<T> bg) {
     // err_slab (adjoint stage with the λ error, si given): each x̄ block adds, for its entries,
     // (e / sk)², e = Σ_j ec_j lk_j + ec_n·λsᵀJ, sk = abstol + reltol·max(|λ|, |λs|) (stage_error_kernel's
     // statement), into err_slab[its index]; the stage's final reduction sums the nbx·nxg rows
@@ -803,10 +945,14 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
     T* L = reinterpret_cast<T*>(pb_raw);
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1)
     const int b = blockIdx.x;
-    if (b < nP) {
-        const int wk = (int)(K < kWOPK ? K : kWOPK);
-        wideout_param_body<T, PATH>(M, lc1, (const T*)nullptr, pslab, nblk, ybar, pbar, K, b % nrc, b / nrc, assign, L,
-                                    wk);
+    if (KAN_ABL == 9 || (KAN_ABL == 4 && b < nP)) return;
+    if (KAN_ABL == 5 && b >= nP && (b - nP) / nbx >= np) return;
+    if (KAN_ABL == 6 && b >= nP && (b - nP) / nbx < np) return;
+    if (b < nP) {   // four wide-out parameter units per block, one per wave
+        const int w = threadIdx.x / kWave;
+        const int64_t ph = (int64_t)(lc1->G + 1) * K;
+        wideout_param_wave<T, PATH>(M, *lc1, pslab, nblk, ybar, pbar, K, 4 * b + w, nrc * lc1->I, nrc, assign,
+                                    L + w * ph);
         return;
     }
     const int q = b - nP;
@@ -821,8 +967,8 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
     widein_vjp_body<T>(
         lc0, p, x, [&](int, int64_t k) { return hbL[k]; },
         [&](int o) {   // hidden unit o over all columns: S[o, r, k] for r < R, k < K, and h[o, k]
-            block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K, nblk,
-                                 red, Sv);
+            block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K,
+                                 KAN_ABL == 3 ? 0 : nblk, red, Sv);
             for (int64_t k = threadIdx.x; k < K; k += blockDim.x)
                 hv[k] = layer_in<T>(nullptr, pslab, nblk, H, K, o, k);
             __syncthreads();
@@ -832,7 +978,7 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
         },
         [&](T* ybL, int t, int64_t k) {   // column k over all hidden units: S[i, r, k] and h[i, k]
             block_gather_sums<T>(
-                [&](int v, int c) { return S[c * bs + (int64_t)v * K + k]; }, H * R, nblk, red, Sv);
+                [&](int v, int c) { return S[c * bs + (int64_t)v * K + k]; }, H * R, KAN_ABL == 3 ? 0 : nblk, red, Sv);
             if (t < H) hv[t] = layer_in<T>(nullptr, pslab, nblk, H, K, t, k);
             __syncthreads();
             if (t < H) ybL[t] = wideout_xfin_lds<T, PATH>(M, l1, hv[t], Sv + t * R, 1);
@@ -852,7 +998,7 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
             const double r = e / sk;
             eacc = ::fma(r, r, eacc);
         },
-        xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L);
+        xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L, bg.phi ? &bg : nullptr);
     if (err_slab && q / nbx >= np) {   // an x̄ block: its error partial
         __shared__ double ered[256 / kWave];
         const double v[1] = {eacc};
@@ -965,21 +1111,26 @@ template <typename T>
 hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
                               const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
                               T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab,
-                              int err_rows, double* err_out) {
+                              int err_rows, double* err_out, T* bas) {
     if (K < 1 || K > kPairMaxK || !xb) return hipErrorNotSupported;
+    // the wide-in basis store (WideBasisG): phi [K][I][G], sw [K][I], dsw [K][I]
+    WideBasisG<T> bg{};
+    if (bas) {
+        bg.phi = bas;
+        bg.sw = bas + K * h0.I * h0.G;
+        bg.dsw = bg.sw + K * h0.I;
+    }
     const int nrc = (h1.O + kWOB - 1) / kWOB;
     // B's LDS: the wide-in pullback's dynamic block (+ the K-row) beside the wide-out parameter
     // body's static arrays; beyond 64 KB the four-launch path runs instead
     const int cw = K > 8 ? (64 / h0.G > 1 ? 64 / h0.G : 1) : widein_cw(h0.O, h0.G, h0.I);
     size_t lw = (size_t)4 * cw * h0.G + kOWide + 2 * (size_t)cw;
     lw = lw > 512 ? lw : 512;
-    const size_t wk = (size_t)(K < kWOPK ? K : kWOPK);
-    const size_t R1 = (size_t)h1.G + (h1.use_base ? 1 : 0), H = (size_t)h1.I;
+    const size_t R1 = (size_t)h1.G + (h1.use_base ? 1 : 0), H = (size_t)h1.I, R1w = (size_t)h1.G + 1;
     const size_t lds_w = lw + (size_t)K + 256 + (R1 * K > H * R1 ? R1 * K : H * R1) + ((size_t)K > H ? (size_t)K : H);
-    const size_t lds_p = (size_t)(kMaxGrid + 1) * wk;
+    const size_t lds_p = 4 * R1w * (size_t)K;   // wideout_param_wave: four waves' [(G + 1)][K] blocks
     const size_t lds_b = sizeof(T) * (lds_w > lds_p ? lds_w : lds_p);
-    const size_t static_b = sizeof(T) * (size_t)kSW * kWOB;
-    if (lds_b + static_b > 65536) return hipErrorNotSupported;
+    if (lds_b > 65536) return hipErrorNotSupported;
     // A
     const int nblk = widein_chunks(h0);
     const int gyF = (int)(K < 65535 ? K : 65535);
@@ -991,9 +1142,9 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
 #define KAN_PA(MV, MW)                                                                                             \
     do {                                                                                                           \
         if (si) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(nF), dim3(256), 0, st, lc, lc + 1,  \
-                                   p, x, pslab, ybar, S, K, nblk, gyF, sa);                                        \
+                                   p, x, pslab, ybar, S, K, nblk, gyF, sa, bg);                                    \
         else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(nF), dim3(256), 0, st, lc, lc + 1,   \
-                                p, x, pslab, ybar, S, K, nblk, gyF, sa);                                           \
+                                p, x, pslab, ybar, S, K, nblk, gyF, sa, bg);                                       \
     } while (0)
     if (nv <= 8 && nw <= 2) KAN_PA(8, 2);
     else if (nv <= 16 && nw <= 4) KAN_PA(16, 4);
@@ -1002,7 +1153,7 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // B
-    const int nP = pbar ? nrc * h1.I : 0;
+    const int nP = pbar ? (nrc * h1.I + 3) / 4 : 0;   // wide-out parameter blocks, four units each
     const int nbx = (h0.I + cw - 1) / cw;
     const int np = pbar ? h0.O : 0;
     const int nxg = (int)(K < 4096 ? K : 4096);
@@ -1014,7 +1165,7 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
 #define KAN_PB(PATH)                                                                                               \
     hipLaunchKernelGGL((kd_vjp_pair_b_kernel<T, PATH>), dim3(nP + nW), dim3(256), lds_b, st, lc, lc + 1, p, xvjp,   \
                        pslab, nblk, yb_b, S, xb, pbar, K, nP, nrc, np, nxg, cw, nbx, (int)lw, assign ? 1 : 0, sa,      \
-                       err ? err_slab : nullptr)
+                       err ? err_slab : nullptr, bg)
     switch (h1.path) {
     case PATH_REC_CORR: KAN_PB(PATH_REC_CORR); break;
     case PATH_REC: KAN_PB(PATH_REC); break;
@@ -1037,7 +1188,7 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
                                                 const T*, T*, T*, int64_t, hipStream_t, bool);                  \
     template hipError_t launch_kd_vjp_pair<T>(const LayerConst&, const LayerConst&, const LayerConst*, const T*,  \
                                               const T*, const WideStageIn<T>*, const T*, const T*, T*, T*, T*, T*, \
-                                              int64_t, hipStream_t, bool, double*, int, double*);
+                                              int64_t, hipStream_t, bool, double*, int, double*, T*);
 KAN_WIDE_INST(double)
 KAN_WIDE_INST(float)
 #undef KAN_WIDE_INST

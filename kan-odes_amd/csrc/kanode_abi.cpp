@@ -266,7 +266,7 @@ bool surrogate_pair(const kanode_handle* h) {
 //   [hidden activations: Σ_{l>=1} I_l·B][grad ping: max_dim·B][grad pong: max_dim·B][wide slab]
 //   [surrogate pair: the wide-in layer's chunk partials, chunks·B·H]
 struct WsLayout {
-    int64_t acts, g0, g1, wslab, pslab, sslab, total;
+    int64_t acts, g0, g1, wslab, pslab, sslab, bslab, total;
 };
 WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     WsLayout w{};
@@ -284,6 +284,9 @@ WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     // [surrogate pair, two-launch pullback: the wide-out dot products' chunk partials, chunks·H·(G+1)·B]
     w.sslab = e;
     if (surrogate_pair(h)) e += (int64_t)kan::widein_chunks(h->hlc[0]) * h->hlc[1].I * (h->hlc[1].G + 1) * B;
+    // [surrogate pair, two-launch pullback: the wide-in layer's basis store, B·I·(G + 2)]
+    w.bslab = e;
+    if (surrogate_pair(h)) e += kan::pair_basis_elems(h->hlc[0], B);
     w.total = e;
     return w;
 }
@@ -448,7 +451,8 @@ kanode_status vjp_t(kanode_handle* h, const T* p, const T* u, const T* lam, T* l
             // products' chunk partials; the wide-out parameter cotangents beside the wide-in pullback
             // (x̄ of the hidden layer formed per block)
             const hipError_t e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, nullptr, lam, u, ps,
-                                                            ws + wl.sslab, lamJ, dp, B, st, false);
+                                                            ws + wl.sslab, lamJ, dp, B, st, false, nullptr, 0,
+                                                            nullptr, ws + wl.bslab);
             if (e == hipSuccess) return KANODE_OK;
             if (e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
@@ -705,7 +709,8 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         if (h->pair_vjp) {   // two launches (see vjp_t), plus the λ error's final sum
             double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
             e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab, lamJ,
-                                           dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out);
+                                           dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out,
+                                           ws + wl.bslab);
             if (e != hipSuccess && e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
             err_done = e == hipSuccess && err_out != nullptr;

@@ -118,7 +118,12 @@ struct kanode_solution {
         size_t adj_meta_bytes = 0;
     } fused;
     double* dscal = nullptr;         // device scalars (norm totals; an adaptive FK adjoint step's 1 + P terms)
-    double* hscal = nullptr;         // pinned host mirror
+    double* hscal = nullptr;         // pinned host mirror (mapped, coherent)
+    // device address of hscal: the host-controlled adaptive loops have their step-control scalars written
+    // there by the producing kernels, so reading them costs a stream synchronisation and no copy launch
+    // (a D2H hipMemcpyAsync of 8 bytes ran as a ~4.4 us blit kernel, twice per FK training step).
+    // nullptr if the runtime gave no device address: those loops then copy from dscal as before.
+    double* mscal = nullptr;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -255,6 +260,17 @@ kanode_status read_scalars(kanode_handle* h, kanode_solution* s, int cnt, hipStr
     return KANODE_OK;
 }
 
+// Step-control scalars of the host-controlled adaptive loops: where the producing kernels write them
+// (ctl) and how the host gets slots [off, off + cnt) into hscal (read_ctl).
+inline double* ctl(kanode_solution* s) { return s->mscal ? s->mscal : s->dscal; }
+kanode_status read_ctl(kanode_handle* h, kanode_solution* s, int off, int cnt, hipStream_t st) {
+    if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
+    if (!s->mscal)
+        SOLVE_HIP(h, hipMemcpyAsync(s->hscal + off, s->dscal + off, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    return KANODE_OK;
+}
+
 kanode_stage make_stage(int nk, void* const* k, const double* c) {
     kanode_stage sg{};
     sg.n_prev = nk;
@@ -347,7 +363,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             void* kout[6] = {s->q(step, 1), s->q(step, 2), s->q(step, 3), s->q(step, 4), nullptr, s->k(step, 7)};
             SOLVE_TRY(kanode_internal_fk_step(h, p, s->u(step), ks[0], kout, s->u(step + 1), a66,
                                               o.adaptive ? e7 : nullptr, q47, o.abstol, o.reltol,
-                                              o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
+                                              o.adaptive ? ctl(s) : nullptr, s->batch, st, fused_step));
             if (!fused_step) return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5: fused step not launched");
         } else {   // a small chain: the six stages per column in one launch
             double a66[36] = {}, e7[7];
@@ -356,7 +372,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             for (int j = 0; j < 7; ++j) e7[j] = dt * BT[j];
             SOLVE_TRY(kanode_internal_chain_step(h, p, s->u(step), ks[0], ks + 1, s->u(step + 1), a66,
                                                  o.adaptive ? e7 : nullptr, o.abstol, o.reltol,
-                                                 o.adaptive ? s->dscal : nullptr, s->batch, st, fused_step));
+                                                 o.adaptive ? ctl(s) : nullptr, s->batch, st, fused_step));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double c[6];
@@ -369,7 +385,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
                     for (int j = 0; j < 7; ++j) sg.ec[j] = dt * BT[j];
                     sg.abstol = o.abstol;
                     sg.reltol = o.reltol;
-                    sg.error_sumsq = s->dscal;
+                    sg.error_sumsq = ctl(s);
                 }
             }
             SOLVE_TRY(kanode_rhs_stage(h, p, s->u(step), &sg, ks[i + 1], s->batch, st));
@@ -377,7 +393,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         nf += 6;
         double dtnew = dt;
         if (o.adaptive) {
-            SOLVE_TRY(read_scalars(h, s, 1, st));
+            SOLVE_TRY(read_ctl(h, s, 0, 1, st));
             const double EEst = std::sqrt(s->hscal[0] / (double)s->n);
             const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
             if (EEst > 1.0 && dt > o.dtmin) {
@@ -949,9 +965,9 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             for (int j = 0; j < 7; ++j) af.bt[j] = hstep * BT[j];
             af.abstol = o.abstol;
             af.reltol = o.reltol;
-            af.out = s->dscal + 8;
+            af.out = ctl(s) + 8;
             af.done = &finished;
-            SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? s->dscal + 0 : nullptr, s->batch,
+            SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? ctl(s) + 0 : nullptr, s->batch,
                                                       st, fused_step, &combined, &mup,
                                                       o.adaptive && P <= KANODE_MAX_GRID + 1 ? &af : nullptr));
         }
@@ -962,7 +978,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                 double ec[7];
                 for (int j = 0; j < 7; ++j) ec[j] = hstep * BT[j];
                 SOLVE_TRY(adj_rhs(tau + hstep, lam[lcur], 6, kl, lc, kl[6], km[6], lam[lcur ^ 1], o.adaptive ? ec : nullptr,
-                                  s->dscal + 0, true));
+                                  ctl(s) + 0, true));
             } else {
                 SOLVE_TRY(adj_rhs(tau + TC[i] * hstep, lam[lcur], i + 1, kl, lc, kl[i + 1], km[i + 1], nullptr,
                                   nullptr, nullptr, true));
@@ -986,7 +1002,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             for (int j = 0; j < 6; ++j) f.a[j] = a6[j];
             f.abstol = o.abstol;
             f.reltol = o.reltol;
-            SOLVE_HIP(h, kan::launch_adj_step_finish<T>((const T*)mu[mcur], (T*)mu[mcur ^ 1], f, s->dscal + 16, P, &fin_blocks,
+            SOLVE_HIP(h, kan::launch_adj_step_finish<T>((const T*)mu[mcur], (T*)mu[mcur ^ 1], f, ctl(s) + 16, P, &fin_blocks,
                                                         st));
         } else {
             SOLVE_TRY(lincomb<T>(h, mu[mcur], 6, km, a6, mu[mcur ^ 1], P, st));   // μ_new = μ + h Σ a_6j km_j
@@ -995,16 +1011,12 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         if (o.adaptive) {
             double sumsq = 0.0;
             if (finished) {   // the λ sum and the P μ terms in one read, summed here in order
-                if (capturing(st))
-                    return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
-                SOLVE_HIP(h, hipMemcpyAsync(s->hscal, s->dscal + 8, (size_t)(1 + P) * sizeof(double),
-                                            hipMemcpyDeviceToHost, st));
-                SOLVE_HIP(h, hipStreamSynchronize(st));
+                SOLVE_TRY(read_ctl(h, s, 8, (int)(1 + P), st));
                 double mus = 0.0;
-                for (int64_t q = 0; q < P; ++q) mus += s->hscal[1 + q];
-                sumsq = s->hscal[0] + mus;
-            } else {   // the λ total (dscal[0]) and the μ partials (dscal[16..]) in one read
-                SOLVE_TRY(read_scalars(h, s, 16 + fin_blocks, st));
+                for (int64_t q = 0; q < P; ++q) mus += s->hscal[9 + q];
+                sumsq = s->hscal[8] + mus;
+            } else {   // the λ total (slot 0) and the μ partials (slots 16..) in one read
+                SOLVE_TRY(read_ctl(h, s, 0, 16 + fin_blocks, st));
                 double mus = 0.0;
                 for (int b = 0; b < fin_blocks; ++b) mus += s->hscal[16 + b];
                 sumsq = s->hscal[0] + mus;
@@ -1234,10 +1246,15 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         s->n = n;
         s->record = record;
         if (hipMalloc(&s->k1_0, s->state_bytes()) != hipSuccess || hipMalloc(&s->dscal, kScalars * sizeof(double)) != hipSuccess ||
-            hipHostMalloc((void**)&s->hscal, kScalars * sizeof(double)) != hipSuccess) {
+            hipHostMalloc((void**)&s->hscal, kScalars * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess) {
             (void)hipGetLastError();
             delete s;
             return kanode_internal_fail(h, KANODE_ERR_ALLOC, "solve: out of device memory");
+        }
+        if (hipHostGetDevicePointer((void**)&s->mscal, s->hscal, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            s->mscal = nullptr;   // copy path (read_ctl)
         }
     }
     s->batch = batch;
