@@ -114,7 +114,9 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
                              const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
                              int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build,
-                             int grid_ovr = 0);
+                             int grid_ovr = 0, int* parts_out = nullptr);
+// (parts_out != nullptr with err_out: the per-block error partials are left in err_slab[0, *parts_out)
+// for the caller to sum -- the host, from mapped memory -- instead of a final reduction launch)
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,

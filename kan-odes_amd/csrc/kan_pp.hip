@@ -1087,7 +1087,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_NORED
 #define KAN_VROWS_NORED 0
 #endif
-template <int NORM, int PATH, int GT, int NP>
+template <int NORM, int PATH, int GT, int NP, int CMB>
 __global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
 fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                         const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
@@ -1132,10 +1132,18 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     const RecScalars<double> rc(lc);
     const int P = GT + (lc.use_base ? 1 : 0);
     double eacc = 0.0;
-    const bool combine = a.combine != 0;
+    const bool combine = a.combine != 0;   // (a runtime flag: a compile-time one made the fixed-step
+                                           // instantiation spill 1.2 KB/lane)
     double comb[GT + 1];
 #pragma unroll
     for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
+    // CMB == 2: the μ error combination E is accumulated in this thread's LDS column (in registers it
+    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch)
+    __shared__ double combe[CMB == 2 ? (GT + 1) * kVjpBlock : 1];
+    if constexpr (CMB == 2) {
+#pragma unroll
+        for (int j = 0; j <= GT; ++j) combe[j * kVjpBlock + threadIdx.x] = 0.0;
+    }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         double S0[GT];
@@ -1247,6 +1255,11 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             if (threadIdx.x == 0) a.slab[s][(int64_t)blockIdx.x * P] = t;
         }
 #else
+        if constexpr (CMB == 2) {   // the μ error combination over all six stages
+#pragma unroll
+            for (int j = 0; j <= GT; ++j)
+                combe[j * kVjpBlock + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * kVjpBlock + threadIdx.x]);
+        }
         if (combine && s < 5) {
 #pragma unroll
             for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
@@ -1258,6 +1271,13 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     if (combine) {
         __syncthreads();   // red is reused
         block_sum_to<double, GT + 1>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
+    }
+    if constexpr (CMB == 2) {
+        double ce[GT + 1];
+#pragma unroll
+        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
+        __syncthreads();
+        block_sum_to<double, GT + 1>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
     }
     if (a.err_slab) {
         const double v[1] = {eacc};
@@ -1694,7 +1714,8 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
                              const double* p, double* table, double cd, double co, int Nx, const double* u,
                              const double* k1, double* const* kout, double* u_new, const double* a6x6,
                              const double* e7, const double* q4x7, double abstol, double reltol, double* err_slab,
-                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build, int grid_ovr) {
+                             int slab_blocks, double* err_out, int64_t B, hipStream_t st, bool build, int grid_ovr,
+                             int* parts_out) {
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const int fn_phi = PP_PHI;
     hipError_t e = hipSuccess;
@@ -1737,6 +1758,10 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
 #undef KAN_STEP_WAVE
     e = hipGetLastError();
     if (e != hipSuccess || !err_out) return e;
+    if (parts_out) {
+        *parts_out = grid;
+        return hipSuccess;
+    }
     return launch_stage_error_final(err_slab, grid, err_out, st);
 }
 
@@ -1868,7 +1893,9 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     int grid = 0;
     // one row per wave, the row's stages in registers, where the grid of one row per wave fits the slab
     const bool use_rows = rows && grid_ovr == 0 && Nx <= 256 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks;
-    if (!use_rows || a.err_slab) a.combine = 0;   // only the rows kernel combines, and only without the error
+    // only the rows kernel combines: fixed steps (1) through A alone, adaptive steps (2) through A and the
+    // μ error combination E (the caller asks for 2 with the error slab)
+    if (!use_rows || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2)) a.combine = 0;
     if (combined_out) *combined_out = a.combine;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
@@ -1882,8 +1909,14 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
             grid = grid_for(B, kVjpBlock / kWave, slab_blocks);                                                  \
             for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
             if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
-            hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2)>), dim3(grid), dim3(kVjpBlock), lds, st, \
-                               lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, B, a);          \
+            if (a.combine == 2)                                                                                  \
+                hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 2>), dim3(grid),    \
+                                   dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
+                                   hpc.x0, cd, co, B, a);                                                        \
+            else                                                                                                 \
+                hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 0>), dim3(grid),    \
+                                   dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
+                                   hpc.x0, cd, co, B, a);                                                        \
             break;                                                                                               \
         }                                                                                                        \
         static int cap = 0;                                                                                      \

@@ -174,16 +174,19 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             wv[m] = t < tn && f < nw ? Wb[f] : T(0);
         }
         if constexpr (STAGE) {
+            // y by the first wave, λs by the second (ni <= 64): the two combinations' loads in flight
+            // together (in one thread the y_out store, which may alias λ, kept them one round apart)
             if (t < ni) {
                 const int64_t idx = (int64_t)I * k + i0 + t;
                 const T v = wide_stage_comb<T>(x, si->su, idx);
                 xL[t] = v;
                 if (si->y_out) si->y_out[idx] = v;
-                if (si->lam) {
-                    const T l = wide_stage_comb<T>(si->lam, si->sl, idx);
-                    si->ls_out[idx] = l;
-                    if constexpr (DOT) lsL[t] = l;
-                }
+            } else if (t >= kWideInMaxInputs && t - kWideInMaxInputs < ni && si->lam) {
+                const int tl = t - kWideInMaxInputs;
+                const int64_t idx = (int64_t)I * k + i0 + tl;
+                const T l = wide_stage_comb<T>(si->lam, si->sl, idx);
+                si->ls_out[idx] = l;
+                if constexpr (DOT) lsL[tl] = l;
             }
             __syncthreads();
         } else if constexpr (DOT) {

@@ -1190,19 +1190,23 @@ bool kanode_internal_fk_step_ok(const kanode_handle* h) {
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
-                                      int64_t batch, void* stream, bool& launched) {
+                                      int64_t batch, void* stream, bool& launched, double* err_parts,
+                                      int* nparts) {
     launched = false;
+    if (nparts) *nparts = 0;
     if (!kanode_internal_fk_step_ok(h)) return KANODE_OK;
     const double dx2 = h->spec.dx * h->spec.dx;
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     HIP_TRY(h, kan::launch_fk_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                       (int)h->spec.nx, (const double*)u, (const double*)k1, (double* const*)kout,
-                                      (double*)u_new, a6x6, e7, q4x7, abstol, reltol, (double*)h->slab, kSlabBlocks,
-                                      err_out, batch, (hipStream_t)stream, table_build(h, h->built_phi),
-                                      h->grid_ovr.rhs));
+                                      (double*)u_new, a6x6, e7, q4x7, abstol, reltol,
+                                      err_parts && nparts ? err_parts : (double*)h->slab, kSlabBlocks, err_out, batch,
+                                      (hipStream_t)stream, table_build(h, h->built_phi), h->grid_ovr.rhs,
+                                      err_parts && nparts ? nparts : nullptr));
     launched = true;
     return KANODE_OK;
 }
+int kanode_internal_max_parts() { return kSlabBlocks; }
 kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                          void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                          double abstol, double reltol, double* err_out, int64_t batch, void* stream,
@@ -1249,14 +1253,14 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     a->err_slab = err_out ? (double*)h->step_slab : nullptr;   // relocated by the launcher
     int grid = 0, comb = 0;
-    a->combine = combined != nullptr && err_out == nullptr ? 1 : 0;
+    a->combine = err_out && af ? 2 : (combined != nullptr && err_out == nullptr ? 1 : 0);
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                           (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
                                           table_build(h, h->built_vjp), h->grid_ovr.vstep,
                                           h->grid_ovr.vstep_rows, &comb));
     kan::FinishJobs jobs{};
     double* base = (double*)h->step_slab;
-    if (comb) {
+    if (comb == 1) {
         // km[0] <- Σ_{s<5} h·a6_{s+1}·kμ_{s+2} (the kernel's combined rows), km[5] <- kμ_7
         for (int q = 0; q < 2; ++q) {
             const int s = q == 0 ? 0 : 5;
@@ -1281,13 +1285,26 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
         // adaptive step: the six stage sums, μ_new = μ + Σ h a6_j kμ_j, kμ_7 and the μ error terms in one
         // launch (slab s holds kμ_{s+2})
         kan::AdjFinish f{};
-        for (int s = 0; s < 6; ++s) {
-            f.slab[s] = base + (int64_t)s * grid * P;
-            f.ca[s] = s < 5 ? af->a6[s + 1] : 0.0;
-            f.ce[s] = af->bt[s + 1];
+        if (comb == 2) {
+            // the rows kernel reduced A = Σ_{s<5} h a6_{s+1} kμ_{s+2} (slab 0), E = Σ_s h b̃_{s+1} kμ_{s+2}
+            // (slab 1) and kμ_7 (slab 5) instead of the six stage sums
+            const int which[3] = {0, 1, 5};
+            for (int q = 0; q < 3; ++q) {
+                f.slab[q] = base + (int64_t)which[q] * grid * P;
+                f.ca[q] = q == 0 ? 1.0 : 0.0;
+                f.ce[q] = q == 1 ? 1.0 : 0.0;
+            }
+            f.nslab = 3;
+            f.k7 = 2;
+        } else {
+            for (int s = 0; s < 6; ++s) {
+                f.slab[s] = base + (int64_t)s * grid * P;
+                f.ca[s] = s < 5 ? af->a6[s + 1] : 0.0;
+                f.ce[s] = af->bt[s + 1];
+            }
+            f.nslab = 6;
+            f.k7 = 5;
         }
-        f.nslab = 6;
-        f.k7 = 5;
         f.nblk = grid;
         f.a0 = af->a6[0];
         f.e0 = af->bt[0];

@@ -53,7 +53,12 @@ bool kanode_internal_fk_step_ok(const kanode_handle* h);
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
-                                      int64_t batch, void* stream, bool& launched);
+                                      int64_t batch, void* stream, bool& launched, double* err_parts = nullptr,
+                                      int* nparts = nullptr);
+// (err_parts, nparts: the step's per-block error partials written to err_parts -- at most
+// kanode_internal_max_parts() of them, device-visible memory -- and their count returned for the caller
+// to sum, instead of the total into err_out)
+int kanode_internal_max_parts();
 // a whole Tsit5 step of a small chain per column (kd_chain_step_kernel); K-form dense output
 kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                          void* const* kout, void* u_new, const double* a6x6, const double* e7,

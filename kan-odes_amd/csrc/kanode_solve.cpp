@@ -124,6 +124,10 @@ struct kanode_solution {
     // (a D2H hipMemcpyAsync of 8 bytes ran as a ~4.4 us blit kernel, twice per FK training step).
     // nullptr if the runtime gave no device address: those loops then copy from dscal as before.
     double* mscal = nullptr;
+    // mapped, coherent pinned host memory for a step's per-block error partials (the FK step path: the
+    // host sums them, so no final-reduction launch per adaptive step); hparts / its device address
+    double* hparts = nullptr;
+    double* mparts = nullptr;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -161,6 +165,7 @@ struct kanode_solution {
         if (k1_0) (void)hipFree(k1_0);
         if (dscal) (void)hipFree(dscal);
         if (hscal) (void)hipHostFree(hscal);
+        if (hparts) (void)hipHostFree(hparts);
         if (adj) (void)hipFree(adj);
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
         if (g.cap_stream) (void)hipStreamDestroy(g.cap_stream);
@@ -353,6 +358,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         void* ks[7];
         for (int j = 0; j < 7; ++j) ks[j] = s->k(step, j + 1);
         bool fused_step = false;   // Fisher-KPP table path: the six stages in one launch
+        int nparts = 0;            // > 0: the error is that many partials in hparts (not hscal[0])
         if (s->qform) {
             double a66[36] = {}, e7[7], q47[28];
             for (int i = 0; i < 6; ++i)
@@ -363,7 +369,8 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             void* kout[6] = {s->q(step, 1), s->q(step, 2), s->q(step, 3), s->q(step, 4), nullptr, s->k(step, 7)};
             SOLVE_TRY(kanode_internal_fk_step(h, p, s->u(step), ks[0], kout, s->u(step + 1), a66,
                                               o.adaptive ? e7 : nullptr, q47, o.abstol, o.reltol,
-                                              o.adaptive ? ctl(s) : nullptr, s->batch, st, fused_step));
+                                              o.adaptive ? ctl(s) : nullptr, s->batch, st, fused_step,
+                                              o.adaptive ? s->mparts : nullptr, &nparts));
             if (!fused_step) return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5: fused step not launched");
         } else {   // a small chain: the six stages per column in one launch
             double a66[36] = {}, e7[7];
@@ -394,7 +401,12 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         double dtnew = dt;
         if (o.adaptive) {
             SOLVE_TRY(read_ctl(h, s, 0, 1, st));
-            const double EEst = std::sqrt(s->hscal[0] / (double)s->n);
+            double sumsq = s->hscal[0];
+            if (nparts > 0) {   // the step kernel's per-block partials, summed here in block order
+                sumsq = 0.0;
+                for (int b = 0; b < nparts; ++b) sumsq += s->hparts[b];
+            }
+            const double EEst = std::sqrt(sumsq / (double)s->n);
             const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
             if (EEst > 1.0 && dt > o.dtmin) {
                 ++nreject;
@@ -1256,6 +1268,14 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
             (void)hipGetLastError();
             s->mscal = nullptr;   // copy path (read_ctl)
         }
+        const size_t pb = (size_t)kanode_internal_max_parts() * sizeof(double);
+        if (s->mscal && hipHostMalloc((void**)&s->hparts, pb, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer((void**)&s->mparts, s->hparts, 0) != hipSuccess) {
+            (void)hipHostFree(s->hparts);
+            s->hparts = nullptr;
+        }
+        (void)hipGetLastError();
+        if (!s->hparts) s->mparts = nullptr;   // the final-reduction launch then sums them
     }
     s->batch = batch;
     s->t0 = t0;
