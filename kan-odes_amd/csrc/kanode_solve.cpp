@@ -17,6 +17,7 @@
 #include <string>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <vector>
 
 #include "kan_kernels.hpp"
@@ -276,6 +277,48 @@ kanode_status read_ctl(kanode_handle* h, kanode_solution* s, int off, int cnt, h
     return KANODE_OK;
 }
 
+// Mapped step control without a stream synchronisation: the host marks the slots a step's kernels will
+// write with a NaN bit pattern no kernel produces (arm_ctl), launches, and spins until every slot has been
+// written (wait_ctl).  A GPU store to coherent host memory is visible to the host within about a
+// microsecond, while hipStreamSynchronize's wake-up put ~20 us between the kernel's end and the host's
+// next launch (the FK adaptive epoch's kernel trace: a 24 us gap before every step kernel).  The stream
+// is queried every few hundred polls: when it has drained, every slot must have been written (kernel
+// completion releases the stores), otherwise the call fails instead of spinning forever.
+constexpr uint64_t kCtlUnset = 0x7FF4DEADBEEF0001ull;   // a signalling-NaN payload
+inline void arm_ctl(double* p, int n) {
+    for (int i = 0; i < n; ++i) __atomic_store_n(reinterpret_cast<uint64_t*>(p + i), kCtlUnset, __ATOMIC_RELAXED);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+}
+inline bool ctl_ready(const double* p, int n) {
+    for (int i = 0; i < n; ++i)
+        if (__atomic_load_n(reinterpret_cast<const uint64_t*>(p + i), __ATOMIC_ACQUIRE) == kCtlUnset) return false;
+    return true;
+}
+struct CtlRange {
+    const double* p;
+    int n;
+};
+kanode_status wait_ctl(kanode_handle* h, hipStream_t st, std::initializer_list<CtlRange> rs) {
+    if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
+    auto ready = [&] {
+        for (const CtlRange& r : rs)
+            if (!ctl_ready(r.p, r.n)) return false;
+        return true;
+    };
+    for (uint64_t it = 1;; ++it) {
+        if (ready()) return KANODE_OK;
+        if ((it & 255) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) {
+                if (ready()) return KANODE_OK;
+                return kanode_internal_fail(h, KANODE_ERR_HIP, "step control: the stream drained without the error terms");
+            }
+            if (q != hipErrorNotReady) SOLVE_HIP(h, q);
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 kanode_stage make_stage(int nk, void* const* k, const double* c) {
     kanode_stage sg{};
     sg.n_prev = nk;
@@ -359,6 +402,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         for (int j = 0; j < 7; ++j) ks[j] = s->k(step, j + 1);
         bool fused_step = false;   // Fisher-KPP table path: the six stages in one launch
         int nparts = 0;            // > 0: the error is that many partials in hparts (not hscal[0])
+        if (o.adaptive && s->mscal) arm_ctl(s->hscal, 1);
         if (s->qform) {
             double a66[36] = {}, e7[7], q47[28];
             for (int i = 0; i < 6; ++i)
@@ -400,11 +444,16 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
         nf += 6;
         double dtnew = dt;
         if (o.adaptive) {
-            SOLVE_TRY(read_ctl(h, s, 0, 1, st));
-            double sumsq = s->hscal[0];
+            double sumsq;
             if (nparts > 0) {   // the step kernel's per-block partials, summed here in block order
+                SOLVE_TRY(wait_ctl(h, st, {{s->hparts, nparts}}));
                 sumsq = 0.0;
                 for (int b = 0; b < nparts; ++b) sumsq += s->hparts[b];
+                arm_ctl(s->hparts, nparts);   // (every slot stays armed between steps)
+            } else {
+                if (s->mscal) SOLVE_TRY(wait_ctl(h, st, {{s->hscal, 1}}));
+                else SOLVE_TRY(read_ctl(h, s, 0, 1, st));
+                sumsq = s->hscal[0];
             }
             const double EEst = std::sqrt(sumsq / (double)s->n);
             const double q11 = EEst > 0 ? std::pow(EEst, o.beta1) : 0.0;
@@ -945,6 +994,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         // so nothing may read them when `combined` is set
         bool combined = false;
         bool finished = false;     // adaptive step: μ_new, kμ_7 and the μ error terms formed by the finish launch
+        if (o.adaptive && s->mscal) arm_ctl(s->hscal, kScalars);
         if (s->qform) {
             kan::AdjStepArgs a{};
             for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];
@@ -1023,12 +1073,14 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         if (o.adaptive) {
             double sumsq = 0.0;
             if (finished) {   // the λ sum and the P μ terms in one read, summed here in order
-                SOLVE_TRY(read_ctl(h, s, 8, (int)(1 + P), st));
+                if (s->mscal) SOLVE_TRY(wait_ctl(h, st, {{s->hscal + 8, (int)(1 + P)}}));
+                else SOLVE_TRY(read_ctl(h, s, 8, (int)(1 + P), st));
                 double mus = 0.0;
                 for (int64_t q = 0; q < P; ++q) mus += s->hscal[9 + q];
                 sumsq = s->hscal[8] + mus;
             } else {   // the λ total (slot 0) and the μ partials (slots 16..) in one read
-                SOLVE_TRY(read_ctl(h, s, 0, 16 + fin_blocks, st));
+                if (s->mscal) SOLVE_TRY(wait_ctl(h, st, {{s->hscal, 1}, {s->hscal + 16, fin_blocks}}));
+                else SOLVE_TRY(read_ctl(h, s, 0, 16 + fin_blocks, st));
                 double mus = 0.0;
                 for (int b = 0; b < fin_blocks; ++b) mus += s->hscal[16 + b];
                 sumsq = s->hscal[0] + mus;
@@ -1276,6 +1328,7 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         }
         (void)hipGetLastError();
         if (!s->hparts) s->mparts = nullptr;   // the final-reduction launch then sums them
+        else arm_ctl(s->hparts, kanode_internal_max_parts());
     }
     s->batch = batch;
     s->t0 = t0;
