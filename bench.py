@@ -680,7 +680,12 @@ def main() -> None:
                                                          0 if (args.no_cpu_baseline or world > 1) else 2)
 
     if dist and not args.no_dist_surrogates:
-        sd = surrogate_dist_bench(dev, rank, world, args.dist_backend)
+        # a secondary leg: an exception here (raised on every rank alike: the ranks run the same code)
+        # is recorded in the line instead of taking the metric above down with it
+        try:
+            sd = surrogate_dist_bench(dev, rank, world, args.dist_backend)
+        except Exception as e:  # noqa: BLE001
+            sd = {"dist_surrogates_error": f"{type(e).__name__}: {e}"[:300]}
         if rank == 0:
             out.update(sd)
 

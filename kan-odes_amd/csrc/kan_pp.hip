@@ -482,8 +482,12 @@ __device__ __forceinline__ void st_fstep(double* p, kd2 v) {
 // (ceil(B / (4 chunk)) blocks, dispatched as the hardware frees slots); chunk = 0 is the persistent
 // grid-stride form.  At 1M trajectories the contiguous chunks stream faster than a persistent grid
 // (the table staging is amortised over 4·chunk rows; profiles/r02/ab/).
+#ifndef KAN_PP_RHS_BS
+#define KAN_PP_RHS_BS 256
+#endif
+constexpr int kRhsBlock = KAN_PP_RHS_BS;   // threads per block of the table RHS kernel
 template <int NORM, int BASIS, int NP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
+__global__ void __launch_bounds__(kRhsBlock) __attribute__((amdgpu_waves_per_eu(KAN_PP_WPE)))
 fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                       const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
                       const double* __restrict__ u, double* __restrict__ du, int64_t B, int chunk) {
@@ -491,10 +495,10 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     extern __shared__ double2 tl[];
     constexpr int R = KAN_PP_ROWS;   // rows per wave per pipeline step
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rstride = chunk > 0 ? (int64_t)(kBlock / kWave) : (int64_t)gridDim.x * (kBlock / kWave);
-    int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) * (chunk > 0 ? chunk : 1) + (threadIdx.x >> 6);
+    const int64_t rstride = chunk > 0 ? (int64_t)(kRhsBlock / kWave) : (int64_t)gridDim.x * (kRhsBlock / kWave);
+    int64_t b = (int64_t)blockIdx.x * (kRhsBlock / kWave) * (chunk > 0 ? chunk : 1) + (threadIdx.x >> 6);
     if (chunk > 0) {
-        const int64_t end = ((int64_t)blockIdx.x + 1) * (kBlock / kWave) * chunk;
+        const int64_t end = ((int64_t)blockIdx.x + 1) * (kRhsBlock / kWave) * chunk;
         B = end < B ? end : B;
     }
     // the first rows' loads are in flight while the block stages its table
@@ -507,7 +511,7 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             for (int k = 0; k < NP; ++k) v[r][k] = ld_stream(u + br * Nx + 128 * k + 2 * lane);
         }
     }
-    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kRhsBlock) tl[i] = table[i];
 #if KAN_PP_COLD_GLOBAL_EXP
     // only the cold direct-formula branch takes exponentials: it reads the 2 KB 2^(j/256) table from
     // global memory instead of every block staging it in LDS
@@ -1640,11 +1644,11 @@ hipError_t launch_fk_rhs_pp(const PPConst& hpc, const LayerConst& hlc, const Lay
 #define KAN_PP_WAVE(NORM, BASIS, NP)                                                                             \
     do {                                                                                                         \
         static int cap = 0;                                                                                      \
-        if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds);                              \
+        if (!cap) cap = pp_grid_cap(fk_rhs_pp_wave_kernel<NORM, BASIS, NP>, lds, kRhsBlock);                   \
         const int chunk = grid_ovr > 0 ? 0 : kPPChunk;                                                          \
-        const int grid = chunk > 0 ? grid_for(B, (kBlock / kWave) * chunk, 1 << 30)                               \
-                                   : grid_for(B, kBlock / kWave, grid_ovr > 0 ? grid_ovr : cap);                \
-        hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,   \
+        const int grid = chunk > 0 ? grid_for(B, (kRhsBlock / kWave) * chunk, 1 << 30)                            \
+                                   : grid_for(B, kRhsBlock / kWave, grid_ovr > 0 ? grid_ovr : cap);             \
+        hipLaunchKernelGGL((fk_rhs_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kRhsBlock), lds, st, lc, p, \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, du, B, chunk);           \
     } while (0)
 #define KAN_PP_PAIR(NORM, BASIS, SHORT)                                                                          \

@@ -35,6 +35,15 @@ echo "== epoch kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/epoch -o run --output-format csv -- \
   python3 tools/prof_epoch.py --batch 4096 --reps 3 > $OUT/epoch.log 2>&1 || { tail -5 $OUT/epoch.log; exit 3; }
 cp $OUT/epoch/run_kernel_stats.csv $OUT/epoch_kernel_stats.csv
+echo "== adaptive epoch and surrogate training kernel traces"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/epoch_adaptive -o run --output-format csv -- \
+  python3 tools/prof_epoch_adaptive.py > $OUT/epoch_adaptive.log 2>&1 || { tail -5 $OUT/epoch_adaptive.log; exit 3; }
+cp $OUT/epoch_adaptive/run_kernel_stats.csv $OUT/epoch_adaptive_kernel_stats.csv
+for c in burgers512 schrodinger1024; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/train_$c -o run --output-format csv -- \
+    python3 tools/prof_surrogate_train.py --case $c --reps 2 > $OUT/train_$c.log 2>&1 || { tail -5 $OUT/train_$c.log; exit 3; }
+  cp $OUT/train_$c/run_kernel_stats.csv $OUT/train_${c}_kernel_stats.csv
+done
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 BATCH=${BATCH:-1048576} python3 tools/traffic.py $OUT > $OUT/traffic.json
 cat $OUT/pmc_summary.txt $OUT/traffic.json
