@@ -158,6 +158,10 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *   KANODE_OPT_PAIR_VJP (default 1): the VJP / adjoint stage of a surrogate chain KAN [N, H, N]
  *     (wide-in then wide-out layer) runs as two launches (batches up to 64); 0 = the four-launch
  *     path.  Equal to the summation order of the wide-out dot products (both fixed-order).
+ *   KANODE_OPT_PAIR_FUSE (default 1): the integrator's adjoint stages of such a chain hold each
+ *     stage's second launch until the next stage is issued and run the two in one launch (the
+ *     x̄ block of stage s forms stage s+1's input λs over its own chunk); 0 = two launches per
+ *     stage.  Bitwise equal.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -169,7 +173,8 @@ typedef enum {
     KANODE_OPT_GRID_VJP = 6,
     KANODE_OPT_GRID_ADJ_STEP = 7,
     KANODE_OPT_ADJ_STEP_ROWS = 8,
-    KANODE_OPT_PAIR_VJP = 9
+    KANODE_OPT_PAIR_VJP = 9,
+    KANODE_OPT_PAIR_FUSE = 10
 } kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);

@@ -414,4 +414,64 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
 // elements of the pair's wide-in basis store (bas above: φ [K][I][G], swish and swish' [K][I])
 inline int64_t pair_basis_elems(const LayerConst& h0, int64_t K) { return K * h0.I * (h0.G + 2); }
 
+// The pair pullback as a plan of its two launches (kan_wide.hip), so that a caller running adjoint stages
+// back to back (the solver's deferred stages, kanode_abi.cpp) can hold a stage's second launch until the
+// next stage is known and run the two together (launch_pair_second with `next`: kd_vjp_pair_ba_kernel).
+// The wide-in basis store (WideBasisG): phi [K][I][G] = φ_g(x_ik), sw / dsw [K][I] = swish(x_ik), swish'.
+template <typename T>
+struct WideBasisG {
+    T* phi;
+    T* sw;
+    T* dsw;
+};
+template <typename T>
+struct PairBArgs {   // the second launch's kernel arguments
+    const T* x;          // the layer-1 input the pullback reads (u, or the stage's y)
+    const T* pslab;      // the first launch's hidden-layer chunk partials
+    int nblk;
+    const T* ybar;       // λ, or the stage's λs
+    const T* S;          // the dot products' chunk partials
+    T* xbar;
+    T* pbar;
+    int64_t K;
+    int nP, nrc, np, nxg, cw, nbx, hb_off, assign;
+    WideStageIn<T> si;
+    double* err_slab;
+    WideBasisG<T> bg;
+};
+template <typename T>
+struct PairAArgs {   // the first launch's (a stage's) kernel arguments beyond the layer constants
+    const T* x;          // the stage base u
+    T* pslab;
+    T* spart;
+    WideStageIn<T> si;
+    WideBasisG<T> bg;
+};
+template <typename T>
+struct PairPlan {
+    const LayerConst* lc;
+    const T* p;
+    int path;            // the wide-out layer's basis path
+    bool stage;          // an adjoint stage (si given): the first launch forms y and λs
+    PairAArgs<T> a;
+    const T* ybar_a;     // (no stage) λ
+    int nF, nblk, mv;    // first launch: blocks, wide-in chunks, load-slot instantiation (0 = <8,2>)
+    PairBArgs<T> b;
+    int gridB;
+    size_t ldsB;
+    double* err_out;     // the λ error total (b.err_slab != nullptr), summed over err_rows partials
+    int err_rows;
+    bool fuse_ok;        // this plan's second launch can carry the next stage's first (same chunking)
+};
+template <typename T>
+hipError_t plan_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p, const T* x,
+                            const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S, T* xb, T* pbar,
+                            int64_t K, bool assign, double* err_slab, int err_rows, double* err_out, T* bas,
+                            PairPlan<T>* out);
+template <typename T>
+hipError_t launch_pair_first(const PairPlan<T>& pl, hipStream_t st);
+// next != nullptr: also runs next's first launch, inside this launch when the two fuse (*fused = true)
+template <typename T>
+hipError_t launch_pair_second(const PairPlan<T>& pl, const PairPlan<T>* next, hipStream_t st, bool* fused = nullptr);
+
 }  // namespace kan

@@ -116,6 +116,20 @@ __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const S
         if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), kv[j], v);
     return v;
 }
+// the same combination with its last array's entry given (the value the fused pair step's block has
+// just formed itself, kd_vjp_pair_ba_kernel): the same fma order, so the same bits
+template <typename T>
+__device__ __forceinline__ T wide_stage_comb_last(const T* __restrict__ base, const StageArgs<T>& sa, int64_t idx,
+                                                  T last) {
+    const double sc = stage_scale(sa.cscale);
+    T kv[kMaxStages];
+    stage_ld<T>(sa, base, idx, kv);
+    T v = base[idx];
+#pragma unroll
+    for (int j = 0; j < kMaxStages; ++j)
+        if (j < sa.nk) v = kfma<T>((T)(sa.c[j] * sc), j == sa.nk - 1 ? last : kv[j], v);
+    return v;
+}
 // MV / MW: C / W load slots per thread (>= the chunk's entries / tn; the launch picks the smallest
 // instantiation that covers the chunk -- unused predicated slots still cost instructions).
 // The pair pullback's dot products, formed by the wide-in forward blocks (DOT): the chunk's input
@@ -123,16 +137,9 @@ __device__ __forceinline__ T wide_stage_comb(const T* __restrict__ base, const S
 // that holds ȳ[i0 .. i0 + ni, k] (λs it formed, or λ) forms the partial sums
 //     spart[(bx·IR + q)·K + k] = Σ_{o in chunk} row_q[o] ȳ[o, k],   row_q = C2[:, r + G2 i2] (r < G2) or
 // W2[:, i2] (r = G2), q = i2·R2 + r, IR = I2·R2; the consumer sums the nblk chunk partials in order.
-// The pair's forward blocks also store the wide-in layer's basis values, which the pullback's
-// parameter and x̄ blocks would otherwise recompute (one exponential each, ten times over for the
-// ten parameter blocks of a chunk): phi[(k·I + i)·G + g] = φ_g(x_ik), sw / dsw[k·I + i] = swish(x_ik)
-// and its rrule derivative.  Bitwise the values the recomputation gives (same statements).
-template <typename T>
-struct WideBasisG {
-    T* phi;
-    T* sw;
-    T* dsw;
-};
+// The pair's forward blocks also store the wide-in layer's basis values (WideBasisG, kan_kernels.hpp),
+// which the pullback's parameter and x̄ blocks would otherwise recompute (one exponential each, ten times
+// over for the ten parameter blocks of a chunk).  Bitwise the values the recomputation gives.
 template <typename T>
 struct PairDot {
     const LayerConst* lc1;
@@ -144,7 +151,7 @@ template <typename T, bool STAGE, int MV, int MW, bool DOT = false>
 __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ lcp, const T* __restrict__ p,
                                                 const T* __restrict__ x, T* __restrict__ slab, int64_t K,
                                                 const WideStageIn<T>* si, int bx, int by, int gy,
-                                                const PairDot<T>* pd = nullptr) {
+                                                const PairDot<T>* pd = nullptr, const T* lastk = nullptr) {
     __shared__ T phiL[kWideInMaxInputs * kMaxGrid];
     __shared__ T swL[kWideInMaxInputs];
     __shared__ T xL[kWideInMaxInputs];
@@ -184,7 +191,8 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             } else if (t >= kWideInMaxInputs && t - kWideInMaxInputs < ni && si->lam) {
                 const int tl = t - kWideInMaxInputs;
                 const int64_t idx = (int64_t)I * k + i0 + tl;
-                const T l = wide_stage_comb<T>(si->lam, si->sl, idx);
+                const T l = lastk ? wide_stage_comb_last<T>(si->lam, si->sl, idx, lastk[tl])
+                                  : wide_stage_comb<T>(si->lam, si->sl, idx);
                 si->ls_out[idx] = l;
                 if constexpr (DOT) lsL[tl] = l;
             }
@@ -933,13 +941,12 @@ __device__ __forceinline__ void block_gather_sums(F src, int nt, int nS, T* red,
     }
 }
 
+// The second launch's body (every block type); true for an x̄ block, whose chunk and column are returned.
+// xbst (nullable, LDS): an x̄ block also leaves its x̄ entries there (the fused step's next stage reads them).
 template <typename T, int PATH>
-__global__ void __launch_bounds__(256)
-kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
-                     const T* __restrict__ x, const T* __restrict__ pslab, int nblk, const T* __restrict__ ybar,
-                     const T* __restrict__ S, T* __restrict__ xbar, T* __restrict__ pbar, int64_t K, int nP, int nrc,
-                     int np, int nxg, int cw, int nbx, int hb_off, int assign, WideStageIn<T> si,
-                     double* __restrict__ err_slab, WideBasisG<T> bg) {
+__device__ __forceinline__ bool pair_b_body(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1,
+                                            const T* __restrict__ p, const PairBArgs<T>& a, T* xbst, int& chunk,
+                                            int& col) {
     // err_slab (adjoint stage with the λ error, si given): each x̄ block adds, for its entries,
     // (e / sk)², e = Σ_j ec_j lk_j + ec_n·λsᵀJ, sk = abstol + reltol·max(|λ|, |λs|) (stage_error_kernel's
     // statement), into err_slab[its index]; the stage's final reduction sums the nbx·nxg rows
@@ -948,27 +955,34 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
     T* L = reinterpret_cast<T*>(pb_raw);
     const Math<T> M{kExp2Tab256};   // exp table from global memory (L1)
     const int b = blockIdx.x;
-    if (KAN_ABL == 9 || (KAN_ABL == 4 && b < nP)) return;
-    if (KAN_ABL == 5 && b >= nP && (b - nP) / nbx >= np) return;
-    if (KAN_ABL == 6 && b >= nP && (b - nP) / nbx < np) return;
-    if (b < nP) {   // four wide-out parameter units per block, one per wave
+    const int64_t K = a.K;
+    const int nbx = a.nbx, np = a.np, nblk = a.nblk;
+    const T* __restrict__ pslab = a.pslab;
+    const T* __restrict__ S = a.S;
+    if (KAN_ABL == 9 || (KAN_ABL == 4 && b < a.nP)) return false;
+    if (KAN_ABL == 5 && b >= a.nP && (b - a.nP) / nbx >= np) return false;
+    if (KAN_ABL == 6 && b >= a.nP && (b - a.nP) / nbx < np) return false;
+    if (b < a.nP) {   // four wide-out parameter units per block, one per wave
         const int w = threadIdx.x / kWave;
         const int64_t ph = (int64_t)(lc1->G + 1) * K;
-        wideout_param_wave<T, PATH>(M, *lc1, pslab, nblk, ybar, pbar, K, 4 * b + w, nrc * lc1->I, nrc, assign,
-                                    L + w * ph);
-        return;
+        wideout_param_wave<T, PATH>(M, *lc1, pslab, nblk, a.ybar, a.pbar, K, 4 * b + w, a.nrc * lc1->I, a.nrc,
+                                    a.assign, L + w * ph);
+        return false;
     }
-    const int q = b - nP;
+    const int q = b - a.nP;
     const LayerConst& l1 = *lc1;
     const int H = l1.I, R = l1.G + (l1.use_base ? 1 : 0);
     const int64_t bs = (int64_t)H * R * K;     // stride of one chunk's partials
-    T* hbL = L + hb_off;                       // [K]: a parameter block's cotangent row
+    T* hbL = L + a.hb_off;                     // [K]: a parameter block's cotangent row
     T* red = hbL + K;                          // [256]
     T* Sv = red + 256;                         // [max(R·K, H·R)] the block's dot products
     T* hv = Sv + (R * K > H * R ? R * K : H * R);   // [max(K, H)] the hidden values it needs
     double eacc = 0.0;
+    const WideStageIn<T>& si = a.si;
+    double* __restrict__ err_slab = a.err_slab;
+    const int i0 = (q % nbx) * a.cw;
     widein_vjp_body<T>(
-        lc0, p, x, [&](int, int64_t k) { return hbL[k]; },
+        lc0, p, a.x, [&](int, int64_t k) { return hbL[k]; },
         [&](int o) {   // hidden unit o over all columns: S[o, r, k] for r < R, k < K, and h[o, k]
             block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K,
                                  KAN_ABL == 3 ? 0 : nblk, red, Sv);
@@ -987,6 +1001,7 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
             if (t < H) ybL[t] = wideout_xfin_lds<T, PATH>(M, l1, hv[t], Sv + t * R, 1);
         },
         [&](int64_t idx, T xb) {
+            if (xbst) xbst[idx % l1.O - i0] = xb;   // (l1.O = the state size: idx = N·k + i0 + t)
             if (!err_slab) return;
             const StageArgs<T>& sl = si.sl;
             const double sc = stage_scale(sl.cscale);
@@ -1001,12 +1016,45 @@ kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __res
             const double r = e / sk;
             eacc = ::fma(r, r, eacc);
         },
-        xbar, pbar, K, np, 1, nxg, cw, assign, q % nbx, q / nbx, L, bg.phi ? &bg : nullptr);
-    if (err_slab && q / nbx >= np) {   // an x̄ block: its error partial
+        a.xbar, a.pbar, K, np, 1, a.nxg, a.cw, a.assign, q % nbx, q / nbx, L, a.bg.phi ? &a.bg : nullptr);
+    if (q / nbx < np) return false;
+    if (err_slab) {   // an x̄ block: its error partial
         __shared__ double ered[256 / kWave];
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, ered, err_slab + (q / nbx - np) * nbx + q % nbx);
     }
+    chunk = q % nbx;
+    col = q / nbx - np;
+    return true;
+}
+
+template <typename T, int PATH>
+__global__ void __launch_bounds__(256)
+kd_vjp_pair_b_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
+                     PairBArgs<T> a) {
+    int chunk, col;
+    (void)pair_b_body<T, PATH>(lc0, lc1, p, a, nullptr, chunk, col);
+}
+
+// The fused pair step (the solver's deferred adjoint stages, kanode_abi.cpp): stage s's second launch
+// and stage s+1's first in one.  Stage s+1's first-launch block for (chunk, column) needs, beyond data
+// earlier launches wrote, only the λᵀJ of stage s over that chunk and column (the last term of its λs
+// combination) -- exactly what stage s's x̄ block for (chunk, column) forms.  So every x̄ block, after its
+// pullback, runs the next stage's wide-in forward body for its own chunk and column, taking that term
+// from LDS; the parameter blocks run beside them as in kd_vjp_pair_b_kernel.  The next stage's outputs
+// (hidden and dot-product partials, basis store, y, λs) go to the other buffer of a ping-pong pair, since
+// this launch's parameter blocks still read stage s's.  Same statements in the same order as the two
+// launches: bitwise equal results.
+template <typename T, int PATH, int MV, int MW>
+__global__ void __launch_bounds__(256)
+kd_vjp_pair_ba_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
+                      PairBArgs<T> a, PairAArgs<T> n) {
+    __shared__ T xbst[kWideInMaxInputs];
+    int chunk, col;
+    if (!pair_b_body<T, PATH>(lc0, lc1, p, a, xbst, chunk, col)) return;
+    __syncthreads();   // this block's x̄ entries are in xbst
+    const PairDot<T> pd{lc1, n.spart, n.si.ls_out, n.bg};
+    widein_fwd_body<T, true, MV, MW, true>(lc0, p, n.x, n.pslab, a.K, &n.si, chunk, col, (int)a.K, &pd, xbst);
 }
 
 // ---------------------------------------------------------------------------
@@ -1111,11 +1159,16 @@ hipError_t launch_kd_vjp_widein(const LayerConst& h, const LayerConst* lc, const
 }
 
 template <typename T>
-hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
-                              const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
-                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab,
-                              int err_rows, double* err_out, T* bas) {
+hipError_t plan_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p, const T* x,
+                            const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S, T* xb, T* pbar,
+                            int64_t K, bool assign, double* err_slab, int err_rows, double* err_out, T* bas,
+                            PairPlan<T>* out) {
     if (K < 1 || K > kPairMaxK || !xb) return hipErrorNotSupported;
+    PairPlan<T> pl{};
+    pl.lc = lc;
+    pl.p = p;
+    pl.path = h1.path;
+    pl.stage = si != nullptr;
     // the wide-in basis store (WideBasisG): phi [K][I][G], sw [K][I], dsw [K][I]
     WideBasisG<T> bg{};
     if (bas) {
@@ -1137,47 +1190,117 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
     // A
     const int nblk = widein_chunks(h0);
     const int gyF = (int)(K < 65535 ? K : 65535);
-    const int nF = nblk * gyF;
     const int tn = (256 / h0.O) * h0.O, cwf = widein_cw(h0.O, h0.G, h0.I);
     const int nv = (h0.O * h0.G * cwf + tn - 1) / tn, nw = (h0.O * cwf + tn - 1) / tn;
-    const WideStageIn<T> none{};
-    const WideStageIn<T>& sa = si ? *si : none;
-#define KAN_PA(MV, MW)                                                                                             \
-    do {                                                                                                           \
-        if (si) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(nF), dim3(256), 0, st, lc, lc + 1,  \
-                                   p, x, pslab, ybar, S, K, nblk, gyF, sa, bg);                                    \
-        else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(nF), dim3(256), 0, st, lc, lc + 1,   \
-                                p, x, pslab, ybar, S, K, nblk, gyF, sa, bg);                                       \
-    } while (0)
-    if (nv <= 8 && nw <= 2) KAN_PA(8, 2);
-    else if (nv <= 16 && nw <= 4) KAN_PA(16, 4);
-    else KAN_PA(kWIMaxV, kWIMaxW);
-#undef KAN_PA
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    pl.a.x = x;
+    pl.a.pslab = pslab;
+    pl.a.spart = S;
+    pl.a.si = si ? *si : WideStageIn<T>{};
+    pl.a.bg = bg;
+    pl.ybar_a = ybar;
+    pl.nF = nblk * gyF;
+    pl.nblk = nblk;
+    pl.mv = nv <= 8 && nw <= 2 ? 0 : (nv <= 16 && nw <= 4 ? 1 : 2);
     // B
-    const int nP = pbar ? (nrc * h1.I + 3) / 4 : 0;   // wide-out parameter blocks, four units each
     const int nbx = (h0.I + cw - 1) / cw;
     const int np = pbar ? h0.O : 0;
     const int nxg = (int)(K < 4096 ? K : 4096);
-    const int nW = nbx * (np + nxg);
-    const T* yb_b = si ? si->ls_out : ybar;   // ȳ of the wide-out parameter blocks: λs as A wrote it
-    // the λ error of an adjoint stage: per-x̄-block partials, then the stage's ordered final sum
     const bool err = si && err_out && err_slab && nbx * nxg <= err_rows;
     if (si && err_out && !err) return hipErrorNotSupported;
+    PairBArgs<T>& b = pl.b;
+    b.x = xvjp;
+    b.pslab = pslab;
+    b.nblk = nblk;
+    b.ybar = si ? si->ls_out : ybar;   // ȳ of the wide-out parameter blocks: λs as A wrote it
+    b.S = S;
+    b.xbar = xb;
+    b.pbar = pbar;
+    b.K = K;
+    b.nP = pbar ? (nrc * h1.I + 3) / 4 : 0;   // wide-out parameter blocks, four units each
+    b.nrc = nrc;
+    b.np = np;
+    b.nxg = nxg;
+    b.cw = cw;
+    b.nbx = nbx;
+    b.hb_off = (int)lw;
+    b.assign = assign ? 1 : 0;
+    b.si = pl.a.si;
+    b.err_slab = err ? err_slab : nullptr;
+    b.bg = bg;
+    pl.gridB = b.nP + nbx * (np + nxg);
+    pl.ldsB = lds_b;
+    pl.err_out = err ? err_out : nullptr;
+    pl.err_rows = nbx * nxg;
+    // the next stage's first launch fits this plan's x̄ blocks: one block per (chunk, column) on both
+    // sides, and the small load-slot instantiation (the fused kernel's registers stay at the second
+    // launch's occupancy)
+    pl.fuse_ok = pl.stage && nbx == nblk && cw == cwf && nxg == K && gyF == K && pl.mv == 0;
+    *out = pl;
+    return hipSuccess;
+}
+
+template <typename T>
+hipError_t launch_pair_first(const PairPlan<T>& pl, hipStream_t st) {
+    const LayerConst* lc = pl.lc;
+    const int64_t K = pl.b.K;
+    const int gyF = (int)(K < 65535 ? K : 65535);
+#define KAN_PA(MV, MW)                                                                                             \
+    do {                                                                                                           \
+        if (pl.stage) hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, true>), dim3(pl.nF), dim3(256), 0, st, lc, \
+                                         lc + 1, pl.p, pl.a.x, pl.a.pslab, pl.ybar_a, pl.a.spart, K, pl.nblk, gyF,  \
+                                         pl.a.si, pl.a.bg);                                                        \
+        else hipLaunchKernelGGL((kd_vjp_pair_a_kernel<T, MV, MW, false>), dim3(pl.nF), dim3(256), 0, st, lc,        \
+                                lc + 1, pl.p, pl.a.x, pl.a.pslab, pl.ybar_a, pl.a.spart, K, pl.nblk, gyF,           \
+                                pl.a.si, pl.a.bg);                                                                 \
+    } while (0)
+    if (pl.mv == 0) KAN_PA(8, 2);
+    else if (pl.mv == 1) KAN_PA(16, 4);
+    else KAN_PA(kWIMaxV, kWIMaxW);
+#undef KAN_PA
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_pair_second(const PairPlan<T>& pl, const PairPlan<T>* next, hipStream_t st, bool* fused) {
+    const LayerConst* lc = pl.lc;
+    bool fuse = false;
+    if (next && pl.fuse_ok && next->fuse_ok && next->lc == pl.lc && next->p == pl.p && next->b.K == pl.b.K &&
+        next->mv == 0) {
+        const StageArgs<T>& sl = next->a.si.sl;
+        fuse = sl.nk >= 1 && sl.k[sl.nk - 1] == pl.b.xbar;
+    }
+    if (fused) *fused = fuse;
 #define KAN_PB(PATH)                                                                                               \
-    hipLaunchKernelGGL((kd_vjp_pair_b_kernel<T, PATH>), dim3(nP + nW), dim3(256), lds_b, st, lc, lc + 1, p, xvjp,   \
-                       pslab, nblk, yb_b, S, xb, pbar, K, nP, nrc, np, nxg, cw, nbx, (int)lw, assign ? 1 : 0, sa,      \
-                       err ? err_slab : nullptr, bg)
-    switch (h1.path) {
+    do {                                                                                                           \
+        if (fuse) hipLaunchKernelGGL((kd_vjp_pair_ba_kernel<T, PATH, 8, 2>), dim3(pl.gridB), dim3(256), pl.ldsB, st, \
+                                     lc, lc + 1, pl.p, pl.b, next->a);                                             \
+        else hipLaunchKernelGGL((kd_vjp_pair_b_kernel<T, PATH>), dim3(pl.gridB), dim3(256), pl.ldsB, st, lc, lc + 1, \
+                                pl.p, pl.b);                                                                       \
+    } while (0)
+    switch (pl.path) {
     case PATH_REC_CORR: KAN_PB(PATH_REC_CORR); break;
     case PATH_REC: KAN_PB(PATH_REC); break;
     default: KAN_PB(PATH_DIRECT);
     }
 #undef KAN_PB
-    e = hipGetLastError();
-    if (e != hipSuccess || !err) return e;
-    return launch_stage_error_final(err_slab, nbx * nxg, err_out, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (pl.err_out && (e = launch_stage_error_final(pl.b.err_slab, pl.err_rows, pl.err_out, st)) != hipSuccess) return e;
+    if (next && !fuse) return launch_pair_first(*next, st);
+    return hipSuccess;
+}
+
+template <typename T>
+hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const LayerConst* lc, const T* p,
+                              const T* x, const WideStageIn<T>* si, const T* ybar, const T* xvjp, T* pslab, T* S,
+                              T* xb, T* pbar, int64_t K, hipStream_t st, bool assign, double* err_slab,
+                              int err_rows, double* err_out, T* bas) {
+    PairPlan<T> pl;
+    hipError_t e = plan_kd_vjp_pair<T>(h0, h1, lc, p, x, si, ybar, xvjp, pslab, S, xb, pbar, K, assign, err_slab,
+                                       err_rows, err_out, bas, &pl);
+    if (e != hipSuccess) return e;
+    if ((e = launch_pair_first<T>(pl, st)) != hipSuccess) return e;
+    return launch_pair_second<T>(pl, nullptr, st);
 }
 
 #define KAN_WIDE_INST(T)                                                                                       \
@@ -1191,7 +1314,12 @@ hipError_t launch_kd_vjp_pair(const LayerConst& h0, const LayerConst& h1, const 
                                                 const T*, T*, T*, int64_t, hipStream_t, bool);                  \
     template hipError_t launch_kd_vjp_pair<T>(const LayerConst&, const LayerConst&, const LayerConst*, const T*,  \
                                               const T*, const WideStageIn<T>*, const T*, const T*, T*, T*, T*, T*, \
-                                              int64_t, hipStream_t, bool, double*, int, double*, T*);
+                                              int64_t, hipStream_t, bool, double*, int, double*, T*);              \
+    template hipError_t plan_kd_vjp_pair<T>(const LayerConst&, const LayerConst&, const LayerConst*, const T*,    \
+                                            const T*, const WideStageIn<T>*, const T*, const T*, T*, T*, T*, T*,   \
+                                            int64_t, bool, double*, int, double*, T*, PairPlan<T>*);               \
+    template hipError_t launch_pair_first<T>(const PairPlan<T>&, hipStream_t);                                     \
+    template hipError_t launch_pair_second<T>(const PairPlan<T>&, const PairPlan<T>*, hipStream_t, bool*);
 KAN_WIDE_INST(double)
 KAN_WIDE_INST(float)
 #undef KAN_WIDE_INST

@@ -63,6 +63,14 @@ struct kanode_handle {
     bool fused_step = true;           // KANODE_OPT_FUSED_STEP
     bool fused_solve = true;          // KANODE_OPT_FUSED_SOLVE
     bool pair_vjp = true;             // KANODE_OPT_PAIR_VJP
+    bool pair_fuse = true;            // KANODE_OPT_PAIR_FUSE
+    // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
+    // (then both run as kd_vjp_pair_ba_kernel) or kanode_internal_vjp_flush; pair_par picks the buffers of
+    // the ping-pong pairs (hidden / dot-product partials, basis store, y, λs) the next stage writes
+    kan::PairPlan<double> pend_d{};
+    kan::PairPlan<float> pend_f{};
+    bool pend_valid = false;
+    int pair_par = 0;
     int fused_solve_cap = 0;          // KANODE_OPT_FUSED_SOLVE_CAP (0 = the kernel's block)
     kan::GridOverride grid_ovr{};     // KANODE_OPT_GRID_{RHS,VJP,ADJ_STEP} (0 = default)
     // the integrator's storage for solves without a dense output (kanode_solve.cpp)
@@ -266,7 +274,7 @@ bool surrogate_pair(const kanode_handle* h) {
 //   [hidden activations: Σ_{l>=1} I_l·B][grad ping: max_dim·B][grad pong: max_dim·B][wide slab]
 //   [surrogate pair: the wide-in layer's chunk partials, chunks·B·H]
 struct WsLayout {
-    int64_t acts, g0, g1, wslab, pslab, sslab, bslab, total;
+    int64_t acts, g0, g1, wslab, pslab, sslab, bslab, pair2, total;   // pair2: offset of the second copy of [pslab, pair2)
 };
 WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     WsLayout w{};
@@ -287,6 +295,9 @@ WsLayout ws_layout(const kanode_handle* h, int64_t B) {
     // [surrogate pair, two-launch pullback: the wide-in layer's basis store, B·I·(G + 2)]
     w.bslab = e;
     if (surrogate_pair(h)) e += kan::pair_basis_elems(h->hlc[0], B);
+    // [surrogate pair: the second buffer of the ping-pong pairs pslab .. bslab (fused deferred stages)]
+    w.pair2 = e;
+    if (surrogate_pair(h)) e += e - w.pslab;
     w.total = e;
     return w;
 }
@@ -619,7 +630,25 @@ kanode_status ensure_adjoint_slabs(kanode_handle* h, hipStream_t st, bool at_cre
     return KANODE_OK;
 }
 
+template <typename T>
+kan::PairPlan<T>& pair_pending(kanode_handle* h);
+template <>
+kan::PairPlan<double>& pair_pending<double>(kanode_handle* h) { return h->pend_d; }
+template <>
+kan::PairPlan<float>& pair_pending<float>(kanode_handle* h) { return h->pend_f; }
+
+// the deferred surrogate-pair stage's second launch, alone (nothing to fuse it with)
+kanode_status flush_pair(kanode_handle* h, hipStream_t st) {
+    if (!h->pend_valid) return KANODE_OK;
+    h->pend_valid = false;
+    const hipError_t e = h->spec.dtype == KANODE_F64 ? kan::launch_pair_second<double>(h->pend_d, nullptr, st)
+                                                     : kan::launch_pair_second<float>(h->pend_f, nullptr, st);
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_pair_second: ") + hipGetErrorString(e));
+    return KANODE_OK;
+}
+
 kanode_status vjp_flush(kanode_handle* h, hipStream_t st) {
+    if (kanode_status s = flush_pair(h, st); s != KANODE_OK) return s;
     if (h->njobs == 0) return KANODE_OK;
     const int n = h->njobs;
     h->njobs = 0;
@@ -688,14 +717,21 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
     }
     if (h->spec.rhs_kind == KANODE_RHS_CHAIN && surrogate_pair(h) && lamJ) {
         // surrogate pair: y and λs formed by the wide-in forward (no combination launches), the
-        // parameter cotangents written with = when dp_assign (no memset): four launches per stage
+        // parameter cotangents written with = when dp_assign (no memset): four launches per stage.
+        // Deferred stages (the integrator's, `defer`) run lazily: a stage's second launch waits for the next
+        // stage and both run as one (launch_pair_second with next), alternating the ping-pong buffers.
+        const bool lazy = defer && h->pair_vjp && h->pair_fuse;
+        if (!lazy || chain_ws_bytes(h, B) > h->ws_bytes || 4 * (size_t)n * sizeof(T) > h->stage_ws_bytes)
+            if ((s = flush_pair(h, st)) != KANODE_OK) return s;   // (and before any buffer is reallocated)
         if ((s = ensure_ws(h, B, st)) != KANODE_OK) return s;
-        if ((s = ensure_stage_ws(h, 2 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
-        T* y = (T*)h->stage_ws;
-        T* ls = adj->y_out ? (T*)adj->y_out : (T*)h->stage_ws + n;
+        if ((s = ensure_stage_ws(h, 4 * (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
+        const int par = lazy ? h->pair_par : 0;
         const WsLayout wl = ws_layout(h, B);
         T* ws = (T*)h->ws;
-        T* ps = ws + wl.pslab;
+        const int64_t pp = par ? wl.pair2 - wl.pslab : 0;   // the ping-pong pairs' second buffer
+        T* y = (T*)h->stage_ws + (size_t)par * 2 * n;
+        T* ls = adj->y_out ? (T*)adj->y_out : y + n;
+        T* ps = ws + wl.pslab + pp;
         T* hbar = ws + wl.g0;
         const int nb = kan::widein_chunks(h->hlc[0]);
         kan::WideStageIn<T> si{};
@@ -706,11 +742,31 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         si.ls_out = ls;
         hipError_t e = hipErrorNotSupported;
         bool err_done = false;
-        if (h->pair_vjp) {   // two launches (see vjp_t), plus the λ error's final sum
+        if (lazy) {
             double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
-            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab, lamJ,
-                                           dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out,
-                                           ws + wl.bslab);
+            kan::PairPlan<T> pl;
+            e = kan::plan_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab + pp, lamJ,
+                                         dp, B, dp_assign, (double*)h->slab, kSlabBlocks, err_out, ws + wl.bslab + pp,
+                                         &pl);
+            if (e == hipSuccess) {
+                kan::PairPlan<T>& pend = pair_pending<T>(h);
+                if (h->pend_valid) e = kan::launch_pair_second<T>(pend, &pl, st);
+                else e = kan::launch_pair_first<T>(pl, st);
+                if (e != hipSuccess)
+                    return fail(h, KANODE_ERR_HIP, std::string("pair stage: ") + hipGetErrorString(e));
+                pend = pl;
+                h->pend_valid = true;
+                h->pair_par ^= 1;
+                return KANODE_OK;
+            }
+            if (e != hipErrorNotSupported)
+                return fail(h, KANODE_ERR_HIP, std::string("plan_kd_vjp_pair: ") + hipGetErrorString(e));
+            if ((s = flush_pair(h, st)) != KANODE_OK) return s;
+        } else if (h->pair_vjp) {   // two launches (see vjp_t), plus the λ error's final sum
+            double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
+            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab + pp,
+                                           lamJ, dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out,
+                                           ws + wl.bslab + pp);
             if (e != hipSuccess && e != hipErrorNotSupported)
                 return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
             err_done = e == hipSuccess && err_out != nullptr;
@@ -949,6 +1005,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
     case KANODE_OPT_ADJ_STEP_ROWS: return flag(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS");
     case KANODE_OPT_PAIR_VJP: return flag(h->pair_vjp, "PAIR_VJP");
+    case KANODE_OPT_PAIR_FUSE: return flag(h->pair_fuse, "PAIR_FUSE");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -965,6 +1022,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_GRID_ADJ_STEP: return h->grid_ovr.vstep;
     case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows ? 1 : 0;
     case KANODE_OPT_PAIR_VJP: return h->pair_vjp ? 1 : 0;
+    case KANODE_OPT_PAIR_FUSE: return h->pair_fuse ? 1 : 0;
     }
     return -1;
 }
@@ -1174,7 +1232,10 @@ kanode_status kanode_internal_check(kanode_handle* h) { return check_handle(h); 
 kanode_status kanode_internal_vjp_flush(kanode_handle* h, void* stream) {
     return vjp_flush(h, (hipStream_t)stream);
 }
-void kanode_internal_vjp_discard(kanode_handle* h) { h->njobs = 0; }
+void kanode_internal_vjp_discard(kanode_handle* h) {
+    h->njobs = 0;
+    h->pend_valid = false;
+}
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
     if (h->spec.rhs_kind != KANODE_RHS_CHAIN || batch < 1 || batch > kan::kChainSolveMaxBatch) return false;
     if (!h->fused_solve) return false;

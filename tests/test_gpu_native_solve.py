@@ -203,6 +203,35 @@ def test_native_surrogate_pair_solve_and_gradient_match_cpu_oracle():
     assert (gug - guc).abs().max().item() <= 200 * opt.reltol * guc.abs().max().item()
 
 
+@pytest.mark.parametrize("N,G,B", [(512, 5, 4), (512, 5, 8), (512, 5, 1)])
+def test_native_surrogate_fused_pair_stages_bitwise(N, G, B):
+    """KANODE_OPT_PAIR_FUSE: the native InterpolatingAdjoint of a surrogate pair holds each deferred
+    stage's second launch and runs it together with the next stage's first (kd_vjp_pair_ba_kernel, the
+    x̄ block forming the next λs over its own chunk, ping-pong buffers).  At the Burgers shapes the
+    fusion applies (one wide-in chunking on both sides); the whole adjoint, with saveat jumps, adaptive
+    error control and every gradient, is bitwise the two-launch one.  The two-launch path itself is
+    pinned to the CPU oracle above (Burgers-41) and in test_gpu_surrogate.py."""
+    chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
+    rhs = kanode.ChainRHS(chain, device=device())
+    x = np.linspace(-1.0, 1.0, N)
+    a = np.random.default_rng(N + B).normal(0.0, 0.1, (B, 3))
+    u0 = t(-np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3)))
+    p0 = t(chain.setup(np.random.default_rng(1))[0].astype(np.float64))
+    ts = [0.0, 0.01, 0.02, 0.035, 0.05]
+    w = torch.as_tensor(np.random.default_rng(2).normal(size=(len(ts),) + tuple(u0.shape)), device=device())
+    out = {}
+    for fuse in (1, 0):
+        with rhs.hd.options(pair_fuse=fuse):
+            p = p0.detach().clone().requires_grad_(True)
+            x0 = u0.detach().clone().requires_grad_(True)
+            sol = kanode.solve(rhs, x0, (0.0, 0.05), p, ts, kanode.Tsit5Options(), sensealg="interpolating_adjoint")
+            g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+            out[fuse] = (sol.u.detach(), g, gu, sol.stats)
+    assert out[1][3]["adjoint"]["naccept"] == out[0][3]["adjoint"]["naccept"] >= 4
+    for a_, b_ in zip(out[1][:3], out[0][:3]):
+        assert torch.equal(a_, b_)
+
+
 def test_native_saveat_edges():
     """saveat at t0, duplicated, between steps, on the final time and past it (dropped, as the
     Python driver never reaches it)."""
