@@ -71,6 +71,10 @@ struct kanode_handle {
     kan::PairPlan<float> pend_f{};
     bool pend_valid = false;
     int pair_par = 0;
+    // (set by the integrator) a lazy pair stage's λ error as per-block partials in err_parts (mapped host
+    // memory, summed by the host), their count in *err_nparts, instead of a final-reduction launch
+    double* err_parts = nullptr;
+    int* err_nparts = nullptr;
     int fused_solve_cap = 0;          // KANODE_OPT_FUSED_SOLVE_CAP (0 = the kernel's block)
     kan::GridOverride grid_ovr{};     // KANODE_OPT_GRID_{RHS,VJP,ADJ_STEP} (0 = default)
     // the integrator's storage for solves without a dense output (kanode_solve.cpp)
@@ -745,10 +749,15 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
         if (lazy) {
             double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
             kan::PairPlan<T> pl;
+            const bool host_parts = err_out && h->err_parts && h->err_nparts;
             e = kan::plan_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab + pp, lamJ,
-                                         dp, B, dp_assign, (double*)h->slab, kSlabBlocks, err_out, ws + wl.bslab + pp,
-                                         &pl);
+                                         dp, B, dp_assign, host_parts ? h->err_parts : (double*)h->slab, kSlabBlocks,
+                                         err_out, ws + wl.bslab + pp, &pl);
             if (e == hipSuccess) {
+                if (host_parts && pl.err_out) {   // the host sums the partials: no final launch
+                    *h->err_nparts = pl.err_rows;
+                    pl.err_out = nullptr;
+                }
                 kan::PairPlan<T>& pend = pair_pending<T>(h);
                 if (h->pend_valid) e = kan::launch_pair_second<T>(pend, &pl, st);
                 else e = kan::launch_pair_first<T>(pl, st);
@@ -764,11 +773,21 @@ kanode_status vjp_stage_t(kanode_handle* h, const T* p, const T* u, const kanode
             if ((s = flush_pair(h, st)) != KANODE_OK) return s;
         } else if (h->pair_vjp) {   // two launches (see vjp_t), plus the λ error's final sum
             double* err_out = adj->want_error ? (double*)adj->error_sumsq : nullptr;
-            e = kan::launch_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab + pp,
-                                           lamJ, dp, B, st, dp_assign, (double*)h->slab, kSlabBlocks, err_out,
-                                           ws + wl.bslab + pp);
-            if (e != hipSuccess && e != hipErrorNotSupported)
-                return fail(h, KANODE_ERR_HIP, std::string("launch_kd_vjp_pair: ") + hipGetErrorString(e));
+            const bool host_parts = err_out && h->err_parts && h->err_nparts;   // (as the lazy path)
+            kan::PairPlan<T> pl;
+            e = kan::plan_kd_vjp_pair<T>(h->hlc[0], h->hlc[1], h->dlc, p, u, &si, lam, y, ps, ws + wl.sslab + pp, lamJ,
+                                         dp, B, dp_assign, host_parts ? h->err_parts : (double*)h->slab, kSlabBlocks,
+                                         err_out, ws + wl.bslab + pp, &pl);
+            if (e == hipSuccess) {
+                if (host_parts && pl.err_out) {
+                    *h->err_nparts = pl.err_rows;
+                    pl.err_out = nullptr;
+                }
+                if ((e = kan::launch_pair_first<T>(pl, st)) == hipSuccess) e = kan::launch_pair_second<T>(pl, nullptr, st);
+                if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("pair stage: ") + hipGetErrorString(e));
+            } else if (e != hipErrorNotSupported) {
+                return fail(h, KANODE_ERR_HIP, std::string("plan_kd_vjp_pair: ") + hipGetErrorString(e));
+            }
             err_done = e == hipSuccess && err_out != nullptr;
         }
         if (e != hipSuccess) {
@@ -1268,6 +1287,13 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
     return KANODE_OK;
 }
 int kanode_internal_max_parts() { return kSlabBlocks; }
+void kanode_internal_set_err_parts(kanode_handle* h, double* parts, int* nparts) {
+    h->err_parts = parts;
+    h->err_nparts = nparts;
+}
+bool kanode_internal_pair_lazy(const kanode_handle* h) {
+    return h->spec.rhs_kind == KANODE_RHS_CHAIN && surrogate_pair(h) && h->pair_vjp && h->pair_fuse;
+}
 kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                          void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                          double abstol, double reltol, double* err_out, int64_t batch, void* stream,

@@ -59,6 +59,10 @@ kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const voi
 // kanode_internal_max_parts() of them, device-visible memory -- and their count returned for the caller
 // to sum, instead of the total into err_out)
 int kanode_internal_max_parts();
+// the surrogate pair's adjoint stages run lazily when deferred (KANODE_OPT_PAIR_FUSE)
+bool kanode_internal_pair_lazy(const kanode_handle* h);
+// the integrator's mapped error-partial buffer for lazy pair stages (nullptr: off), see kanode_abi.cpp
+void kanode_internal_set_err_parts(kanode_handle* h, double* parts, int* nparts);
 // a whole Tsit5 step of a small chain per column (kd_chain_step_kernel); K-form dense output
 kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                          void* const* kout, void* u_new, const double* a6x6, const double* e7,

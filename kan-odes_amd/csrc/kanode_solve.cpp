@@ -916,6 +916,12 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     // (-> lam_out), lamJ = λsᵀ∂f/∂u, dpo = λsᵀ∂f/∂p; ec != NULL adds the λ error total -> err
     // defer: the dp / error reductions of this stage wait for flush() (one launch per step)
     kanode_internal_vjp_discard(h);   // nothing pending from an earlier failed call
+    int lam_parts = 0;                // > 0: the step's λ error as that many partials in hparts
+    struct PartsOff {                 // the handle must not keep the solution's buffer past this call
+        kanode_handle* h;
+        ~PartsOff() { kanode_internal_set_err_parts(h, nullptr, nullptr); }
+    } parts_off{h};
+    if (o.adaptive && s->mparts) kanode_internal_set_err_parts(h, s->mparts, &lam_parts);
     auto adj_rhs = [&](double tau, const void* l, int nl, void* const* lks, const double* lc, void* lamJ, void* dpo,
                        void* lam_out, const double* ec, double* err, bool defer = false) -> kanode_status {
         const double t = tf - tau;
@@ -995,6 +1001,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         bool combined = false;
         bool finished = false;     // adaptive step: μ_new, kμ_7 and the μ error terms formed by the finish launch
         if (o.adaptive && s->mscal) arm_ctl(s->hscal, kScalars);
+        lam_parts = 0;
         if (s->qform) {
             kan::AdjStepArgs a{};
             for (int j = 0; j < 7; ++j) a.kl[j] = (double*)kl[j];
@@ -1078,6 +1085,13 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                 double mus = 0.0;
                 for (int64_t q = 0; q < P; ++q) mus += s->hscal[9 + q];
                 sumsq = s->hscal[8] + mus;
+            } else if (lam_parts > 0) {   // the λ error partials (hparts) and the μ partials (slots 16..)
+                SOLVE_TRY(wait_ctl(h, st, {{s->hparts, lam_parts}, {s->hscal + 16, fin_blocks}}));
+                double ls = 0.0, mus = 0.0;
+                for (int b = 0; b < lam_parts; ++b) ls += s->hparts[b];
+                for (int b = 0; b < fin_blocks; ++b) mus += s->hscal[16 + b];
+                arm_ctl(s->hparts, lam_parts);
+                sumsq = ls + mus;
             } else {   // the λ total (slot 0) and the μ partials (slots 16..) in one read
                 if (s->mscal) SOLVE_TRY(wait_ctl(h, st, {{s->hscal, 1}, {s->hscal + 16, fin_blocks}}));
                 else SOLVE_TRY(read_ctl(h, s, 0, 16 + fin_blocks, st));
@@ -1121,7 +1135,10 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
                         ones[ng++] = 1.0;
                     }
                     key->live = false;
-                    SOLVE_TRY(adj_rhs(tau, lam[lcur], ng, g, ones, kl[0], km[0], lam[lcur ^ 1], nullptr, nullptr));
+                    // (deferred where the surrogate pair's stages run lazily: its second launch then runs
+                    // together with the next step's first stage, whose λs starts from this kλ_1)
+                    SOLVE_TRY(adj_rhs(tau, lam[lcur], ng, g, ones, kl[0], km[0], lam[lcur ^ 1], nullptr, nullptr,
+                                      kanode_internal_pair_lazy(h)));
                     lcur ^= 1;
                 } else {
                     SOLVE_TRY(add_jump(*key, lam[lcur]));                   // callback: λ += ∂L/∂u(t_j)
@@ -1133,6 +1150,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         }
         hstep = hnew;
     }
+    SOLVE_TRY(kanode_internal_vjp_flush(h, st));   // (a deferred stage's last launch)
     if (it == o.maxiters && !(tau >= TT - 1e-14 * std::max(1.0, TT)))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
     for (auto& jm : jumps)   // a saveat at t0 adds to dL/du0 only
