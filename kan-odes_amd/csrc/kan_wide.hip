@@ -28,14 +28,6 @@
 
 namespace kan {
 
-// KAN_ABL (timing experiments only, tools/surr_ablate.sh; results are wrong when set): 1 the wide-in
-// parameter blocks' column loop, 3 the dot-product gathers, 7 the pair forward's dot products skipped;
-// 4 / 5 / 6 the pair pullback's wide-out parameter / x̄ / wide-in parameter blocks exit at once; 8 / 9
-// the pair's first / second launch exits at once
-#ifndef KAN_ABL
-#define KAN_ABL 0
-#endif
-
 
 constexpr int kKT = 8;        // column tile (trajectories per pass)
 constexpr int kOWide = 16;    // max out_dims of a wide-in layer
@@ -249,7 +241,7 @@ __device__ __forceinline__ void widein_fwd_body(const LayerConst* __restrict__ l
             const LayerConst& l1 = *pd->lc1;
             const int R1 = l1.G + (l1.use_base ? 1 : 0), IR = l1.I * R1, O1 = l1.O;
             const int ns = IR >= 256 ? 1 : 256 / IR;
-            for (int q0 = 0; q0 < (KAN_ABL == 7 ? 0 : IR); q0 += 256 / ns) {
+            for (int q0 = 0; q0 < IR; q0 += 256 / ns) {
                 const int q = q0 + t / ns, sub = t - (t / ns) * ns;
                 T a = T(0);
                 if (q < IR && t / ns < 256 / ns) {
@@ -641,7 +633,7 @@ __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ l
         T dcv[kS], dwv[kS];
 #pragma unroll
         for (int m = 0; m < kS; ++m) dcv[m] = dwv[m] = T(0);
-        if (q < nq && KAN_ABL != 1 && bg) {
+        if (q < nq && bg) {
             // the basis values the pair's forward blocks stored (WideBasisG): per slot, eight columns'
             // loads in flight, accumulated in ascending k (the per-slot order of the loop below)
             const int64_t ps = (int64_t)I * G;
@@ -673,7 +665,7 @@ __device__ __forceinline__ void widein_vjp_body(const LayerConst* __restrict__ l
                     }
                 }
             }
-        } else if (q < nq && KAN_ABL != 1) {
+        } else if (q < nq) {
             for (int64_t k = q; k < K; k += nq) {
                 const T yb = yb_at(o, k);
 #pragma unroll
@@ -823,7 +815,6 @@ __global__ void __launch_bounds__(256)
 kd_vjp_pair_a_kernel(const LayerConst* __restrict__ lc0, const LayerConst* __restrict__ lc1, const T* __restrict__ p,
                      const T* __restrict__ x, T* __restrict__ pslab, const T* __restrict__ ybar, T* __restrict__ spart,
                      int64_t K, int nblk, int gyF, WideStageIn<T> si, WideBasisG<T> bg) {
-    if (KAN_ABL == 8) return;
     const PairDot<T> pd{lc1, spart, ybar, bg};
     widein_fwd_body<T, STAGE, MV, MW, true>(lc0, p, x, pslab, K, STAGE ? &si : nullptr, blockIdx.x % nblk,
                                             blockIdx.x / nblk, gyF, &pd);
@@ -959,9 +950,6 @@ __device__ __forceinline__ bool pair_b_body(const LayerConst* __restrict__ lc0, 
     const int nbx = a.nbx, np = a.np, nblk = a.nblk;
     const T* __restrict__ pslab = a.pslab;
     const T* __restrict__ S = a.S;
-    if (KAN_ABL == 9 || (KAN_ABL == 4 && b < a.nP)) return false;
-    if (KAN_ABL == 5 && b >= a.nP && (b - a.nP) / nbx >= np) return false;
-    if (KAN_ABL == 6 && b >= a.nP && (b - a.nP) / nbx < np) return false;
     if (b < a.nP) {   // four wide-out parameter units per block, one per wave
         const int w = threadIdx.x / kWave;
         const int64_t ph = (int64_t)(lc1->G + 1) * K;
@@ -984,8 +972,8 @@ __device__ __forceinline__ bool pair_b_body(const LayerConst* __restrict__ lc0, 
     widein_vjp_body<T>(
         lc0, p, a.x, [&](int, int64_t k) { return hbL[k]; },
         [&](int o) {   // hidden unit o over all columns: S[o, r, k] for r < R, k < K, and h[o, k]
-            block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K,
-                                 KAN_ABL == 3 ? 0 : nblk, red, Sv);
+            block_gather_sums<T>([&](int v, int c) { return S[c * bs + (int64_t)o * R * K + v]; }, R * (int)K, nblk,
+                                 red, Sv);
             for (int64_t k = threadIdx.x; k < K; k += blockDim.x)
                 hv[k] = layer_in<T>(nullptr, pslab, nblk, H, K, o, k);
             __syncthreads();
@@ -995,7 +983,7 @@ __device__ __forceinline__ bool pair_b_body(const LayerConst* __restrict__ lc0, 
         },
         [&](T* ybL, int t, int64_t k) {   // column k over all hidden units: S[i, r, k] and h[i, k]
             block_gather_sums<T>(
-                [&](int v, int c) { return S[c * bs + (int64_t)v * K + k]; }, H * R, KAN_ABL == 3 ? 0 : nblk, red, Sv);
+                [&](int v, int c) { return S[c * bs + (int64_t)v * K + k]; }, H * R, nblk, red, Sv);
             if (t < H) hv[t] = layer_in<T>(nullptr, pslab, nblk, H, K, t, k);
             __syncthreads();
             if (t < H) ybL[t] = wideout_xfin_lds<T, PATH>(M, l1, hv[t], Sv + t * R, 1);
