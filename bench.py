@@ -11,10 +11,15 @@ call: table build + RHS kernel; the parameters alternate between two bitwise-dif
 vectors so that every step rebuilds the table).  value = total trajectories x steps /
 max-over-ranks wall time.
 
-Multi-GPU: one process per GPU (torchrun); the fixed total batch (default
-1,048,576 trajectories = 8 x 131,072) shards evenly across ranks with no
-collective on the data path: strong scaling, total work fixed as N grows
-(`--batch-per-gpu` switches to weak scaling).
+Multi-GPU: one process per GPU; the fixed total batch (default 1,048,576
+trajectories = 8 x 131,072) shards evenly across ranks with no collective on the
+data path: strong scaling, total work fixed as N grows (`--batch-per-gpu`
+switches to weak scaling).  Under an external launcher (torchrun: WORLD_SIZE set)
+`--gpus` must equal WORLD_SIZE.  Without one, `--gpus N > 1` starts N child
+processes of this script itself (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, before
+anything in this process touches the GPU), forwards rank 0's JSON line and exits
+non-zero if any rank fails.  The line carries `rccl_world` (the process group's
+own world size after init) and every rank's timed-region seconds.
 
 Extra JSON fields: `roofline` (dominant kernel, HIP-event timed on its stream),
 `cpu_baseline` (the CPU restatement of the reference algorithm — dense Laplacian
@@ -26,6 +31,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -502,6 +509,72 @@ def surrogate_dist_bench(dev, rank: int, world: int, backend: str, reps: int = 2
     return out
 
 
+LAUNCH_ENV = "KANODE_BENCH_LAUNCH"      # set by launch_ranks in the children it starts
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_world(gpus: int, env) -> tuple[str, int]:
+    """How this process runs: ("single", 1), ("rank", WORLD_SIZE) under a launcher, or ("spawn", N)
+    when --gpus N > 1 and nothing launched us.  Raises SystemExit when an external launcher's
+    WORLD_SIZE disagrees with --gpus (the driver's `torchrun --nproc-per-node N bench.py --gpus N`
+    must time N ranks, never silently fewer)."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("spawn", gpus) if gpus > 1 else ("single", 1)
+    world = int(ws)
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("rank", world) if world > 1 else ("single", 1)
+
+
+def launch_ranks(n: int, cmd: list[str], env=None, poll_s: float = 0.2, grace_s: float = 20.0) -> int:
+    """Start n fresh processes of `cmd` as the ranks of one job (127.0.0.1 rendezvous on a free port),
+    each with RANK = LOCAL_RANK = r, WORLD_SIZE = n.  Children are started, never exec'd into: this
+    process has not touched the GPU and does not.  The children inherit stdout (rank 0 prints the JSON
+    line).  If a rank exits non-zero the others are terminated (exact PIDs; killed after `grace_s`) so a
+    rank blocked in a collective cannot hang the job.  Returns 0 when every rank succeeded, otherwise
+    the first failing rank's exit status (1 for a signal)."""
+    base = dict(os.environ if env is None else env)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), LAUNCH_ENV: "self"})
+        procs.append(subprocess.Popen(cmd, env=e))
+    rc, live = 0, set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    procs[q].terminate()
+                t_end = time.time() + grace_s
+                for q in live:
+                    try:
+                        procs[q].wait(timeout=max(0.1, t_end - time.time()))
+                    except subprocess.TimeoutExpired:
+                        procs[q].kill()
+                        procs[q].wait()
+                live.clear()
+        if live:
+            time.sleep(poll_s)
+    return rc
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -530,18 +603,28 @@ def main() -> None:
                     help="tuning: persistent grid of the table RHS kernel (KANODE_OPT_GRID_RHS; 0 = default)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    mode, world = resolve_world(args.gpus, os.environ)
+    if mode == "spawn":
+        # nothing in this process has touched the GPU: the ranks are fresh children of this script
+        raise SystemExit(launch_ranks(world, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()) if dist else 0)
     torch.cuda.set_device(dev)
+    rccl_world = None
     if dist:
+        import datetime
         import torch.distributed as tdist
+        # a rank that dies inside a collective must not hang the others forever
+        tmo = datetime.timedelta(minutes=10)
         if args.dist_backend == "nccl":
-            tdist.init_process_group("nccl", device_id=dev)
+            tdist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            tdist.init_process_group("gloo")
+            tdist.init_process_group("gloo", timeout=tmo)
+        rccl_world = tdist.get_world_size()
+        if rccl_world != world:
+            raise SystemExit(f"bench.py: process group has {rccl_world} ranks, expected {world}")
 
     nx, D = 256, 0.01
     dx = 1.0 / (nx - 1)
@@ -591,10 +674,14 @@ def main() -> None:
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    rank_elapsed = [elapsed]
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        cdev = dev if args.dist_backend == "nccl" else "cpu"
+        mine = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        allt = [torch.zeros_like(mine) for _ in range(world)]
+        tdist.all_gather(allt, mine)
+        rank_elapsed = [float(t.item()) for t in allt]
+        elapsed = max(rank_elapsed)
     kern_ms = e_beg.elapsed_time(e_end) / args.steps
     # this box's streaming reference: a device copy moving the same bytes (u -> du)
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -629,6 +716,11 @@ def main() -> None:
                    "kan": "KDense(1,1,10) softsign rbf",
                    "kan_eval": "piecewise-polynomial table" if table else "basis recurrence",
                    "parallelism": f"trajectory-sharded x{world} (no data-path collective)"},
+        "rccl_world": rccl_world,
+        "dist_backend": args.dist_backend if dist else None,
+        "launch": ("self-spawned ranks (bench.py --gpus)" if os.environ.get(LAUNCH_ENV) == "self"
+                   else "external launcher (WORLD_SIZE)") if dist else "single process",
+        "rank_timed_s": rank_elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("fk_pp_build_kernel + fk_rhs_pp_wave_kernel<SOFTSIGN,RBF,2>" if table
@@ -680,12 +772,22 @@ def main() -> None:
                                                          0 if (args.no_cpu_baseline or world > 1) else 2)
 
     if dist and not args.no_dist_surrogates:
-        # a secondary leg: an exception here (raised on every rank alike: the ranks run the same code)
-        # is recorded in the line instead of taking the metric above down with it
+        # a secondary leg: an exception here is recorded in the line instead of taking the metric above
+        # down with it.  Every rank then all-reduces a failure flag before any further collective, so a
+        # rank that failed alone (an allocation, a HIP error on one GPU) does not leave the others
+        # waiting; a rank that dies inside one of the leg's collectives ends at the process-group timeout
+        # and the launcher stops the job.
+        err = None
         try:
             sd = surrogate_dist_bench(dev, rank, world, args.dist_backend)
         except Exception as e:  # noqa: BLE001
-            sd = {"dist_surrogates_error": f"{type(e).__name__}: {e}"[:300]}
+            err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
+            sd = {}
+        flag = torch.tensor([1.0 if err else 0.0], dtype=torch.float64,
+                            device=dev if args.dist_backend == "nccl" else "cpu")
+        tdist.all_reduce(flag, op=tdist.ReduceOp.MAX)
+        if float(flag.item()) > 0:
+            sd = {"dist_surrogates_error": err or "failed on another rank"}
         if rank == 0:
             out.update(sd)
 

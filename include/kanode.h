@@ -129,7 +129,10 @@ kanode_status kanode_knots(const kanode_handle* h, int32_t layer, float* grid_ou
 /* Pre-size handle workspaces for batches up to max_batch (no allocation in later
  * device calls with batch <= max_batch; required before hipGraph capture).  A device
  * call that would still need to allocate while its stream is capturing returns
- * KANODE_ERR_CAPTURE instead. */
+ * KANODE_ERR_CAPTURE instead.  It takes no stream, so it SYNCHRONISES THE WHOLE DEVICE
+ * (hipDeviceSynchronize, then a synchronous reset of the table stamps): call it outside the
+ * timed / overlapped region, and never while any stream of the process is being captured (a
+ * device-wide synchronisation invalidates a global-mode capture on another thread). */
 kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
 
 /* Evaluation-strategy switches (no reference counterpart: they select between

@@ -308,11 +308,15 @@ WsLayout ws_layout(const kanode_handle* h, int64_t B) {
 
 size_t chain_ws_bytes(const kanode_handle* h, int64_t B) { return (size_t)ws_layout(h, B).total * h->esize; }
 
+kanode_status flush_pair(kanode_handle* h, hipStream_t st);
+
 kanode_status ensure_ws(kanode_handle* h, int64_t B, hipStream_t st) {
     const size_t need = h->spec.rhs_kind == KANODE_RHS_CHAIN ? chain_ws_bytes(h, B) : 0;
     if (need <= h->ws_bytes) return KANODE_OK;
     if (is_capturing(st))
         return fail(h, KANODE_ERR_CAPTURE, "batch exceeds reserved workspace during stream capture; call kanode_reserve");
+    // a deferred surrogate-pair stage reads the old workspace: launch it before the buffer goes away
+    if (kanode_status s = flush_pair(h, st); s != KANODE_OK) return s;
     HIP_TRY(h, hipStreamSynchronize(st));
     if (h->ws) HIP_TRY(h, hipFree(h->ws));
     h->ws = nullptr;
@@ -588,6 +592,7 @@ kanode_status stage_t(kanode_handle* h, const T* p, const T* u, const kanode_sta
 kanode_status ensure_stage_ws(kanode_handle* h, size_t need, hipStream_t st) {
     if (need <= h->stage_ws_bytes) return KANODE_OK;
     if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "stage workspace too small during capture");
+    if (kanode_status s = flush_pair(h, st); s != KANODE_OK) return s;   // (reads the old stage workspace)
     HIP_TRY(h, hipStreamSynchronize(st));
     if (h->stage_ws) HIP_TRY(h, hipFree(h->stage_ws));
     h->stage_ws = nullptr;

@@ -129,6 +129,9 @@ struct kanode_solution {
     // host sums them, so no final-reduction launch per adaptive step); hparts / its device address
     double* hparts = nullptr;
     double* mparts = nullptr;
+    // a call on this solution failed: its kernels may still be in flight and its mapped step-control slots
+    // may hold written values; the next call drains the stream and re-arms every slot first (ctl_begin)
+    bool ctl_dirty = false;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -317,6 +320,18 @@ kanode_status wait_ctl(kanode_handle* h, hipStream_t st, std::initializer_list<C
         }
         __builtin_ia32_pause();
     }
+}
+
+// Before a solve / adjoint on a solution whose previous call failed: wait for that call's kernels (they may
+// still write the mapped slots), then arm every partials slot again, so a polled step control never reads
+// an earlier call's values.  The happy path costs nothing.
+kanode_status ctl_begin(kanode_handle* h, kanode_solution* s, hipStream_t st) {
+    if (!s->ctl_dirty) return KANODE_OK;
+    if (!capturing(st)) SOLVE_HIP(h, hipStreamSynchronize(st));
+    if (s->hparts) arm_ctl(s->hparts, kanode_internal_max_parts());
+    if (s->hscal) arm_ctl(s->hscal, kScalars);
+    s->ctl_dirty = false;
+    return KANODE_OK;
 }
 
 kanode_stage make_stage(int nk, void* const* k, const double* c) {
@@ -1355,8 +1370,8 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
     s->ts.clear();
     s->dts.clear();
     s->qform = false;   // K-form dense output unless the host loop takes the Fisher-KPP step path
-    kanode_status r;
-    {
+    kanode_status r = ctl_begin(h, s, st);
+    if (r == KANODE_OK) {
         TableHold hold(h);
         // auto = host: a replayed graph node costs the GPU what an eager launch does (ROCm 7.2,
         // tools/solve_modes.py), so device control only wins where the per-step norm read is a
@@ -1380,6 +1395,7 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
                                         : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
         }
     }
+    if (r != KANODE_OK) s->ctl_dirty = true;
     if (record || s->state_bytes() <= (size_t)64 << 20) {
         *slot = s;   // kept for the next solve (a large scratch solve gives its memory back)
     } else {
@@ -1401,11 +1417,19 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
     if (s->h != h || !s->record)
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint: dense output of another handle or not recorded");
     hipStream_t st = (hipStream_t)stream;
+    SOLVE_TRY(ctl_begin(h, s, st));
     TableHold hold(h);
     bool done = false;
-    SOLVE_TRY(s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
-                                     : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done));
-    if (done) return KANODE_OK;
-    return s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
-                                  : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);
+    kanode_status r = s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
+                                             : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done);
+    if (r == KANODE_OK && !done)
+        r = s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
+                                   : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);
+    if (r != KANODE_OK) {
+        // a failed adjoint may leave a deferred surrogate-pair stage (raw pointers into this solution and the
+        // handle's workspace) and finish jobs pending on the handle: drop them, so no later call launches them
+        kanode_internal_vjp_discard(h);
+        s->ctl_dirty = true;
+    }
+    return r;
 }

@@ -627,3 +627,38 @@ def test_options_round_trip_and_reject_bad_values():
             hd.set_option(name, bad)
     with pytest.raises(KeyError):
         hd.set_option("no_such_option", 1)
+
+
+def test_failed_adjoint_leaves_no_pending_stage():
+    """a lazy surrogate-pair adjoint stage keeps raw pointers into the solution and the
+    handle's workspace until the next stage.  An adjoint that fails mid-run (here: maxiters) must drop it:
+    afterwards the same handle's adjoint stage and a full adjoint over the same dense output equal a fresh
+    handle's, bit for bit (a stale second launch would have added into them)."""
+    N, G, B = 512, 5, 4
+    mk = lambda: kanode.ChainRHS(kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"),   # noqa: E731
+                                              kanode.KDense(10, N, G, normalizer="softsign")), device=device())
+    rhs, fresh = mk(), mk()
+    x = np.linspace(-1.0, 1.0, N)
+    a = np.random.default_rng(7).normal(0.0, 0.1, (B, 3))
+    u0 = t(-np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3)))
+    p = t(rhs.chain.setup(np.random.default_rng(1))[0].astype(np.float64))
+    ts = [0.0, 0.01, 0.02, 0.035, 0.05]
+    g = torch.as_tensor(np.random.default_rng(2).normal(size=(len(ts),) + tuple(u0.shape)), device=device())
+    opt = kanode.Tsit5Options()
+    for r in (rhs, fresh):
+        r.hd.set_option("pair_fuse", 1)
+    _, _, dense = rhs.hd.solve_tsit5(p, u0, 0.0, 0.05, ts, opt.to_c(), keep_dense=True)
+    bad = opt.to_c()
+    bad.maxiters = 2
+    with pytest.raises(kanode.KanodeError, match="maxiters"):
+        rhs.hd.adjoint_tsit5(p, dense, g, bad, tuple(u0.shape))
+    lam = torch.as_tensor(np.random.default_rng(3).normal(size=tuple(u0.shape)), device=device())
+    r1 = rhs.hd.vjp_stage(p, u0, [], [], lam, [], [])
+    r2 = fresh.hd.vjp_stage(p, u0, [], [], lam, [], [])
+    torch.cuda.synchronize()
+    assert torch.equal(r1[0], r2[0]) and torch.equal(r1[1], r2[1])
+    du0, dp, st = rhs.hd.adjoint_tsit5(p, dense, g, opt.to_c(), tuple(u0.shape))
+    _, _, dense2 = fresh.hd.solve_tsit5(p, u0, 0.0, 0.05, ts, opt.to_c(), keep_dense=True)
+    du0f, dpf, stf = fresh.hd.adjoint_tsit5(p, dense2, g, opt.to_c(), tuple(u0.shape))
+    assert st == stf
+    assert torch.equal(du0, du0f) and torch.equal(dp, dpf)
