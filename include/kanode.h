@@ -12,6 +12,8 @@
  *       Lotka-Volterra/src/kdense.jl:20-107 (PDE copy: PDE examples/src/kdense.jl:20-107)
  *   kanode_layer_forward
  *       (l::KDense)(x, p, st) -> (y, st)                     Lotka-Volterra/src/kdense.jl:109-130
+ *   kanode_layer_forward_stage
+ *       the same call at a Runge-Kutta stage input (grid-sharded surrogate, PDE examples/Burgers_Surrogate.jl:85-97)
  *   kanode_layer_vjp
  *       Zygote pullback of the above incl. rrule(_rbf)        Lotka-Volterra/src/utils.jl:15-21
  *   kanode_rhs  (rhs_kind = CHAIN)
@@ -321,6 +323,16 @@ kanode_status kanode_vjp_host(kanode_handle* h, const void* p, const void* u, co
 /* y[O,K] = KDense_layer(x[I,K]; p_layer)  (p_layer = that layer's (C, W) slice) */
 kanode_status kanode_layer_forward(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, void* y,
                                    int64_t K, void* stream);
+/* The same layer at a Runge-Kutta / adjoint stage input (the grid-sharded surrogate's first layer,
+ * kanode/tp.py; Burgers_Surrogate.jl:85-97 "grid sharded"):
+ *     y  = x + Σ_{j<sx->n_prev} sx->c[j]·sx->k[j]        -> sx->y_out (nullable)
+ *     λs = lam + Σ_{j<sl->n_prev} sl->c[j]·sl->k[j]      -> sl->y_out (only when lam != NULL)
+ *     out[O,K] = KDense_layer(y; p_layer)
+ * k, lam, y_out are [I,K] arrays; want_error is ignored.  A wide input layer forms y and λs inside its
+ * forward kernel (no combination launches); other layers run the combinations as separate launches. */
+kanode_status kanode_layer_forward_stage(kanode_handle* h, int32_t layer, const void* p_layer, const void* x,
+                                         const kanode_stage* sx, const void* lam, const kanode_stage* sl, void* out,
+                                         int64_t K, void* stream);
 /* xbar[I,K] = pullback(ybar)  (nullable); pbar_layer[P_l] += ... (nullable) */
 kanode_status kanode_layer_vjp(kanode_handle* h, int32_t layer, const void* p_layer, const void* x,
                                const void* ybar, void* xbar, void* pbar_layer, int64_t K, void* stream);

@@ -828,6 +828,40 @@ kanode_status check_handle(kanode_handle* h) {
 
 }  // namespace
 
+namespace {
+// one layer at a stage input (kanode_layer_forward_stage): y = x + Σ c·k (and λs = lam + Σ c·k) formed by the
+// wide-in forward's blocks themselves (kd_fwd_widein_stage_kernel, the fma order of stage_lincomb_kernel);
+// any other layer kind gets the combinations as their own launches first
+template <typename T>
+kanode_status layer_fwd_stage_t(kanode_handle* h, int l, const T* p_full, const T* x, const kanode_stage* sx,
+                                const T* lam, const kanode_stage* sl, T* out, int64_t K, hipStream_t st) {
+    kan::StageArgs<T> su{}, sla{};
+    kanode_status s = stage_args<T>(h, sx, su);
+    if (s != KANODE_OK) return s;
+    if (lam && (s = stage_args<T>(h, sl, sla)) != KANODE_OK) return s;
+    const LayerConst& hl = h->hlc[l];
+    const int64_t n = (int64_t)hl.I * K;
+    if (h->kind[l] == KIND_WIDE_IN) {
+        kan::WideStageIn<T> si{};
+        si.su = su;
+        si.y_out = (T*)sx->y_out;
+        si.lam = lam;
+        si.sl = sla;
+        si.ls_out = lam ? (T*)sl->y_out : nullptr;
+        HIP_TRY(h, kan::launch_kd_fwd_widein<T>(hl, h->dlc + l, p_full, x, out, wide_slab<T>(h, K), K, st, &si));
+        return KANODE_OK;
+    }
+    T* y = (T*)sx->y_out;
+    if (!y) {
+        if ((s = ensure_stage_ws(h, (size_t)n * sizeof(T), st)) != KANODE_OK) return s;
+        y = (T*)h->stage_ws;
+    }
+    HIP_TRY(h, kan::launch_stage_lincomb<T>(x, su, y, n, st));
+    if (lam) HIP_TRY(h, kan::launch_stage_lincomb<T>(lam, sla, (T*)sl->y_out, n, st));
+    return layer_fwd_t<T>(h, l, p_full, y, out, K, st);
+}
+}  // namespace
+
 extern "C" {
 
 int32_t kanode_abi_version(void) { return KANODE_ABI_VERSION; }
@@ -1171,6 +1205,26 @@ kanode_status kanode_layer_forward(kanode_handle* h, int32_t layer, const void* 
     if (h->spec.dtype == KANODE_F64)
         return layer_fwd_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, (double*)y, K, st);
     return layer_fwd_t<float>(h, layer, (const float*)p_layer - off, (const float*)x, (float*)y, K, st);
+}
+
+kanode_status kanode_layer_forward_stage(kanode_handle* h, int32_t layer, const void* p_layer, const void* x,
+                                         const kanode_stage* sx, const void* lam, const kanode_stage* sl, void* out,
+                                         int64_t K, void* stream) {
+    kanode_status s = check_handle(h);
+    if (s != KANODE_OK) return s;
+    if (layer < 0 || layer >= h->n_layers) return fail(h, KANODE_ERR_INVALID_ARG, "layer out of range");
+    if (K < 0) return fail(h, KANODE_ERR_INVALID_ARG, "K < 0");
+    if (K == 0) return KANODE_OK;
+    if (!p_layer || !x || !sx || !out) return fail(h, KANODE_ERR_INVALID_ARG, "null pointer");
+    if (lam && (!sl || !sl->y_out)) return fail(h, KANODE_ERR_INVALID_ARG, "lam needs sl with y_out (the λs output)");
+    const int64_t off = h->hlc[layer].p_off;
+    hipStream_t st = (hipStream_t)stream;
+    if ((s = ensure_ws(h, K, st)) != KANODE_OK) return s;
+    if (h->spec.dtype == KANODE_F64)
+        return layer_fwd_stage_t<double>(h, layer, (const double*)p_layer - off, (const double*)x, sx,
+                                         (const double*)lam, sl, (double*)out, K, st);
+    return layer_fwd_stage_t<float>(h, layer, (const float*)p_layer - off, (const float*)x, sx, (const float*)lam, sl,
+                                    (float*)out, K, st);
 }
 
 kanode_status kanode_layer_vjp(kanode_handle* h, int32_t layer, const void* p_layer, const void* x, const void* ybar,

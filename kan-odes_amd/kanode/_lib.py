@@ -121,6 +121,8 @@ SIGNATURES = [
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
     ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),
     ("kanode_layer_forward", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
+    ("kanode_layer_forward_stage", C.c_int, [_H, C.c_int32, _P, _P, C.POINTER(StageC), _P, C.POINTER(StageC), _P,
+                                             C.c_int64, _P]),
     ("kanode_layer_vjp", C.c_int, [_H, C.c_int32, _P, _P, _P, _P, _P, C.c_int64, _P]),
     ("kanode_edge_activations", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
     ("kanode_adam_step", C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_double,

@@ -137,7 +137,12 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
         if opt.adaptive:
             emu = sum((h * b) * k.double() for b, k in zip(BTILDE, km))        # norms in double
             skm = opt.abstol + torch.maximum(mu.abs(), mu_new.abs()).double() * opt.reltol
-            EEst = math.sqrt(_gsum(f, sumsq.item(), _rms2(emu / skm)) / ntot)
+            red = getattr(f, "reduce_dev", None)
+            if red is not None:     # grid shards: one device all-reduce of the step's error terms, one host read
+                loc = sumsq.reshape(()) + ((emu / skm) ** 2).sum()
+                EEst = math.sqrt(float(red(loc.reshape(1)).item()) / ntot)
+            else:
+                EEst = math.sqrt(_gsum(f, sumsq.item(), _rms2(emu / skm)) / ntot)
             q11 = EEst ** opt.beta1 if EEst > 0 else 0.0
             if EEst > 1.0 and h > opt.dtmin:
                 nreject += 1

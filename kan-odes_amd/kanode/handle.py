@@ -346,6 +346,28 @@ class KanodeHandle:
                                              _stream(self.device)), self._h, "kanode_layer_forward")
         return y
 
+    def layer_forward_stage(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor, ks, c, y_out=None,
+                            lam=None, lks=(), lc=(), ls_out=None) -> torch.Tensor:
+        """kanode_layer_forward_stage: the layer at y = x + Σ c_j k_j (-> y_out if given) and, with lam,
+        λs = lam + Σ lc_j lk_j -> ls_out (required then); returns the layer output (K, O)."""
+        cfg = self.layers[layer]
+        K = x.shape[0]
+        self._check_t(p_layer, (cfg.param_length,), "p_layer")
+        for a, nm in [(x, "x")] + [(k, "k") for k in ks] + ([(y_out, "y_out")] if y_out is not None else []):
+            self._check_t(a, (K, cfg.in_dims), nm)
+        if lam is not None:
+            if ls_out is None:
+                raise ValueError("layer_forward_stage: lam needs ls_out")
+            for a, nm in [(lam, "lam"), (ls_out, "ls_out")] + [(k, "lk") for k in lks]:
+                self._check_t(a, (K, cfg.in_dims), nm)
+        sx = self._stage_struct(ks, c, y_out)
+        sl = self._stage_struct(lks, lc, ls_out) if lam is not None else None
+        y = torch.empty((K, cfg.out_dims), dtype=self.dtype, device=self.device)
+        L.check(L.lib().kanode_layer_forward_stage(self._h, layer, _ptr(p_layer), _ptr(x), C.byref(sx), _ptr(lam),
+                                                   C.byref(sl) if sl is not None else None, _ptr(y), K,
+                                                   _stream(self.device)), self._h, "kanode_layer_forward_stage")
+        return y
+
     def layer_vjp(self, layer: int, p_layer: torch.Tensor, x: torch.Tensor, ybar: torch.Tensor):
         cfg = self.layers[layer]
         K = x.shape[0]

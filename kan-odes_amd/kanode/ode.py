@@ -64,12 +64,13 @@ def rms(x: torch.Tensor) -> torch.Tensor:
 
 def _norm(f, x: torch.Tensor) -> float:
     """ODE_DEFAULT_NORM of x: RMS over every state entry.  A state sharded over ranks
-    (kanode.tp) supplies f.reduce_sum, and the sum and count run over all shards."""
-    red = getattr(f, "reduce_sum", None)
+    (kanode.tp) supplies f.reduce_dev / f.global_count, and the sum and count run over all shards
+    (one device all-reduce, one host read)."""
+    red = getattr(f, "reduce_dev", None)
     if red is None:
         return rms(x).item()
     x = x.detach().double()
-    return math.sqrt(red(float((x * x).sum())) / red(float(x.numel())))
+    return math.sqrt(float(red((x * x).sum().reshape(1)).item()) / f.global_count(x.numel()))
 
 
 @dataclass
@@ -157,7 +158,11 @@ def _step_fused(f, u, p, t, dt, k1, opt: Tsit5Options):
             ks.append(k7)
         else:
             ks.append(f.stage(u, p, ks, c)[0])
-    eest = math.sqrt(sumsq.item() / u.numel()) if sumsq is not None else None
+    eest = None
+    if sumsq is not None:
+        red = getattr(f, "reduce_dev", None)      # a grid-sharded RHS: Σ over the shards on the device
+        eest = (math.sqrt(float(red(sumsq).item()) / f.global_count(u.numel())) if red is not None
+                else math.sqrt(sumsq.item() / u.numel()))
     return unew, ks, eest
 
 

@@ -21,7 +21,9 @@ two 10·B-value collectives per adjoint stage and no layer-2 forward.  Every
 parameter gradient is therefore shard-local: d(Σ_r L_r)/dp_r lands on the rank owning p_r,
 and no gradient all-reduce is needed across the grid shards (a data-parallel group over
 trajectories, if any, still all-reduces its gradients in Trainer).  The adaptive step
-control's error norm is the one global reduction of the integrator (`reduce_sum`).
+control's error norm is the one global reduction of the integrator: each shard's error terms stay on
+the device and are all-reduced once per step (`reduce_dev`), read by the host once (the accept/reject
+decision), so an adjoint step makes one host synchronisation.
 """
 from __future__ import annotations
 
@@ -107,6 +109,7 @@ class GridShardedChainRHS:
             layer_fn = lambda l, pl, x: layer_apply(self._hd, l, pl, x)   # noqa: E731
         self.layer_fn = layer_fn
         self.backend = dist.get_backend(self.group) if self.group is not None else None
+        self._counts = {}
 
     # -- collectives ---------------------------------------------------------------
     def _allreduce(self, x: torch.Tensor) -> torch.Tensor:
@@ -120,7 +123,7 @@ class GridShardedChainRHS:
         return x
 
     def reduce_sum(self, v: float) -> float:
-        """Σ over the grid shards (the integrator's global error norm)."""
+        """Σ over the grid shards of a host scalar (once-per-solve quantities)."""
         if self.world == 1:
             return float(v)
         t = torch.tensor([float(v)], dtype=torch.float64)
@@ -128,6 +131,18 @@ class GridShardedChainRHS:
             t = t.cuda()
         dist.all_reduce(t, group=self.group)
         return float(t.item())
+
+    def reduce_dev(self, t: torch.Tensor) -> torch.Tensor:
+        """Σ over the grid shards of a small device tensor, without reading it on the host (the
+        integrators' per-step error norms: the caller's one .item() is the step's only host sync)."""
+        return self._allreduce(t.contiguous())
+
+    def global_count(self, n: int) -> float:
+        """Σ over the shards of a per-shard entry count (cached: the shard sizes are fixed)."""
+        c = self._counts.get(n)
+        if c is None:
+            c = self._counts[n] = self.reduce_sum(float(n))
+        return c
 
     # -- parameters -------------------------------------------------------------------
     def shard_params(self, p_full: torch.Tensor) -> torch.Tensor:
@@ -145,6 +160,40 @@ class GridShardedChainRHS:
         h = _AllReduceSum.apply(hpart, self._allreduce)           # one [H, B] all-reduce per RHS
         return self.layer_fn(1, p[self.P1:], h)                   # (B, n_r): own rows of du
 
+    @staticmethod
+    def _error_sumsq(base, y, ks, out, error) -> None:
+        """The embedded-error terms of kanode_stage on this shard, on the device:
+        sumsq <- Σ (e / (abstol + reltol·max(|base|, |y|)))², e = Σ ec_j k_j + ec_n out."""
+        ec, abstol, reltol, sumsq = error
+        e = torch.zeros_like(out)
+        for ej, kj in zip(ec[:-1], ks):
+            e = e + ej * kj
+        e = e + ec[-1] * out
+        sk = abstol + reltol * torch.maximum(base.abs(), y.abs())
+        sumsq.copy_(((e / sk).double() ** 2).sum().reshape(sumsq.shape))
+
+    def stage(self, u, p, ks, c, want_y=False, error=None):
+        """Fused Runge-Kutta stage (kanode/ode.py _step_fused; the statement of kanode_rhs_stage) on the
+        grid shard: y = u + Σ c_j k_j formed inside the first layer's kernel (kanode_layer_forward_stage),
+        one [H, B] all-reduce, the second layer on the own rows; `error` receives this shard's Σ (e/sk)²
+        on the device (the integrator all-reduces it with reduce_dev).  Returns (du, y).  Under autograd
+        (the discrete adjoint) the combination is composed of differentiable torch ops instead."""
+        recording = torch.is_grad_enabled() and (p.requires_grad or u.requires_grad or any(k.requires_grad for k in ks))
+        if recording or not hasattr(self, "_hd"):
+            y = u
+            for cj, kj in zip(c, ks):
+                y = torch.addcmul(y, kj, torch.full_like(kj, cj))
+            du = self(y, p)
+        else:
+            y = torch.empty_like(u)
+            hpart = self._hd.layer_forward_stage(0, p[:self.P1].contiguous(), u.contiguous(),
+                                                 [k.contiguous() for k in ks], c, y_out=y)
+            du = self._hd.layer_forward(1, p[self.P1:].contiguous(), self._allreduce(hpart))
+        if error is not None:
+            with torch.no_grad():
+                self._error_sumsq(u, y, ks, du, error)
+        return du, y
+
     def _layer_vjp(self, l: int, pl: torch.Tensor, x: torch.Tensor, g: torch.Tensor):
         """(x̄, p̄_l) of one layer: kanode_layer_vjp on the default handle; through autograd on the
         layer_fn override otherwise."""
@@ -158,29 +207,33 @@ class GridShardedChainRHS:
 
     def vjp_stage(self, u, p, ks, c, lam, lks, lc, lam_out=None, error=None):
         """InterpolatingAdjoint stage on the grid shard (kanode/adjoint.py; the statement of
-        kanode_vjp_stage): y = u + Σ c_j k_j, λs = λ + Σ lc_j lk_j (both local slices), returns this
-        rank's λsᵀ∂f/∂u rows and its parameters' λsᵀ∂f/∂p.  `error` receives this shard's Σ (e/sk)²;
-        the adjoint driver sums it over the shards (reduce_sum) with the μ part."""
-        y = u
-        for cj, kj in zip(c, ks):
-            y = torch.addcmul(y, kj, torch.full_like(kj, cj))
-        ls = lam
-        for cj, kj in zip(lc, lks):
-            ls = torch.addcmul(ls, kj, torch.full_like(kj, cj))
-        p1, p2 = p[:self.P1], p[self.P1:]
-        with torch.no_grad():
-            h = self._allreduce(self.layer_fn(0, p1, y).contiguous())            # forward to the hidden layer
+        kanode_vjp_stage): y = u + Σ c_j k_j, λs = lam + Σ lc_j lk_j (both local slices, formed inside
+        the first layer's forward kernel, kanode_layer_forward_stage), returns this rank's λsᵀ∂f/∂u rows
+        and its parameters' λsᵀ∂f/∂p.  `error` receives this shard's Σ (e/sk)² on the device; the
+        adjoint driver adds the μ part and all-reduces once per step (reduce_dev).  No host sync here."""
+        p1, p2 = p[:self.P1].contiguous(), p[self.P1:].contiguous()
+        if hasattr(self, "_hd"):
+            y = torch.empty_like(u)
+            ls = lam_out if lam_out is not None else torch.empty_like(lam)
+            hpart = self._hd.layer_forward_stage(0, p1, u.contiguous(), [k.contiguous() for k in ks], c, y_out=y,
+                                                 lam=lam.contiguous(), lks=[k.contiguous() for k in lks], lc=lc,
+                                                 ls_out=ls)
+            h = self._allreduce(hpart)                                            # forward to the hidden layer
+        else:
+            y = u
+            for cj, kj in zip(c, ks):
+                y = torch.addcmul(y, kj, torch.full_like(kj, cj))
+            ls = lam
+            for cj, kj in zip(lc, lks):
+                ls = torch.addcmul(ls, kj, torch.full_like(kj, cj))
+            with torch.no_grad():
+                h = self._allreduce(self.layer_fn(0, p1, y).contiguous())
+            if lam_out is not None:
+                lam_out.copy_(ls)
         hbar, dp2 = self._layer_vjp(1, p2, h, ls)
         hbar = self._allreduce(hbar.contiguous())                                 # Σ over the output shards
         lamJ, dp1 = self._layer_vjp(0, p1, y, hbar)
-        if lam_out is not None:
-            lam_out.copy_(ls)
         if error is not None:
-            ec, abstol, reltol, sumsq = error
-            e = torch.zeros_like(lam)
-            for ej, kj in zip(ec[:-1], lks):
-                e = e + ej * kj
-            e = e + ec[-1] * lamJ
-            sk = abstol + reltol * torch.maximum(lam.abs(), ls.abs())
-            sumsq.fill_(float(((e / sk).double() ** 2).sum()))
+            with torch.no_grad():
+                self._error_sumsq(lam, ls, lks, lamJ, error)
         return lamJ, torch.cat([dp1.reshape(-1), dp2.reshape(-1)])

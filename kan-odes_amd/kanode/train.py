@@ -7,10 +7,12 @@
                   mean folded in; what Trainer uses on the GPU
     mse_loss    — `mean(abs2, X .- pred)` (LV_driver_KANODE.jl:197-203, Fisher-KPP_Source.jl:107-109)
     reg_loss    — L1 + entropy on the flat p (LV_driver_KANODE.jl:187-194)
-    Trainer     — one iteration = forward Tsit5 solve, loss, discrete adjoint
-                  (the HIP VJP per stage), ONE all-reduce of [∂L/∂p ; L] across the
-                  trajectory shards (RCCL over xGMI with backend "nccl"; gloo on CPU),
-                  then the identical Adam step on every rank.
+    Trainer     — one iteration = forward Tsit5 solve, loss, the gradient by the
+                  InterpolatingAdjoint (the reference's NeuralODE default sensealg; native
+                  kanode_adjoint_tsit5 on the GPU) wherever the RHS provides the adjoint stage,
+                  else the discrete adjoint (reverse mode through the stages), ONE all-reduce
+                  of [∂L/∂p ; L] across the trajectory shards (RCCL over xGMI with backend
+                  "nccl"; gloo on CPU), then the identical Adam step on every rank.
 """
 from __future__ import annotations
 
@@ -21,30 +23,40 @@ from .ode import Solution, Tsit5Options, solve
 
 class Adam:
     """Flux.Optimise.Adam (legacy API):  mt = β1 mt + (1-β1) Δ;  vt = β2 vt + (1-β2) Δ²;
-    Δ = mt / (1-β1^t) / (√(vt / (1-β2^t)) + ϵ) · η;  x .-= Δ."""
+    Δ = mt / (1-β1^t) / (√(vt / (1-β2^t)) + ϵ) · η;  x .-= Δ.
+
+    Flux evaluates these broadcasts with its Float64 hyper-parameters, so Float32 x, mt, vt are
+    promoted, computed in Float64 and rounded on store.  This torch statement does the same, in the
+    operation order of the fused kernel (kan_optim.hip: every product and sum rounded separately), so
+    the CPU and GPU trainers take the same optimiser trajectory for either dtype."""
 
     def __init__(self, eta: float = 1e-3, beta=(0.9, 0.999), eps: float = 1e-8):
         self.eta, self.beta, self.eps = eta, beta, eps
         self.state = {}
 
     def apply(self, x: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+        """Advances the moments; returns the Float64 step Δ (x is not changed)."""
         b1, b2 = self.beta
         st = self.state.get(id(x))
         if st is None:
             st = [torch.zeros_like(x), torch.zeros_like(x), [b1, b2]]
             self.state[id(x)] = st
         mt, vt, bp = st
-        mt.mul_(b1).add_(d, alpha=1 - b1)
-        vt.mul_(b2).addcmul_(d, d, value=1 - b2)
-        step = mt / (1 - bp[0]) / (torch.sqrt(vt / (1 - bp[1])) + self.eps) * self.eta
+        d64 = d.double()
+        m64 = b1 * mt.double() + (1.0 - b1) * d64
+        v64 = b2 * vt.double() + ((1.0 - b2) * d64) * d64
+        mt.copy_(m64)                                   # the stored moments (rounded for Float32)
+        vt.copy_(v64)
+        den = torch.sqrt(vt.double() / (1.0 - bp[1])) + self.eps
+        step = (mt.double() / (1.0 - bp[0])) / den * self.eta
         bp[0] *= b1
         bp[1] *= b2
         return step
 
     def update(self, x: torch.Tensor, d: torch.Tensor) -> None:
-        """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ)."""
+        """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ) (the subtraction in Float64, rounded on store)."""
         with torch.no_grad():
-            x.sub_(self.apply(x, d))
+            x.copy_(x.double() - self.apply(x, d))
 
 
 class FusedAdam(Adam):
@@ -142,7 +154,7 @@ class Trainer:
         p = self.p.detach().requires_grad_(True)
         sol = self.predict(p)
         if self.tp:   # Σ over the grid shards of these partial sums = the global mean
-            loss = torch.sum((self.target - sol.u) ** 2) / self.rhs.reduce_sum(float(sol.u.numel()))
+            loss = torch.sum((self.target - sol.u) ** 2) / self.rhs.global_count(sol.u.numel())
         else:
             loss = mse_loss(sol.u, self.target)
         if self.sparse_reg:

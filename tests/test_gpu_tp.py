@@ -1,5 +1,5 @@
 """Grid-sharded Burgers surrogate (BASELINE configs[3]: KAN [512, 10, 512], G = 5, softsign)
-on the HIP layers: two ranks share cuda:0 and exchange the hidden partials through gloo
+on the HIP layers: two or four ranks (BASELINE's "grid sharded 4x") share cuda:0 and exchange the hidden partials through gloo
 (host-staged; backend "nccl" = RCCL is the same call on a multi-GPU node), against the
 unsharded HIP chain and the CPU oracle."""
 import os
@@ -67,19 +67,27 @@ def _worker(rank, world, port, q):
         (g,) = torch.autograd.grad((sol.u * torch.as_tensor(w[:, :, a:b].copy(), device=dev)).sum(), [plr])
         out.update(sol=sol.u.detach().cpu().numpy(), naccept=sol.stats["naccept"],
                    grad=tp.gather_params(g).cpu().numpy())
-        # InterpolatingAdjoint at fixed steps (vjp_stage: kanode_layer_forward, two hidden all-reduces,
-        # kanode_layer_vjp x 2 per adjoint stage)
+        # InterpolatingAdjoint at fixed steps (vjp_stage: kanode_layer_forward_stage forming y and λs,
+        # two hidden all-reduces, kanode_layer_vjp x 2 per adjoint stage)
         plf = pl.clone().requires_grad_(True)
         solf = kanode.solve(tp, u, (0.0, 0.1), plf, TS, kanode.Tsit5Options(adaptive=False, dt=0.005),
                             sensealg="interpolating_adjoint")
         (gf,) = torch.autograd.grad((solf.u * torch.as_tensor(w[:, :, a:b].copy(), device=dev)).sum(), [plf])
         out.update(grad_ia=tp.gather_params(gf).cpu().numpy(), stats_ia=dict(solf.stats))
+        # adaptive InterpolatingAdjoint: the per-step error terms reduced on the device (reduce_dev)
+        pla = pl.clone().requires_grad_(True)
+        sola = kanode.solve(tp, u, (0.0, 0.1), pla, TS, kanode.Tsit5Options(abstol=1e-8, reltol=1e-8),
+                            sensealg="interpolating_adjoint")
+        (ga,) = torch.autograd.grad((sola.u * torch.as_tensor(w[:, :, a:b].copy(), device=dev)).sum(), [pla])
+        out.update(sol_a=sola.u.detach().cpu().numpy(), grad_a=tp.gather_params(ga).cpu().numpy(),
+                   stats_a=dict(sola.stats))
         q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-def test_grid_sharded_burgers_on_hip_layers():
+@pytest.mark.parametrize("world", [2, 4])
+def test_grid_sharded_burgers_on_hip_layers(world):
     dev = device()
     u0, p, w = _problem()
     c1, c2 = _cfgs()
@@ -95,7 +103,10 @@ def test_grid_sharded_burgers_on_hip_layers():
     solf = kanode.solve(full, t(u0), (0.0, 0.1), pf, TS, kanode.Tsit5Options(adaptive=False, dt=0.005),
                         sensealg="interpolating_adjoint")
     (gf,) = torch.autograd.grad((solf.u * t(w)).sum(), [pf])
-    world = 2
+    pa = t(p).requires_grad_(True)
+    sola = kanode.solve(full, t(u0), (0.0, 0.1), pa, TS, kanode.Tsit5Options(abstol=1e-8, reltol=1e-8),
+                        sensealg="interpolating_adjoint")
+    (ga,) = torch.autograd.grad((sola.u * t(w)).sum(), [pa])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -119,3 +130,9 @@ def test_grid_sharded_burgers_on_hip_layers():
         assert r["stats_ia"]["adjoint"]["naccept"] == solf.stats["adjoint"]["naccept"]
         gfn = gf.cpu().numpy()
         assert np.max(np.abs(r["grad_ia"] - gfn)) <= 1e-10 * np.abs(gfn).max()
+        # adaptive: the sharded forward (fused stages) and adjoint take the unsharded native solve's steps
+        assert r["stats_a"]["naccept"] == sola.stats["naccept"]
+        assert r["stats_a"]["adjoint"]["naccept"] == sola.stats["adjoint"]["naccept"]
+        assert np.max(np.abs(r["sol_a"] - sola.u.detach().cpu().numpy()[:, :, a:b])) <= 1e-10
+        gan = ga.cpu().numpy()
+        assert np.max(np.abs(r["grad_a"] - gan)) <= 1e-8 * np.abs(gan).max()

@@ -66,6 +66,12 @@ def test_fused_adam_fp32_promotes_like_flux():
         opt.update(x, t(g, torch.float32))
     got = x.cpu().numpy()
     assert np.max(np.abs(got.astype(np.float64) - ref) / np.abs(ref)) <= 1.2e-7     # one float32 ulp
+    # the CPU trainer's kanode.Adam promotes the same way: the same Float32 trajectory
+    xc = torch.as_tensor(x0.copy())
+    slow = kanode.Adam(1e-3)
+    for g in grads:
+        slow.update(xc, torch.as_tensor(g))
+    assert np.max(np.abs(got.astype(np.float64) - xc.numpy().astype(np.float64)) / np.abs(ref)) <= 1.2e-7
 
 
 def test_fused_adam_rejects_bad_arguments():

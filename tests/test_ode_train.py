@@ -76,6 +76,31 @@ def test_adam_matches_flux_formula():
     assert np.allclose(xs.numpy(), xr, rtol=0, atol=1e-15)
 
 
+def test_adam_float32_promotes_like_flux():
+    """Float32 parameters take Flux's Float64-promoted step (rounded on store), the statement
+    kanode_adam_step runs on the GPU, so CPU and GPU trainers follow one optimiser trajectory."""
+    rng = np.random.default_rng(3)
+    x0 = rng.normal(size=240).astype(np.float32)
+    grads = [rng.normal(size=240).astype(np.float32) for _ in range(5)]
+    x = torch.as_tensor(x0.copy())
+    opt = kanode.Adam(1e-3)
+    m = np.zeros(240, np.float32)
+    v = np.zeros(240, np.float32)
+    xr = x0.copy()
+    b1, b2, bp1, bp2 = 0.9, 0.999, 0.9, 0.999
+    for g in grads:
+        opt.update(x, torch.as_tensor(g))
+        d = g.astype(np.float64)
+        m = (b1 * m.astype(np.float64) + (1 - b1) * d).astype(np.float32)
+        v = (b2 * v.astype(np.float64) + ((1 - b2) * d) * d).astype(np.float32)
+        step = m.astype(np.float64) / (1 - bp1) / (np.sqrt(v.astype(np.float64) / (1 - bp2)) + 1e-8) * 1e-3
+        xr = (xr.astype(np.float64) - step).astype(np.float32)
+        bp1 *= b1
+        bp2 *= b2
+    assert x.dtype == torch.float32
+    assert np.array_equal(x.numpy(), xr)
+
+
 def test_trainer_reduces_loss_on_lv():
     """Fit the LV parameters themselves with the Trainer (torch RHS on CPU)."""
     ptrue = torch.tensor([1.5, 1.0, 1.0, 3.0], dtype=torch.float64)
