@@ -291,8 +291,8 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     u0 = [1, 1], tspan (0, 3.5), saveat 0:0.1:3.4, adaptive Tsit5 at the default tolerances,
     InterpolatingAdjoint, Adam; LV_driver_KANODE.jl:119-122,139-143,175-219).  On the GPU a
     single trajectory runs the forward solve and the adjoint as one workgroup each
-    (kd_chain_tsit5_kernel, kd_chain_adjoint_kernel).  CPU: the oracle chain driven by the same
-    integrator statement in Python (kind "port"); Julia is not available to time the reference."""
+    (kd_chain_tsit5_kernel, kd_chain_adjoint_kernel).  CPU: the same iteration in C on one core over the
+    oracle chain (oracle/cpu_epoch.c, kind "port"); Julia is not available to time the reference."""
     from scipy.integrate import solve_ivp
     ts = [0.1 * i for i in range(35)]
     ts_test = [0.1 * i for i in range(141)]
@@ -302,41 +302,49 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     target = full[:35]
     chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
     p0 = chain.setup(np.random.default_rng(0))[0].astype(np.float64) / 1e5 * 1e4   # a mid-training scale
-    legs = [("gpu", dev, kanode.ChainRHS(chain, device=dev), reps)]
-    if with_cpu:
-        from oracle import oracle as O
-        from oracle.oracle_rhs import OracleChainRHS
-        legs.append(("cpu", "cpu", OracleChainRHS([O.LayerSpec(2, 10, 5, "tanh_fast"),
-                                                   O.LayerSpec(10, 2, 5, "tanh_fast")]), 2))
     out = {"unit": "ms/iteration", "batch": 1, "dtype": "f64",
            "what": "one LV_driver_KANODE.jl iteration (:283-291): adaptive Tsit5 solve + InterpolatingAdjoint "
                    "+ Adam, then the loss_train (tspan_train, 35 saveat) and loss_test (tspan (0, 14), 141 "
                    "saveat) forward solves, LV KAN [2,10,2] G=5, one trajectory"}
-    for name, d, rhs, n in legs:
-        u0 = torch.tensor([[1.0, 1.0]], dtype=torch.float64, device=d)
-        tr = kanode.Trainer(rhs, u0, (0.0, 3.5), ts, torch.as_tensor(target, device=d), torch.as_tensor(p0, device=d),
-                            eta=1e-3, sensealg="interpolating_adjoint")
-        tgt_test = torch.as_tensor(full, device=d)
+    rhs = kanode.ChainRHS(chain, device=dev)
+    u0 = torch.tensor([[1.0, 1.0]], dtype=torch.float64, device=dev)
+    tr = kanode.Trainer(rhs, u0, (0.0, 3.5), ts, torch.as_tensor(target, device=dev), torch.as_tensor(p0, device=dev),
+                        eta=1e-3, sensealg="interpolating_adjoint")
+    tgt_test = torch.as_tensor(full, device=dev)
 
-        def iteration():
-            tr.step()
-            with torch.no_grad():
-                l_tr = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 3.5), tr.p, ts).u, tr.target)
-                l_te = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 14.0), tr.p, ts_test).u, tgt_test)
-            return float(l_tr), float(l_te)
+    def iteration():
+        tr.step()
+        with torch.no_grad():
+            l_tr = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 3.5), tr.p, ts).u, tr.target)
+            l_te = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 14.0), tr.p, ts_test).u, tgt_test)
+        return float(l_tr), float(l_te)
 
+    iteration()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
         iteration()
-        if name == "gpu":
-            torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(n):
-            iteration()
-        if name == "gpu":
-            torch.cuda.synchronize()
-        out[name] = (time.perf_counter() - t0) / n * 1e3
+    torch.cuda.synchronize()
+    out["gpu"] = (time.perf_counter() - t0) / reps * 1e3
     if with_cpu:
-        out.update({"cpu_cores": 1, "cpu_kind": "port (oracle chain, numpy; Python Tsit5 + adjoint driver)",
-                    "speedup": out["cpu"] / out["gpu"]})
+        # the same iteration in C on one core (oracle/cpu_epoch.c: kref_chain_epoch_f64 + two kref_chain_solve_f64,
+        # pinned to the Python statement by tests/test_cpu_epoch.py); median of 20 after 3 warm-ups
+        from oracle import oracle as O
+        specs = [O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")]
+        u0c = np.array([[1.0, 1.0]])
+        pc = p0.copy()
+        times = []
+        for r in range(23):
+            t0 = time.perf_counter()
+            _, _, pc, _, _ = O.chain_epoch(specs, pc, u0c, 3.5, ts, target, eta=1e-3)
+            O.chain_solve(specs, pc, u0c, 3.5, ts)
+            O.chain_solve(specs, pc, u0c, 14.0, ts_test)
+            if r >= 3:
+                times.append(time.perf_counter() - t0)
+        out.update({"cpu": float(np.median(times)) * 1e3, "cpu_cores": 1,
+                    "cpu_kind": "port (oracle/cpu_epoch.c: C Tsit5 + InterpolatingAdjoint + Adam over the oracle "
+                                "chain, plus the two loss solves, one core; median of 20 after 3 warm-ups)",
+                    "speedup": float(np.median(times)) * 1e3 / out["gpu"]})
     return out
 
 

@@ -1,6 +1,6 @@
 /*
- * cpu_epoch.c — CPU BASELINE of one Fisher-KPP training epoch (test infrastructure only; called
- * only by bench.py's epoch legs and tests/test_cpu_epoch.py).
+ * cpu_epoch.c — CPU BASELINE of one KAN-ODE training epoch (test infrastructure only; called
+ * only by bench.py's epoch / lv1_train legs and tests/test_cpu_epoch.py).
  *
  * One iteration of the reference's training loop (PDE examples/Fisher-KPP_Source.jl:101-109,
  * 195-201): predict(p) = solve(ODEProblem(rc_kanode, u0, (0, T), p), Tsit5(); saveat), the MSE loss,
@@ -14,7 +14,10 @@
  *   Hairer-Wanner initial step, PI controller (beta1 7/50, beta2 2/25, gamma 9/10, qmin 1/5, qmax 10,
  *   qoldinit 1e-4), RMS error norm over the whole state ([λ; μ] in the adjoint), saveat from the
  *   free interpolant, λ jumps at the saveat times with FSAL re-evaluated.
- * u, targets: [Nx, B] column-major (trajectory contiguous); targets [n_save][Nx*B].
+ * The same epoch for a Lux.Chain NeuralODE RHS (kref_chain_epoch_f64; LV_driver_KANODE.jl:180-219,
+ * 279-287: dudt = Chain(u), its pullback by kref_chain_vjp_f64), and the forward solve alone
+ * (kref_chain_solve_f64: the driver's loss_train / loss_test solves, :290-291).
+ * u, targets: [N, B] column-major (trajectory contiguous); targets [n_save][N*B].
  */
 #include "kanode_ref.h"
 #include <math.h>
@@ -47,17 +50,25 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-typedef struct {
-    const kref_layer* L;
+typedef struct epoch_ctx epoch_ctx;
+struct epoch_ctx {
+    void (*rhs)(epoch_ctx* c, const double* u, double* du);
+    /* lamJ = (∂f/∂u)^T lam ; dp = Σ lam ∂f/∂p (overwritten) */
+    void (*vjp)(epoch_ctx* c, const double* u, const double* lam, double* lamJ, double* dp);
     const double* p;
-    int64_t Nx, B, n, P;
+    int64_t B, n, P;
+    /* Fisher-KPP */
+    const kref_layer* L;
+    int64_t Nx;
     double D, dx;
     double* A;      /* dense D*lap, column-major */
-    double* tmp;    /* [n] */
-    int64_t nf_fwd, nf_adj;
-} fk_ctx;
+    double* tmp;    /* [Nx] */
+    /* chain */
+    int32_t nl;
+    const kref_layer* Ls;
+};
 
-static void rhs(fk_ctx* c, const double* u, double* du) {
+static void fk_rhs(epoch_ctx* c, const double* u, double* du) {
     kref_fk_rhs_f64(c->L, c->p, 0.0, c->dx, c->Nx, u, c->B, du, 0);   /* kan1_.(u) (D = 0: no stencil) */
     for (int64_t b = 0; b < c->B; ++b) {                                /* + (D*lap) u, dense gemv 'N' */
         const double* ub = u + c->Nx * b;
@@ -70,11 +81,9 @@ static void rhs(fk_ctx* c, const double* u, double* du) {
         }
         for (int64_t i = 0; i < c->Nx; ++i) du[c->Nx * b + i] += db[i];
     }
-    c->nf_fwd++;
 }
 
-/* lamJ = (∂f/∂u)^T lam ; dp = Σ lam ∂f/∂p (overwritten) */
-static void vjp(fk_ctx* c, const double* u, const double* lam, double* lamJ, double* dp) {
+static void fk_vjp(epoch_ctx* c, const double* u, const double* lam, double* lamJ, double* dp) {
     memset(dp, 0, sizeof(double) * (size_t)c->P);
     kref_fk_vjp_f64(c->L, c->p, 0.0, c->dx, c->Nx, u, lam, c->B, lamJ, dp);
     for (int64_t b = 0; b < c->B; ++b) {                                /* + (D*lap)^T λ, dense gemv 'T' */
@@ -86,7 +95,14 @@ static void vjp(fk_ctx* c, const double* u, const double* lam, double* lamJ, dou
             lamJ[c->Nx * b + j] += s;
         }
     }
-    c->nf_adj++;
+}
+
+/* NeuralODE dudt(u, p, t) = first(Chain(u, p, st)) (LV_driver_KANODE.jl:180) and its Zygote pullback */
+static void chain_rhs(epoch_ctx* c, const double* u, double* du) { kref_chain_fwd_f64(c->nl, c->Ls, c->p, u, c->B, du); }
+
+static void chain_vjp(epoch_ctx* c, const double* u, const double* lam, double* lamJ, double* dp) {
+    memset(dp, 0, sizeof(double) * (size_t)c->P);
+    kref_chain_vjp_f64(c->nl, c->Ls, c->p, u, lam, c->B, lamJ, dp);
 }
 
 static void interp_w(double th, double* w) {
@@ -146,44 +162,30 @@ static double sumsq_scaled(const double* x, const double* sk, int64_t n) {
     return s;
 }
 
-/* One epoch.  Returns 0 on success; loss, grad[P] (dL/dp) and the stats out. */
-int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0, int64_t B,
-                      double T, const double* saveat, int32_t n_save, const double* target, double abstol,
-                      double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
-                      int64_t* stats /* [4]: fwd accept, fwd reject, adj accept, adj reject */, double* seconds) {
-    const double t_start = now_s();
-    fk_ctx c = {L, p, Nx, B, Nx * B, kref_layer_param_length(L), D, dx, NULL, NULL, 0, 0};
-    const int64_t n = c.n, P = c.P;
-    c.A = calloc((size_t)(Nx * Nx), sizeof(double));
-    c.tmp = malloc(sizeof(double) * Nx);
-    const double dx2 = dx * dx, cd = D * (-2.0 / dx2), co = D * (1.0 / dx2);
-    for (int64_t i = 0; i < Nx; ++i) {
-        c.A[i + Nx * i] = cd;
-        if (i + 1 < Nx) { c.A[i + Nx * (i + 1)] = co; c.A[(i + 1) + Nx * i] = co; }
-    }
-    c.A[0 + Nx * (Nx - 1)] = co;
-    c.A[(Nx - 1) + Nx * 0] = co;
-    double* buf = malloc(sizeof(double) * n * 24);
+/* The forward solve: solve(prob, Tsit5(); saveat) from t = 0 to T, pred[n_save][n]; the dense output kept
+ * in rec when rec != NULL.  Returns 0, or -1 when out of memory. */
+static int forward(epoch_ctx* c, const double* u0, double T, const double* saveat, int32_t n_save, double abstol,
+                   double reltol, int32_t adaptive, double dt_fixed, double* pred, dense_rec* rec, int64_t* nacc_out,
+                   int64_t* nrej_out) {
+    const int64_t n = c->n;
+    double* buf = malloc(sizeof(double) * n * 12);
+    if (!buf) return -1;
     double *u = buf, *unew = buf + n, *y = buf + 2 * n, *sk = buf + 3 * n, *e = buf + 4 * n;
     double* ks[7];
     for (int i = 0; i < 7; ++i) ks[i] = buf + (5 + i) * n;
-    double* pred = malloc(sizeof(double) * n * n_save);
-    dense_rec rec = {0, 0, NULL, NULL, NULL, NULL};
     const double beta1 = 7.0 / 50.0, beta2 = 2.0 / 25.0, gamma = 0.9, qmin = 0.2, qmax = 10.0, qoldinit = 1e-4;
-
-    /* ---- forward: solve(prob, Tsit5(); saveat) with the dense output kept ---- */
     memcpy(u, u0, sizeof(double) * n);
     int32_t si = 0;
     while (si < n_save && saveat[si] <= 1e-14) { memcpy(pred + si * n, u0, sizeof(double) * n); ++si; }
     double t = 0.0, dt;
-    rhs(&c, u, ks[0]);
+    c->rhs(c, u, ks[0]);
     if (adaptive) {   /* _initdt */
         for (int64_t i = 0; i < n; ++i) sk[i] = abstol + fabs(u[i]) * reltol;
         const double d0 = sqrt(sumsq_scaled(u, sk, n) / n), d1 = sqrt(sumsq_scaled(ks[0], sk, n) / n);
         double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         if (dt0 > T) dt0 = T;
         for (int64_t i = 0; i < n; ++i) y[i] = u[i] + dt0 * ks[0][i];
-        rhs(&c, y, ks[1]);
+        c->rhs(c, y, ks[1]);
         for (int64_t i = 0; i < n; ++i) e[i] = ks[1][i] - ks[0][i];
         const double d2 = sqrt(sumsq_scaled(e, sk, n) / n) / dt0;
         const double mx = d1 > d2 ? d1 : d2;
@@ -203,7 +205,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
                 y[i] = acc;
             }
             if (s == 5) memcpy(unew, y, sizeof(double) * n);
-            rhs(&c, y, ks[s + 1]);
+            c->rhs(c, y, ks[s + 1]);
         }
         double dtnew = dt;
         if (adaptive) {
@@ -237,13 +239,35 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
             }
             ++si;
         }
-        if (rec_add(&rec, n, t, dt, u, ks)) return -1;
+        if (rec && rec_add(rec, n, t, dt, u, ks)) { free(buf); return -1; }
         t = tn;
         memcpy(u, unew, sizeof(double) * n);
         memcpy(ks[0], ks[6], sizeof(double) * n);
         ++nacc;
         dt = dtnew;
+        if (nacc + nrej > 100000) { free(buf); return -3; }   /* maxiters */
     }
+    *nacc_out = nacc;
+    *nrej_out = nrej;
+    free(buf);
+    return 0;
+}
+
+/* One epoch on the context's RHS.  Returns 0 on success; loss, grad[P] (dL/dp) and the stats out. */
+static int run_epoch(epoch_ctx* cp, double* p, const double* u0, double T, const double* saveat, int32_t n_save,
+                     const double* target, double abstol, double reltol, int32_t adaptive, double dt_fixed, double eta,
+                     double* loss_out, double* grad, int64_t* stats) {
+    epoch_ctx c = *cp;
+    const int64_t n = c.n, P = c.P;
+    const double beta1 = 7.0 / 50.0, beta2 = 2.0 / 25.0, gamma = 0.9, qmin = 0.2, qmax = 10.0, qoldinit = 1e-4;
+    if (n_save > 64) return -2;
+    double* buf = malloc(sizeof(double) * n * 24);
+    double* pred = malloc(sizeof(double) * n * n_save);
+    dense_rec rec = {0, 0, NULL, NULL, NULL, NULL};
+    int64_t nacc = 0, nrej = 0;
+    int rc = forward(&c, u0, T, saveat, n_save, abstol, reltol, adaptive, dt_fixed, pred, &rec, &nacc, &nrej);
+    if (rc) return rc;
+    double *y = buf + 2 * n, *sk = buf + 3 * n, *e = buf + 4 * n;
     /* ---- loss = mean(abs2, target - pred); ∂L/∂u(t_j) = -2 (target - pred) / numel ---- */
     const double numel = (double)n * n_save;
     double loss = 0.0;
@@ -266,7 +290,6 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
     double* skm = malloc(sizeof(double) * P);
     memset(lam, 0, sizeof(double) * n);
     int32_t used[64] = {0};
-    if (n_save > 64) return -2;
     const double eps = 1e-12 * fmax(1.0, fabs(T));
     for (int32_t j = 0; j < n_save; ++j)
         if (fabs(saveat[j] - T) <= 0.0 && !used[j]) {   /* the jump at tf sets the initial λ */
@@ -283,7 +306,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
     stops[nst++] = T;
     double tau = 0.0, h;
     rec_eval(&rec, n, T - 0.0, y);
-    vjp(&c, y, lam, kl[0], km);
+    c.vjp(&c, y, lam, kl[0], km);
     const double ntot = (double)(n + P);
     if (adaptive) {
         for (int64_t i = 0; i < n; ++i) sk[i] = abstol + fabs(lam[i]) * reltol;
@@ -294,7 +317,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
         if (h0 > T) h0 = T;
         for (int64_t i = 0; i < n; ++i) ls[i] = lam[i] + h0 * kl[0][i];
         rec_eval(&rec, n, T - h0, y);
-        vjp(&c, y, ls, kl[1], km + P);
+        c.vjp(&c, y, ls, kl[1], km + P);
         for (int64_t i = 0; i < n; ++i) e[i] = kl[1][i] - kl[0][i];
         for (int64_t q = 0; q < P; ++q) emu[q] = km[P + q] - km[q];
         const double d2 = sqrt((sumsq_scaled(e, sk, n) + sumsq_scaled(emu, skm, P)) / ntot) / h0;
@@ -304,7 +327,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
     } else {
         h = dt_fixed;
     }
-    qold = qoldinit;
+    double qold = qoldinit;
     int32_t sti = 0;
     int64_t aacc = 0, arej = 0;
     while (tau < T - 1e-14 * fmax(1.0, T)) {
@@ -317,7 +340,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
             }
             if (s == 5) memcpy(lnew, ls, sizeof(double) * n);
             rec_eval(&rec, n, T - (tau + TC[s] * h), y);
-            vjp(&c, y, ls, kl[s + 1], km + (s + 1) * P);
+            c.vjp(&c, y, ls, kl[s + 1], km + (s + 1) * P);
         }
         for (int64_t q = 0; q < P; ++q) {
             double acc = 0.0;
@@ -362,7 +385,7 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
                         used[j] = 1;
                     }
                 rec_eval(&rec, n, T - tau, y);           /* u_modified!: FSAL re-evaluated */
-                vjp(&c, y, lam, kl[0], km);
+                c.vjp(&c, y, lam, kl[0], km);
             }
             sti = sti + 1 < nst ? sti + 1 : nst - 1;
         }
@@ -377,8 +400,78 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
     }
     *loss_out = loss;
     stats[0] = nacc; stats[1] = nrej; stats[2] = aacc; stats[3] = arej;
-    free(c.A); free(c.tmp); free(buf); free(pred); free(g); free(km); free(mu); free(munew); free(emu); free(skm);
+    free(buf); free(pred); free(g); free(km); free(mu); free(munew); free(emu); free(skm);
     free(rec.t); free(rec.dt); free(rec.u); free(rec.k);
-    *seconds = now_s() - t_start;
     return 0;
+}
+
+int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0, int64_t B,
+                      double T, const double* saveat, int32_t n_save, const double* target, double abstol,
+                      double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
+                      int64_t* stats /* [4]: fwd accept, fwd reject, adj accept, adj reject */, double* seconds) {
+    const double t_start = now_s();
+    epoch_ctx c = {0};
+    c.rhs = fk_rhs;
+    c.vjp = fk_vjp;
+    c.p = p;
+    c.B = B;
+    c.n = Nx * B;
+    c.P = kref_layer_param_length(L);
+    c.L = L;
+    c.Nx = Nx;
+    c.D = D;
+    c.dx = dx;
+    c.A = calloc((size_t)(Nx * Nx), sizeof(double));
+    c.tmp = malloc(sizeof(double) * Nx);
+    const double dx2 = dx * dx, cd = D * (-2.0 / dx2), co = D * (1.0 / dx2);
+    for (int64_t i = 0; i < Nx; ++i) {
+        c.A[i + Nx * i] = cd;
+        if (i + 1 < Nx) { c.A[i + Nx * (i + 1)] = co; c.A[(i + 1) + Nx * i] = co; }
+    }
+    c.A[0 + Nx * (Nx - 1)] = co;
+    c.A[(Nx - 1) + Nx * 0] = co;
+    const int rc = run_epoch(&c, p, u0, T, saveat, n_save, target, abstol, reltol, adaptive, dt_fixed, eta, loss_out,
+                             grad, stats);
+    free(c.A);
+    free(c.tmp);
+    *seconds = now_s() - t_start;
+    return rc;
+}
+
+static epoch_ctx chain_ctx(int32_t nl, const kref_layer* Ls, const double* p, int64_t B) {
+    epoch_ctx c = {0};
+    c.rhs = chain_rhs;
+    c.vjp = chain_vjp;
+    c.p = p;
+    c.B = B;
+    c.n = (int64_t)Ls[0].in_dims * B;
+    c.P = 0;
+    for (int32_t l = 0; l < nl; ++l) c.P += kref_layer_param_length(&Ls[l]);
+    c.nl = nl;
+    c.Ls = Ls;
+    return c;
+}
+
+int kref_chain_epoch_f64(int32_t nl, const kref_layer* Ls, double* p, const double* u0, int64_t B, double T,
+                         const double* saveat, int32_t n_save, const double* target, double abstol, double reltol,
+                         int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad, int64_t* stats,
+                         double* seconds) {
+    const double t_start = now_s();
+    if (nl < 1 || Ls[nl - 1].out_dims != Ls[0].in_dims) return -4;
+    epoch_ctx c = chain_ctx(nl, Ls, p, B);
+    const int rc = run_epoch(&c, p, u0, T, saveat, n_save, target, abstol, reltol, adaptive, dt_fixed, eta, loss_out,
+                             grad, stats);
+    *seconds = now_s() - t_start;
+    return rc;
+}
+
+int kref_chain_solve_f64(int32_t nl, const kref_layer* Ls, const double* p, const double* u0, int64_t B, double T,
+                         const double* saveat, int32_t n_save, double abstol, double reltol, double* pred,
+                         int64_t* stats /* [2] */, double* seconds) {
+    const double t_start = now_s();
+    if (nl < 1 || Ls[nl - 1].out_dims != Ls[0].in_dims) return -4;
+    epoch_ctx c = chain_ctx(nl, Ls, p, B);
+    const int rc = forward(&c, u0, T, saveat, n_save, abstol, reltol, 1, 0.0, pred, NULL, &stats[0], &stats[1]);
+    *seconds = now_s() - t_start;
+    return rc;
 }

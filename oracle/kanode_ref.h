@@ -97,6 +97,17 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
                       double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
                       int64_t* stats, double* seconds);
 
+/* The same epoch for a Lux.Chain NeuralODE RHS (LV_driver_KANODE.jl:180-219,279-287), u0 [N, B] with
+ * N = Ls[0].in_dims = Ls[nl-1].out_dims; and the forward solve alone from t = 0 to T at the adaptive
+ * tolerances (the driver's loss_train / loss_test solves, :290-291), pred [n_save][N, B], stats [2]. */
+int kref_chain_epoch_f64(int32_t nl, const kref_layer* Ls, double* p, const double* u0, int64_t B, double T,
+                         const double* saveat, int32_t n_save, const double* target, double abstol, double reltol,
+                         int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad, int64_t* stats,
+                         double* seconds);
+int kref_chain_solve_f64(int32_t nl, const kref_layer* Ls, const double* p, const double* u0, int64_t B, double T,
+                         const double* saveat, int32_t n_save, double abstol, double reltol, double* pred,
+                         int64_t* stats, double* seconds);
+
 /* per-edge activations (Activation_getter.jl:3-63): act [O, I, K] (o fastest) */
 void kref_edge_act_f64(const kref_layer* L, const double* p, const double* x, int64_t K, double* act);
 

@@ -103,6 +103,12 @@ def lib() -> C.CDLL:
         L.kref_fk_epoch_f64.argtypes = [LP, P, C.c_double, C.c_double, C.c_int64, P, C.c_int64, C.c_double, P,
                                         C.c_int32, P, C.c_double, C.c_double, C.c_int32, C.c_double, C.c_double,
                                         P, P, P, P]
+        L.kref_chain_epoch_f64.restype = C.c_int
+        L.kref_chain_epoch_f64.argtypes = [C.c_int32, LP, P, P, C.c_int64, C.c_double, P, C.c_int32, P, C.c_double,
+                                           C.c_double, C.c_int32, C.c_double, C.c_double, P, P, P, P]
+        L.kref_chain_solve_f64.restype = C.c_int
+        L.kref_chain_solve_f64.argtypes = [C.c_int32, LP, P, P, C.c_int64, C.c_double, P, C.c_int32, C.c_double,
+                                           C.c_double, P, P, P]
         _lib = L
     return _lib
 
@@ -256,6 +262,45 @@ def fk_epoch(spec: LayerSpec, p: np.ndarray, D: float, dx: float, u0: np.ndarray
         raise RuntimeError(f"kref_fk_epoch_f64 failed ({rc})")
     stats = dict(naccept=int(st[0]), nreject=int(st[1]), adjoint_naccept=int(st[2]), adjoint_nreject=int(st[3]))
     return loss.value, grad, pn, stats, secs.value
+
+
+def chain_epoch(specs, p: np.ndarray, u0: np.ndarray, T: float, saveat, target, abstol=1e-6, reltol=1e-3,
+                adaptive=True, dt=0.0, eta=5e-4):
+    """One NeuralODE (Lux.Chain RHS) training epoch in C on one core (oracle/cpu_epoch.c), the statement of
+    kanode.Trainer.step with the InterpolatingAdjoint.  u0 (B, N); target (n_save, B, N).
+    Returns (loss, grad, p_new, stats dict, seconds)."""
+    u0 = np.ascontiguousarray(u0, dtype=np.float64)
+    B, N = u0.shape
+    sv = np.ascontiguousarray(saveat, dtype=np.float64)
+    tg = np.ascontiguousarray(target, dtype=np.float64)
+    assert tg.shape == (sv.size, B, N)
+    pn = np.ascontiguousarray(p, dtype=np.float64).copy()
+    grad = np.zeros_like(pn)
+    loss, secs = C.c_double(), C.c_double()
+    st = np.zeros(4, np.int64)
+    rc = lib().kref_chain_epoch_f64(len(specs), _layers(specs), _ptr(pn), _ptr(u0), B, T, _ptr(sv), sv.size, _ptr(tg),
+                                    abstol, reltol, int(adaptive), dt, eta, C.byref(loss), _ptr(grad), _ptr(st),
+                                    C.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"kref_chain_epoch_f64 failed ({rc})")
+    stats = dict(naccept=int(st[0]), nreject=int(st[1]), adjoint_naccept=int(st[2]), adjoint_nreject=int(st[3]))
+    return loss.value, grad, pn, stats, secs.value
+
+
+def chain_solve(specs, p: np.ndarray, u0: np.ndarray, T: float, saveat, abstol=1e-6, reltol=1e-3):
+    """The adaptive forward solve alone (C, one core): (pred (n_save, B, N), stats, seconds)."""
+    u0 = np.ascontiguousarray(u0, dtype=np.float64)
+    B, N = u0.shape
+    sv = np.ascontiguousarray(saveat, dtype=np.float64)
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    pred = np.zeros((sv.size, B, N))
+    st = np.zeros(2, np.int64)
+    secs = C.c_double()
+    rc = lib().kref_chain_solve_f64(len(specs), _layers(specs), _ptr(p), _ptr(u0), B, T, _ptr(sv), sv.size, abstol,
+                                    reltol, _ptr(pred), _ptr(st), C.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"kref_chain_solve_f64 failed ({rc})")
+    return pred, dict(naccept=int(st[0]), nreject=int(st[1])), secs.value
 
 
 def omp_max_threads() -> int:

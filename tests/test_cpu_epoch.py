@@ -44,3 +44,37 @@ def test_c_epoch_matches_python_driver(adaptive):
     tr.step()
     assert np.max(np.abs(p_new - tr.p.numpy())) <= 1e-12 * np.max(np.abs(p0))
     assert secs > 0
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_c_chain_epoch_matches_python_driver(adaptive):
+    """The LV comparator (bench.py lv1_train's CPU leg): the C NeuralODE epoch over the oracle chain
+    (LV_driver_KANODE.jl:180-219,279-287) against Trainer + InterpolatingAdjoint over OracleChainRHS."""
+    from oracle.oracle_rhs import OracleChainRHS
+    specs = [O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")]
+    rng = np.random.default_rng(4)
+    P = 240                                    # LV [2, 10, 2] G = 5
+    p0 = rng.uniform(-0.3, 0.3, P)
+    u0 = np.array([[1.0, 1.0], [0.8, 1.3]])
+    saveat = [0.1 * i for i in range(8)]
+    T = 0.7
+    target = np.ascontiguousarray(np.broadcast_to(u0 * 1.05, (len(saveat), 2, 2)))
+    dt = 0.01
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8) if adaptive else kanode.Tsit5Options(adaptive=False, dt=dt)
+    loss, grad, p_new, st, secs = O.chain_epoch(specs, p0, u0, T, saveat, target, abstol=1e-8, reltol=1e-8,
+                                                adaptive=adaptive, dt=dt, eta=5e-4)
+    tr = kanode.Trainer(OracleChainRHS(specs), torch.as_tensor(u0), (0.0, T), saveat, torch.as_tensor(target),
+                        torch.as_tensor(p0), eta=5e-4, solver=opt, sensealg="interpolating_adjoint")
+    lt, gt, sol = tr.loss_and_grad()
+    assert st["naccept"] == sol.stats["naccept"] and st["nreject"] == sol.stats["nreject"]
+    assert st["adjoint_naccept"] == sol.stats["adjoint"]["naccept"]
+    assert abs(loss - lt.item()) <= 1e-12 * abs(loss)
+    assert np.max(np.abs(grad - gt.numpy())) <= 1e-10 * np.max(np.abs(gt.numpy()))
+    tr.step()
+    assert np.max(np.abs(p_new - tr.p.numpy())) <= 1e-12 * np.max(np.abs(p0))
+    # the forward solve alone (the driver's loss_train / loss_test solves)
+    pred, st2, _ = O.chain_solve(specs, p0, u0, T, saveat, abstol=1e-8, reltol=1e-8)
+    ref = kanode.solve(OracleChainRHS(specs), torch.as_tensor(u0), (0.0, T), torch.as_tensor(p0), saveat,
+                       kanode.Tsit5Options(abstol=1e-8, reltol=1e-8))
+    assert st2["naccept"] == ref.stats["naccept"]
+    assert np.max(np.abs(pred - ref.u.numpy())) <= 1e-12
