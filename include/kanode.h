@@ -167,6 +167,11 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     stage's second launch until the next stage is issued and run the two in one launch (the
  *     x̄ block of stage s forms stage s+1's input λs over its own chunk); 0 = two launches per
  *     stage.  Bitwise equal.
+ *   KANODE_OPT_PAIR_PERSIST (default 0): kanode_adjoint_tsit5 of such a chain (fp64, after a
+ *     host-loop forward solve) runs the whole InterpolatingAdjoint as ONE launch: the grid split
+ *     over workgroups of KANODE_OPT_PAIR_PERSIST_S points (default 8), two exchanges of the H·B
+ *     hidden partials between workgroups per adjoint stage, μ and its stage vectors resident in
+ *     LDS, the step control on the device.  Same algorithm; sums in another fixed order.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -179,7 +184,9 @@ typedef enum {
     KANODE_OPT_GRID_ADJ_STEP = 7,
     KANODE_OPT_ADJ_STEP_ROWS = 8,
     KANODE_OPT_PAIR_VJP = 9,
-    KANODE_OPT_PAIR_FUSE = 10
+    KANODE_OPT_PAIR_FUSE = 10,
+    KANODE_OPT_PAIR_PERSIST = 11,
+    KANODE_OPT_PAIR_PERSIST_S = 12
 } kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);

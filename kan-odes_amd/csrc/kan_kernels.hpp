@@ -310,6 +310,21 @@ struct ChainAdjointArgs {
     void* dp;               // [P] or null
     int64_t* out;           // naccept, nreject, nf, status (0 ok, 1 maxiters)
 };
+// The whole InterpolatingAdjoint of a surrogate pair KDense(N -> H) + KDense(H -> N) in ONE launch
+// (kd_pair_adjoint_kernel, kan_pair_adj.hip): the grid split over workgroups of S points, two exchanges
+// of H·B partials per adjoint stage.  c.rec is the device table of the forward solve's slot pointers
+// ([nsteps]; slot i = u_i, k_2..k_7, each n = N·B entries), c.k1_0 the first step's k_1.
+struct PairAdjArgs {
+    ChainAdjointArgs c;
+    double* xbuf;     // [2][nwg][256] exchange slots (write-through stores and loads)
+    unsigned* ctr;    // arrival counter; ctr[1]: abort word (the 16 bytes are zeroed before every launch)
+    unsigned* abrt;
+    int64_t P;        // parameters of the chain (the error norm's count)
+    int S;            // grid points per workgroup (0: 8)
+};
+int pair_adjoint_workgroups(const LayerConst* hl, int64_t B, int S);
+hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, const double* p, int64_t B,
+                                  PairAdjArgs pa, hipStream_t st);
 constexpr int kChainAdjointMaxSteps = 1024;   // forward steps held in LDS
 template <typename T>
 hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,

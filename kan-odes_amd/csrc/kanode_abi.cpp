@@ -64,6 +64,8 @@ struct kanode_handle {
     bool fused_solve = true;          // KANODE_OPT_FUSED_SOLVE
     bool pair_vjp = true;             // KANODE_OPT_PAIR_VJP
     bool pair_fuse = true;            // KANODE_OPT_PAIR_FUSE
+    bool pair_persist = false;        // KANODE_OPT_PAIR_PERSIST
+    int pair_persist_s = 0;           // KANODE_OPT_PAIR_PERSIST_S (0: the kernel's default)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
     // (then both run as kd_vjp_pair_ba_kernel) or kanode_internal_vjp_flush; pair_par picks the buffers of
     // the ping-pong pairs (hidden / dot-product partials, basis store, y, λs) the next stage writes
@@ -1064,6 +1066,11 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_ADJ_STEP_ROWS: return flag(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS");
     case KANODE_OPT_PAIR_VJP: return flag(h->pair_vjp, "PAIR_VJP");
     case KANODE_OPT_PAIR_FUSE: return flag(h->pair_fuse, "PAIR_FUSE");
+    case KANODE_OPT_PAIR_PERSIST: return flag(h->pair_persist, "PAIR_PERSIST");
+    case KANODE_OPT_PAIR_PERSIST_S:
+        if (value < 0 || value > 256) return fail(h, KANODE_ERR_INVALID_ARG, "PAIR_PERSIST_S must be in [0, 256]");
+        h->pair_persist_s = (int)value;
+        return KANODE_OK;
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -1081,6 +1088,8 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows ? 1 : 0;
     case KANODE_OPT_PAIR_VJP: return h->pair_vjp ? 1 : 0;
     case KANODE_OPT_PAIR_FUSE: return h->pair_fuse ? 1 : 0;
+    case KANODE_OPT_PAIR_PERSIST: return h->pair_persist ? 1 : 0;
+    case KANODE_OPT_PAIR_PERSIST_S: return h->pair_persist_s;
     }
     return -1;
 }
@@ -1494,6 +1503,25 @@ kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int
     if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_adjoint: ") + hipGetErrorString(e));
     launched = true;
     return KANODE_OK;
+}
+bool kanode_internal_pair_persist_ok(const kanode_handle* h) {
+    return h->pair_persist && h->spec.dtype == KANODE_F64 && h->spec.rhs_kind == KANODE_RHS_CHAIN && surrogate_pair(h);
+}
+int64_t kanode_internal_param_length(const kanode_handle* h) { return h->P; }
+kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int64_t batch, kan::PairAdjArgs* a,
+                                           void* stream, bool& launched) {
+    launched = false;
+    if (!kanode_internal_pair_persist_ok(h)) return KANODE_OK;
+    a->S = h->pair_persist_s;
+    a->P = h->P;
+    const hipError_t e = kan::launch_kd_pair_adjoint(h->hlc, h->dlc, (const double*)p, batch, *a, (hipStream_t)stream);
+    if (e == hipErrorNotSupported) return KANODE_OK;
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_pair_adjoint: ") + hipGetErrorString(e));
+    launched = true;
+    return KANODE_OK;
+}
+int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch) {
+    return kan::pair_adjoint_workgroups(h->hlc, batch, h->pair_persist_s);
 }
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched) {

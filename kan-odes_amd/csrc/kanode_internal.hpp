@@ -14,6 +14,7 @@ namespace kan {
 struct ChainSolveArgs;
 struct ChainAdjointArgs;
 struct AdjStepArgs;
+struct PairAdjArgs;
 }
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -95,6 +96,14 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
                                               const AdjAdaptiveFinish* af = nullptr);
 kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int64_t batch,
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched);   // drop pending reductions (error paths)
+// the persistent surrogate-pair adjoint (kd_pair_adjoint_kernel): whether the handle takes it
+// (KANODE_OPT_PAIR_PERSIST, fp64 surrogate pair), its workgroup count, and the launch (launched =
+// false when the kernel does not cover the shape / batch)
+bool kanode_internal_pair_persist_ok(const kanode_handle* h);
+int64_t kanode_internal_param_length(const kanode_handle* h);
+int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch);
+kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int64_t batch, kan::PairAdjArgs* a,
+                                           void* stream, bool& launched);
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;
 // while *skip != 0 (device, nullable) the stage kernels return at once (a finished graph-mode solve)
 kanode_status kanode_internal_rhs_stage(kanode_handle* h, const void* p, const void* u, const kanode_stage* sg,

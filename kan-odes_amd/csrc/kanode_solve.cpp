@@ -132,6 +132,9 @@ struct kanode_solution {
     // a call on this solution failed: its kernels may still be in flight and its mapped step-control slots
     // may hold written values; the next call drains the stream and re-arms every slot first (ctl_begin)
     bool ctl_dirty = false;
+    // the persistent pair adjoint's device buffer: [arrival counter, abort word][slot table | ts | dts][exchange slots]
+    void* padj = nullptr;
+    size_t padj_bytes = 0;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -171,6 +174,7 @@ struct kanode_solution {
         if (hscal) (void)hipHostFree(hscal);
         if (hparts) (void)hipHostFree(hparts);
         if (adj) (void)hipFree(adj);
+        if (padj) (void)hipFree(padj);
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
         if (g.cap_stream) (void)hipStreamDestroy(g.cap_stream);
         for (void* p : {(void*)g.bufs, (void*)g.ctl, (void*)g.saveat, g.save, (void*)g.slots, (void*)g.ts, (void*)g.dts})
@@ -1180,18 +1184,11 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     return KANODE_OK;
 }
 
-// ---- one-workgroup adjoint of a small chain (kd_chain_adjoint_kernel) ---------------------
-// Needs the contiguous dense output of the one-workgroup forward solve; done = false when not
-// covered (the host loop adjoint_t runs instead).
-template <typename T>
-kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0,
-                              void* dp, const kanode_solver_options& o, kanode_solve_stats* stats, hipStream_t st,
-                              bool& done) {
-    done = false;
-    const int64_t nsteps = (int64_t)s->ts.size();
-    if (o.control != 0 || capturing(st) || !s->slots_borrowed || nsteps < 1 ||
-        !kanode_internal_chain_tsit5_ok(h, s->batch))
-        return KANODE_OK;
+// The stops, saveat jump groups and options of the one-launch adjoints (adjoint_t's semantics): the jump
+// groups and stops go to the solution's adj_meta buffer, everything else into a (rec, k1_0, ts, dts and
+// nsteps are the caller's).
+kanode_status one_launch_adj_args(kanode_handle* h, kanode_solution* s, const void* dl_du, void* du0, void* dp,
+                                  const kanode_solver_options& o, kan::ChainAdjointArgs& a) {
     if (!o.adaptive && !(o.dt > 0))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step adjoint needs opt->dt > 0");
     const double t0 = s->t0, tf = s->tf, TT = tf - t0;
@@ -1249,7 +1246,7 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
                     rows.size() * sizeof(int32_t));
     SOLVE_HIP(h, hipMemcpy(f.adj_meta, host.data(), bytes, hipMemcpyHostToDevice));
     if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
-    kan::ChainAdjointArgs a{};
+    a = kan::ChainAdjointArgs{};
     a.t0 = t0;
     a.tf = tf;
     a.dt = o.dt;
@@ -1264,11 +1261,6 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
     a.qoldinit = o.qoldinit;
     a.adaptive = o.adaptive ? 1 : 0;
     a.maxiters = o.maxiters;
-    a.rec = f.block;
-    a.k1_0 = s->k1_0;
-    a.ts = f.ts;
-    a.dts = f.ts + f.cap;
-    a.nsteps = nsteps;
     a.dl_du = dl_du;
     a.stops = dstops;
     a.nstops = ns;
@@ -1277,6 +1269,29 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
     a.du0 = du0;
     a.dp = dp;
     a.out = f.out;
+    return KANODE_OK;
+}
+
+// ---- one-workgroup adjoint of a small chain (kd_chain_adjoint_kernel) ---------------------
+// Needs the contiguous dense output of the one-workgroup forward solve; done = false when not
+// covered (the host loop adjoint_t runs instead).
+template <typename T>
+kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0,
+                              void* dp, const kanode_solver_options& o, kanode_solve_stats* stats, hipStream_t st,
+                              bool& done) {
+    done = false;
+    const int64_t nsteps = (int64_t)s->ts.size();
+    if (o.control != 0 || capturing(st) || !s->slots_borrowed || nsteps < 1 ||
+        !kanode_internal_chain_tsit5_ok(h, s->batch))
+        return KANODE_OK;
+    kan::ChainAdjointArgs a{};
+    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, a));
+    auto& f = s->fused;
+    a.rec = f.block;
+    a.k1_0 = s->k1_0;
+    a.ts = f.ts;
+    a.dts = f.ts + f.cap;
+    a.nsteps = nsteps;
     bool launched = false;
     SOLVE_TRY(kanode_internal_chain_adjoint(h, p, s->batch, &a, st, launched));
     if (!launched) return KANODE_OK;
@@ -1285,6 +1300,67 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
     int64_t res[4];
     std::memcpy(res, s->hscal, sizeof(res));
     if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
+    if (stats) {
+        stats->naccept = res[0];
+        stats->nreject = res[1];
+        stats->nf = res[2];
+    }
+    done = true;
+    return KANODE_OK;
+}
+
+// ---- the persistent surrogate-pair adjoint (kd_pair_adjoint_kernel) --------------------------
+// KANODE_OPT_PAIR_PERSIST: after a host-loop forward solve of an fp64 surrogate pair (K-form slots),
+// the whole InterpolatingAdjoint is one launch; done = false when not covered (adjoint_t runs instead).
+kanode_status adjoint_pair_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0,
+                             void* dp, const kanode_solver_options& o, kanode_solve_stats* stats, hipStream_t st,
+                             bool& done) {
+    done = false;
+    const int64_t nsteps = (int64_t)s->ts.size();
+    if (o.control != 0 || capturing(st) || s->slots_borrowed || s->qform || !s->record || nsteps < 1 ||
+        s->dtype != KANODE_F64 || (int64_t)s->slots.size() < nsteps || !kanode_internal_pair_persist_ok(h))
+        return KANODE_OK;
+    const int nwg = kanode_internal_pair_adjoint_workgroups(h, s->batch);
+    if (nwg < 1 || nwg > 256) return KANODE_OK;
+    kan::PairAdjArgs pa{};
+    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, pa.c));
+    const size_t tab = (size_t)nsteps * sizeof(double), off_tab = 256, off_ts = off_tab + tab, off_dts = off_ts + tab;
+    const size_t off_x = (off_dts + tab + 255) / 256 * 256;
+    const size_t need = off_x + (size_t)2 * nwg * 256 * sizeof(double);
+    if (s->padj_bytes < need) {
+        if (s->padj) SOLVE_HIP(h, hipFree(s->padj));
+        s->padj = nullptr;
+        s->padj_bytes = 0;
+        SOLVE_HIP(h, hipMalloc(&s->padj, need));
+        s->padj_bytes = need;
+    }
+    std::vector<char> host(3 * tab);
+    static_assert(sizeof(void*) == sizeof(double), "slot table entries are 8 bytes");
+    std::memcpy(host.data(), s->slots.data(), tab);
+    std::memcpy(host.data() + tab, s->ts.data(), tab);
+    std::memcpy(host.data() + 2 * tab, s->dts.data(), tab);
+    char* base = (char*)s->padj;
+    SOLVE_HIP(h, hipStreamSynchronize(st));   // the forward solve's kernels are done with nothing we upload
+    SOLVE_HIP(h, hipMemcpy(base + off_tab, host.data(), 3 * tab, hipMemcpyHostToDevice));
+    pa.c.rec = base + off_tab;
+    pa.c.k1_0 = s->k1_0;
+    pa.c.ts = (const double*)(base + off_ts);
+    pa.c.dts = (const double*)(base + off_dts);
+    pa.c.nsteps = nsteps;
+    pa.ctr = (unsigned*)base;
+    pa.abrt = pa.ctr + 1;
+    pa.xbuf = (double*)(base + off_x);
+    bool launched = false;
+    SOLVE_TRY(kanode_internal_pair_adjoint(h, p, s->batch, &pa, st, launched));
+    if (!launched) return KANODE_OK;
+    auto& f = s->fused;
+    SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    int64_t res[4];
+    std::memcpy(res, s->hscal, sizeof(res));
+    if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
+    if (res[3] == 3)
+        return kanode_internal_fail(h, KANODE_ERR_HIP, "persistent pair adjoint: an exchange between workgroups timed out");
     if (stats) {
         stats->naccept = res[0];
         stats->nreject = res[1];
@@ -1422,6 +1498,7 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
     bool done = false;
     kanode_status r = s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
                                              : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done);
+    if (r == KANODE_OK && !done) r = adjoint_pair_t(h, p, s, dl_du, du0, dp, o, stats, st, done);
     if (r == KANODE_OK && !done)
         r = s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
                                    : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);

@@ -662,3 +662,95 @@ def test_failed_adjoint_leaves_no_pending_stage():
     du0f, dpf, stf = fresh.hd.adjoint_tsit5(p, dense2, g, opt.to_c(), tuple(u0.shape))
     assert st == stf
     assert torch.equal(du0, du0f) and torch.equal(dp, dpf)
+
+
+def _surrogate_ics(name, N, B, seed):
+    rng = np.random.default_rng(seed)
+    if name == "burgers512":
+        x = np.linspace(-1.0, 1.0, N)
+        a = rng.normal(0.0, 0.1, (B, 3))
+        return -np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3))
+    x = np.linspace(-5.0, 5.0, N // 2)
+    amp, th = rng.uniform(0.8, 1.2, (B, 1)), rng.uniform(0.0, 2 * np.pi, (B, 1))
+    env = amp * 2.0 / np.cosh(x)[None, :]
+    return np.concatenate([env * np.cos(th), env * np.sin(th)], axis=1)
+
+
+@pytest.mark.parametrize("name,N,G,B", [("burgers512", 512, 5, 4), ("schrodinger1024", 2048, 10, 8)])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, adaptive):
+    """the BASELINE configs[3]/[4] surrogates at their bench sizes (Burgers KAN [512, 10, 512]
+    G=5, 4 ICs; Schrödinger KAN [2048, 10, 2048] G=10, 8 ICs; Burgers_Surrogate.jl:85-107,187-206,
+    Schrodinger_Surrogate.jl:93-104,198-217), native solve + InterpolatingAdjoint (the pair pullback; at the
+    Burgers shape the fused kd_vjp_pair_ba_kernel stages) against the Python driver over the C oracle chain.
+
+    Bars.  Fixed steps (same step sequence by construction): every RHS / VJP the GPU evaluates is within
+    1e-13 of its Σ|terms| scale of the oracle's (test_gpu_surrogate.py); the solution is a sum of
+    ~6·n_steps such evaluations times h, and dp = μ(t0) a sum of ~6·n_adjoint_steps stage VJPs times h, so
+    both stay within n_evals·1e-13 of their scale over this short span (T·Lipschitz < 1, no growth), i.e.
+    1e-13 × the evaluation count: 1.2e-11 for the solution (120 RHS) and 2.6e-11 for the gradients here.
+    Adaptive: equal accepted-step counts, and the same bars times 10^3 (the step sizes themselves move
+    with rounding-level differences in the embedded error, which the fixed-step runs exclude)."""
+    from oracle_rhs import OracleChainRHS
+    specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
+    chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
+    rhs = kanode.ChainRHS(chain, device=device())
+    u0 = t(_surrogate_ics(name, N, B, 11))
+    p0 = t(chain.setup(np.random.default_rng(0))[0].astype(np.float64))
+    T = 0.05
+    ts = [0.0, 0.02, 0.035, 0.05]
+    w = np.random.default_rng(3).normal(size=(len(ts),) + tuple(u0.shape))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8) if adaptive else kanode.Tsit5Options(adaptive=False, dt=0.0025)
+    res = []
+    for f, dev in ((rhs, device()), (OracleChainRHS(specs), "cpu")):
+        p = p0.detach().to(dev).clone().requires_grad_(True)
+        x0 = u0.detach().to(dev).clone().requires_grad_(True)
+        sol = kanode.solve(f, x0, (0.0, T), p, ts, opt, sensealg="interpolating_adjoint")
+        g, gu = torch.autograd.grad((sol.u * torch.as_tensor(w, device=dev)).sum(), [p, x0])
+        res.append((sol.u.detach().cpu(), g.cpu(), gu.cpu(), sol.stats))
+    (ug, gg, gug, sg), (uc, gc, guc, sc) = res
+    assert sg["naccept"] == sc["naccept"] and sg["adjoint"]["naccept"] == sc["adjoint"]["naccept"]
+    amp = 1e3 if adaptive else 1.0
+    bar_u = amp * 1e-13 * sc["nf"]
+    bar_g = amp * 1e-13 * sc["adjoint"]["nf"]
+    eu = (ug - uc).abs().max().item() / uc.abs().max().item()
+    eg = (gg - gc).abs().max().item() / gc.abs().max().item()
+    egu = (gug - guc).abs().max().item() / guc.abs().max().item()
+    print(f"{name} adaptive={adaptive}: steps {sg['naccept']}/{sg['adjoint']['naccept']}, rel err u {eu:.2e} "
+          f"(bar {bar_u:.1e}), dp {eg:.2e}, du0 {egu:.2e} (bar {bar_g:.1e})")
+    assert eu <= bar_u
+    assert eg <= bar_g and egu <= bar_g
+
+
+@pytest.mark.parametrize("N,G,B,S", [(512, 5, 4, 0), (512, 5, 1, 0), (41, 5, 2, 0), (512, 5, 4, 4), (41, 5, 3, 7)])
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_persistent_pair_adjoint_matches_launch_path(N, G, B, S, adaptive):
+    """KANODE_OPT_PAIR_PERSIST: the whole surrogate adjoint as one launch (kd_pair_adjoint_kernel: the grid
+    split over workgroups of S points, two exchanges of the hidden partials per stage, μ in LDS, the step
+    control on the device) against the launch-per-stage native adjoint, which the full-size oracle test
+    above pins.  Same algorithm, sums in another fixed order: equal step counts, gradients to 1e-11 of
+    their scale (fixed steps) / 1e-9 (adaptive: the step sizes move with the rounding of the error norm);
+    bitwise reproducible between two runs."""
+    chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
+    rhs = kanode.ChainRHS(chain, device=device())
+    x = np.linspace(-1.0, 1.0, N)
+    a = np.random.default_rng(N + B).normal(0.0, 0.1, (B, 3))
+    u0 = t(-np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3)))
+    p0 = t(chain.setup(np.random.default_rng(1))[0].astype(np.float64))
+    ts = [0.0, 0.01, 0.02, 0.035, 0.05]
+    w = torch.as_tensor(np.random.default_rng(2).normal(size=(len(ts),) + tuple(u0.shape)), device=device())
+    opt = kanode.Tsit5Options() if adaptive else kanode.Tsit5Options(adaptive=False, dt=0.004)
+    out = []
+    for persist in (1, 1, 0):
+        with rhs.hd.options(pair_persist=persist, pair_persist_s=S):
+            p = p0.detach().clone().requires_grad_(True)
+            x0 = u0.detach().clone().requires_grad_(True)
+            sol = kanode.solve(rhs, x0, (0.0, 0.05), p, ts, opt, sensealg="interpolating_adjoint")
+            g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+            out.append((g, gu, sol.stats))
+    (g1, gu1, s1), (g1b, gu1b, _), (g0, gu0, s0) = out
+    assert torch.equal(g1, g1b) and torch.equal(gu1, gu1b)
+    assert s1["adjoint"]["naccept"] == s0["adjoint"]["naccept"] and s1["adjoint"]["nreject"] == s0["adjoint"]["nreject"]
+    bar = 1e-9 if adaptive else 1e-11
+    assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
+    assert (gu1 - gu0).abs().max().item() <= bar * gu0.abs().max().item()
