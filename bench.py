@@ -651,7 +651,13 @@ def main() -> None:
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()) if dist else 0)
     torch.cuda.set_device(dev)
     rccl_world = None
+    json_out = sys.stdout
     if dist:
+        # the collective libraries print connection chatter to the process's stdout: route fd 1 to stderr and
+        # keep a private handle on the real stdout for the one JSON line
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         import datetime
         import torch.distributed as tdist
         # a rank that dies inside a collective must not hang the others forever
@@ -835,7 +841,7 @@ def main() -> None:
         out["gpu_vs_cpu"] = value / cb["value"]
 
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if dist:
         tdist.destroy_process_group()
 

@@ -314,9 +314,10 @@ struct ChainAdjointArgs {
 // (kd_pair_adjoint_kernel, kan_pair_adj.hip): the grid split over workgroups of S points, two exchanges
 // of H·B partials per adjoint stage.  c.rec is the device table of the forward solve's slot pointers
 // ([nsteps]; slot i = u_i, k_2..k_7, each n = N·B entries), c.k1_0 the first step's k_1.
+constexpr int kPairAdjXW = 512;   // doubles per workgroup and exchange slot
 struct PairAdjArgs {
     ChainAdjointArgs c;
-    double* xbuf;     // [2][nwg][256] exchange slots (write-through stores and loads)
+    double* xbuf;     // [2][nwg][kPairAdjXW] exchange slots (write-through stores and loads)
     unsigned* ctr;    // arrival counter; ctr[1]: abort word (the 16 bytes are zeroed before every launch)
     unsigned* abrt;
     int64_t P;        // parameters of the chain (the error norm's count)

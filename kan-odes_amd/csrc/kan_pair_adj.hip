@@ -38,7 +38,8 @@ namespace kan {
 namespace {
 
 constexpr int kPA = 256;                // threads per workgroup
-constexpr int kPAMaxXW = 256;           // exchange width (H·B) cap
+constexpr int kPAMaxXW = kPairAdjXW;    // exchange width cap (6·H·B of a step's forward halves)
+constexpr int kPALd = 16;              // exchange loads in flight per thread
 constexpr unsigned kPASpinMax = 1u << 22;   // a few seconds: far beyond any legitimate wait
 
 __device__ __forceinline__ void st_agent(double* p, double v) {
@@ -77,17 +78,24 @@ __device__ bool pa_exchange(const double* vals, int cnt, double* out, double* xb
     }
     __syncthreads();
     if (!*flag) return false;
-    // fixed-order sum: thread t takes output q = t % cnt over the workgroup range of chunk t / cnt; the
-    // chunk partials are then added in chunk order
-    const int nch = cnt > 0 ? (kPA / cnt < nwg ? kPA / cnt : nwg) : 1;
+    // fixed-order sum: item (c, q) sums output q over the workgroup range of chunk c (up to kPALd loads in
+    // flight at once); the chunk partials are then added in chunk order
+    const int nch = cnt >= kPA ? 1 : (kPA / cnt < nwg ? kPA / cnt : nwg);
     const int per = (nwg + nch - 1) / nch;
-    if (threadIdx.x < nch * cnt) {
-        const int q = threadIdx.x % cnt, c = threadIdx.x / cnt;
+    for (int item = threadIdx.x; item < nch * cnt; item += kPA) {
+        const int q = item % cnt, c = item / cnt;
         const int w0 = c * per, w1 = w0 + per < nwg ? w0 + per : nwg;
         double s = 0.0;
-        for (int ww = w0; ww < w1; ++ww) s = ww == w0 ? ld_agent(slot + (size_t)ww * kPAMaxXW + q)
-                                                      : s + ld_agent(slot + (size_t)ww * kPAMaxXW + q);
-        tmp[threadIdx.x] = s;
+        for (int wb = w0; wb < w1; wb += kPALd) {
+            double v[kPALd];
+#pragma unroll
+            for (int r = 0; r < kPALd; ++r)
+                v[r] = wb + r < w1 ? ld_agent(slot + (size_t)(wb + r) * kPAMaxXW + q) : 0.0;
+#pragma unroll
+            for (int r = 0; r < kPALd; ++r)
+                if (wb + r < w1) s = wb + r == w0 ? v[r] : s + v[r];
+        }
+        tmp[item] = s;
     }
     __syncthreads();
     for (int q = threadIdx.x; q < cnt; q += kPA) {
@@ -98,6 +106,24 @@ __device__ bool pa_exchange(const double* vals, int cnt, double* out, double* xb
     __syncthreads();
     return true;
 }
+
+#ifdef KAN_PA_PROF
+// phase timing of workgroup 0 (variant builds only, tools/build_var.sh -DKAN_PA_PROF): wall-clock ticks
+// accumulated per phase mark, read by kanode_debug_pair_profile
+__device__ unsigned long long g_pa_prof[16];
+#define PA_MARK(i)                                                       \
+    do {                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                       \
+            const unsigned long long n_ = wall_clock64();                \
+            prof_acc[i] += n_ - prof_last;                               \
+            prof_last = n_;                                              \
+        }                                                                \
+    } while (0)
+#else
+#define PA_MARK(i) \
+    do {           \
+    } while (0)
+#endif
 
 // Σ of one value per thread over the block, in a fixed order; every thread gets the total
 __device__ __forceinline__ double pa_bsum(double v, double* red) {
@@ -113,16 +139,24 @@ __device__ __forceinline__ double pa_bsum(double v, double* red) {
 
 }  // namespace
 
-// LDS carve (doubles), S points per workgroup, B columns, H hidden, G1 / G2 knots:
+// LDS carve (doubles), S points per workgroup, B columns, H hidden, G1 / G2 knots, NS = 6 stage slots:
 //   ps[Pw] | mu[2][Pw] | km[7][Pw] | dens[8][S·B] | lam[S·B] | kl[7][S·B] | yv[S·B] | lsv[S·B] |
-//   phi1[S·B·G1] | dphi1[S·B·G1] | sw1[S·B] | dsw1[S·B] | hid[H·B] | hbar[H·B] | psi[H·B·G2] |
-//   dpsi[H·B·G2] | sw2[H·B] | dsw2[H·B] | part[H·B] | tmp[kPA] | red[4] | exp table[256]
+//   phi1[NS][S·B·G1] | dphi1[NS][S·B·G1] | sw1[NS][S·B] | dsw1[NS][S·B] | hid[NS][H·B] | hbar[H·B] |
+//   psi[H·B·G2] | dpsi[H·B·G2] | sw2[H·B] | dsw2[H·B] | part[NS·H·B] | tmp[max(kPA, NS·H·B)] | red[4] |
+//   exp table[256] | wsp[max(NS·H·B·S, H·B·(G2+1), S·B·(G1+1))] (per-item terms of the contractions)
+constexpr int kPANS = 6;
 __host__ __device__ inline int64_t pair_adj_pw(int S, int H, int G1, int G2, int ub1, int ub2) {
     return (int64_t)H * G1 * S + (int64_t)H * S * ub1 + (int64_t)S * G2 * H + (int64_t)S * H * ub2;
 }
+__host__ __device__ inline int64_t pair_adj_wsp(int S, int B, int H, int G1, int G2) {
+    const int64_t a = (int64_t)kPANS * H * B * S, b = (int64_t)H * B * (G2 + 1), c = (int64_t)S * B * (G1 + 1);
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
 __host__ __device__ inline int64_t pair_adj_lds_doubles(int S, int B, int H, int G1, int G2, int ub1, int ub2) {
     const int64_t Pw = pair_adj_pw(S, H, G1, G2, ub1, ub2), SB = (int64_t)S * B, HB = (int64_t)H * B;
-    return 10 * Pw + 8 * SB + 8 * SB + 2 * SB + 2 * SB * G1 + 2 * SB + 2 * HB + 2 * HB * G2 + 3 * HB + kPA + 4 + 256;
+    const int64_t nshb = (int64_t)kPANS * HB;
+    return 10 * Pw + 8 * SB + 8 * SB + 2 * SB + kPANS * (2 * SB * G1 + 2 * SB + HB) + HB + 2 * HB * G2 + 2 * HB + nshb +
+           (nshb > kPA ? nshb : kPA) + 4 + 256 + pair_adj_wsp(S, B, H, G1, G2);
 }
 
 __global__ void __launch_bounds__(kPA)
@@ -162,6 +196,10 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     const int64_t oC1 = 0, oW1 = (int64_t)H * G1 * S, oC2 = oW1 + (int64_t)H * S * ub1,
                   oW2 = oC2 + (int64_t)S * G2 * H;
 
+#ifdef KAN_PA_PROF
+    unsigned long long prof_acc[16] = {};
+    unsigned long long prof_last = wall_clock64();
+#endif
     extern __shared__ __attribute__((aligned(16))) double pa_lds[];
     double* ps = pa_lds;
     double* mu = ps + Pw;          // [2][Pw]
@@ -171,20 +209,21 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     double* kl = lam + SB;         // [7][SB]
     double* yv = kl + 7 * SB;
     double* lsv = yv + SB;
-    double* phi1 = lsv + SB;       // [SB][G1]
-    double* dphi1 = phi1 + (int64_t)SB * G1;
-    double* sw1 = dphi1 + (int64_t)SB * G1;
-    double* dsw1 = sw1 + SB;
-    double* hid = dsw1 + SB;       // [HB]
-    double* hbar = hid + HB;
-    double* psi = hbar + HB;       // [HB][G2]
+    double* phi1 = lsv + SB;                              // [NS][SB][G1]
+    double* dphi1 = phi1 + (int64_t)kPANS * SB * G1;       // [NS][SB][G1]
+    double* sw1 = dphi1 + (int64_t)kPANS * SB * G1;        // [NS][SB]
+    double* dsw1 = sw1 + (int64_t)kPANS * SB;              // [NS][SB]
+    double* hid = dsw1 + (int64_t)kPANS * SB;              // [NS][HB]
+    double* hbar = hid + (int64_t)kPANS * HB;              // [HB]
+    double* psi = hbar + HB;                               // [HB][G2]
     double* dpsi = psi + (int64_t)HB * G2;
     double* sw2 = dpsi + (int64_t)HB * G2;
     double* dsw2 = sw2 + HB;
-    double* part = dsw2 + HB;      // [HB] this workgroup's partials of an exchange
-    double* tmp = part + HB;       // [kPA]
-    double* red = tmp + kPA;       // [4]
-    double* tab = red + 4;         // [256] exp table
+    double* part = dsw2 + HB;                              // [NS·HB] this workgroup's partials of an exchange
+    double* tmp = part + (int64_t)kPANS * HB;              // [max(kPA, NS·HB)]
+    double* red = tmp + (kPANS * HB > kPA ? kPANS * HB : kPA);   // [4]
+    double* tab = red + 4;                                 // [256] exp table
+    double* wsp = tab + 256;                               // per-item contraction terms
     __shared__ int xflag;
     for (int i = threadIdx.x; i < 256; i += kPA) tab[i] = kExp2Tab256[i];
     const Math<double> M{tab};
@@ -234,84 +273,109 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         __syncthreads();
     };
 
-    // adjoint RHS at τ with the stage input ls (lsv, LDS): kλ -> kl[kslot], kμ -> km[mslot]
-    auto adj = [&](double tau, int kslot, int mslot) -> bool {
-        const double tt = tf - tau;
-        while (cur > 0 && a.ts[cur] > tt) --cur;
-        while (cur + 1 < a.nsteps && a.ts[cur + 1] <= tt) ++cur;
-        if (cur != cached) {       // the forward step's u_i, k_1..k_7 over this slice
-            const double* base = reinterpret_cast<const double*>(slots[cur]);
-            const double* k1 = cur == 0 ? reinterpret_cast<const double*>(a.k1_0)
-                                        : reinterpret_cast<const double*>(slots[cur - 1]) + 6 * n;
-            for (int q = t; q < 8 * SB; q += kPA) {
-                const int m = q / SB, e = q - m * SB;
-                double v = 0.0;
-                if (act_e(e)) {
-                    const int64_t gi = gidx(e);
-                    v = m == 0 ? base[gi] : (m == 1 ? k1[gi] : base[(int64_t)(m - 1) * n + gi]);
+    // The forward half of ns adjoint stages at the times taus[0..ns): the interpolated forward state
+    // y(tf - τ) = u_i + Σ_m (dt b_m(θ)) k_m (stage_lincomb order) over this slice, layer 1's basis per
+    // (point, column, knot) -> stage slot s, and the hidden pre-activations of every stage in ONE exchange
+    // (they do not depend on λ, so all stages of a step share it) -> hid[s].
+    auto fwd_stages = [&](const double* taus, int ns) -> bool {
+        PA_MARK(0);
+        for (int st = 0; st < ns; ++st) {
+            const double tt = tf - taus[st];
+            while (cur > 0 && a.ts[cur] > tt) --cur;
+            while (cur + 1 < a.nsteps && a.ts[cur + 1] <= tt) ++cur;
+            if (cur != cached) {       // the forward step's u_i, k_1..k_7 over this slice
+                const double* base = reinterpret_cast<const double*>(slots[cur]);
+                const double* k1 = cur == 0 ? reinterpret_cast<const double*>(a.k1_0)
+                                            : reinterpret_cast<const double*>(slots[cur - 1]) + 6 * n;
+                for (int q = t; q < 8 * SB; q += kPA) {
+                    const int m = q / SB, e = q - m * SB;
+                    double v = 0.0;
+                    if (act_e(e)) {
+                        const int64_t gi = gidx(e);
+                        v = m == 0 ? base[gi] : (m == 1 ? k1[gi] : base[(int64_t)(m - 1) * n + gi]);
+                    }
+                    dens[q] = v;
                 }
-                dens[q] = v;
+                cached = cur;
+                __syncthreads();
+                PA_MARK(1);
             }
-            cached = cur;
+            const double dti = a.dts[cur];
+            const double th = ::fmin(1.0, ::fmax(0.0, (tt - a.ts[cur]) / dti));
+            double cw[7];
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                double sm = 0.0, tp = th;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sm += RI[m][r] * tp;
+                    tp *= th;
+                }
+                cw[m] = sm * dti;
+            }
+            for (int e = t; e < SB; e += kPA) {
+                double y = dens[e];
+#pragma unroll
+                for (int m = 0; m < 7; ++m) y = ::fma(cw[m], dens[(m + 1) * SB + e], y);
+                yv[e] = y;
+            }
+            __syncthreads();
+            double* ph1 = phi1 + (int64_t)st * SB * G1;
+            double* dph1 = dphi1 + (int64_t)st * SB * G1;
+            for (int q = t; q < SB * G1; q += kPA) {
+                const int e = q / G1, g = q - e * G1;
+                const double y = yv[e];
+                const double nn = normalize<NORM_RUNTIME, double>(M, L1.norm, y);
+                const double z = (nn - (double)L1.grid[g]) * (double)L1.invh;
+                double aux = 0.0;
+                const double ph = basis_direct<double>(M, L1.basis, z, aux);
+                ph1[q] = act_e(e) ? ph : 0.0;
+                dph1[q] = act_e(e) ? dnormalize<NORM_RUNTIME, double>(L1.norm, nn) *
+                                         (basis_pull<double>(L1.basis, L1.iqf_quirk, z, ph, aux, 1.0) * (double)L1.invh)
+                                   : 0.0;
+                if (g == 0) {
+                    double sw = 0.0, dsw = 0.0;
+                    if (ub1) swish_and_grad<double>(M, y, sw, dsw);
+                    sw1[st * SB + e] = act_e(e) ? sw : 0.0;
+                    dsw1[st * SB + e] = act_e(e) ? dsw : 0.0;
+                }
+            }
             __syncthreads();
         }
-        const double dti = a.dts[cur];
-        const double th = ::fmin(1.0, ::fmax(0.0, (tt - a.ts[cur]) / dti));
-        double cw[7];
-#pragma unroll
-        for (int m = 0; m < 7; ++m) {
-            double s = 0.0, tp = th;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                s += RI[m][r] * tp;
-                tp *= th;
-            }
-            cw[m] = s * dti;
-        }
-        // y = u_i + Σ_m (dt b_m(θ)) k_m (stage_lincomb order), then layer 1's basis per (point, column, knot)
-        for (int e = t; e < SB; e += kPA) {
-            double y = dens[e];
-#pragma unroll
-            for (int m = 0; m < 7; ++m) y = ::fma(cw[m], dens[(m + 1) * SB + e], y);
-            yv[e] = y;
-        }
-        __syncthreads();
-        for (int q = t; q < SB * G1; q += kPA) {
-            const int e = q / G1, g = q - e * G1;
-            const double y = yv[e];
-            const double nn = normalize<NORM_RUNTIME, double>(M, L1.norm, y);
-            const double z = (nn - (double)L1.grid[g]) * (double)L1.invh;
-            double aux = 0.0;
-            const double ph = basis_direct<double>(M, L1.basis, z, aux);
-            phi1[q] = act_e(e) ? ph : 0.0;
-            dphi1[q] = act_e(e) ? dnormalize<NORM_RUNTIME, double>(L1.norm, nn) *
-                                      (basis_pull<double>(L1.basis, L1.iqf_quirk, z, ph, aux, 1.0) * (double)L1.invh)
-                                : 0.0;
-            if (g == 0) {
-                double sw = 0.0, dsw = 0.0;
-                if (ub1) swish_and_grad<double>(M, y, sw, dsw);
-                sw1[e] = act_e(e) ? sw : 0.0;
-                dsw1[e] = act_e(e) ? dsw : 0.0;
-            }
-        }
-        __syncthreads();
-        // exchange A: partial pre-activations over this slice
-        for (int q = t; q < HB; q += kPA) {
-            const int j = q % H, k = q / H;
-            double s = 0.0;
-            for (int il = 0; il < Sw; ++il) {
+        // partial pre-activations of every stage over this slice: item (st, jk, il) forms one input's
+        // terms, then output (st, jk) sums its S items in order
+        for (int q = t; q < ns * HB * S; q += kPA) {
+            const int sjk = q / S, il = q - sjk * S, st = sjk / HB, jk = sjk - st * HB, j = jk % H, k = jk / H;
+            double sm = 0.0;
+            if (il < Sw) {
                 const int e = il + S * k;
-                for (int g = 0; g < G1; ++g) s = ::fma(ps[oC1 + j + H * (g + G1 * il)], phi1[e * G1 + g], s);
-                if (ub1) s = ::fma(ps[oW1 + j + H * il], sw1[e], s);
+                const double* ph1 = phi1 + (int64_t)st * SB * G1;
+                for (int g = 0; g < G1; ++g) sm = ::fma(ps[oC1 + j + H * (g + G1 * il)], ph1[e * G1 + g], sm);
+                if (ub1) sm = ::fma(ps[oW1 + j + H * il], sw1[st * SB + e], sm);
             }
-            part[q] = s;
+            wsp[q] = sm;
         }
         __syncthreads();
-        if (!pa_exchange(part, HB, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag)) return false;
-        // layer 2 at the hidden activations (every workgroup: the same values)
+        for (int q = t; q < ns * HB; q += kPA) {
+            double sm = wsp[q * S];
+            for (int il = 1; il < Sw; ++il) sm += wsp[q * S + il];
+            part[q] = sm;
+        }
+        __syncthreads();
+        PA_MARK(2);
+        if (!pa_exchange(part, ns * HB, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag)) return false;
+        PA_MARK(3);
+        return true;
+    };
+
+    // The backward half of the stage in slot st with the adjoint stage input λs (lsv): layer 2 at the hidden
+    // activations hid[st], the hidden cotangents in one exchange, layer 1's pullback on this slice:
+    // kλ -> kl[kslot], kμ -> km[mslot]
+    auto back_stage = [&](int st, int kslot, int mslot) -> bool {
+        const double* hs = hid + (int64_t)st * HB;
         for (int q = t; q < HB * G2; q += kPA) {
             const int jk = q / G2, g = q - jk * G2;
-            const double h = hid[jk];
+            const double h = hs[jk];
             const double mm = normalize<NORM_RUNTIME, double>(M, L2.norm, h);
             const double z = (mm - (double)L2.grid[g]) * (double)L2.invh;
             double aux = 0.0;
@@ -327,72 +391,88 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             }
         }
         __syncthreads();
-        // exchange B: partial hidden cotangents over this slice's output rows
-        for (int q = t; q < HB; q += kPA) {
-            const int j = q % H, k = q / H;
-            double s = 0.0;
-            for (int g = 0; g < G2; ++g) {
-                double c = 0.0;
+        PA_MARK(4);
+        // partial hidden cotangents over this slice's output rows: item (jk, g) (g = G2: the base term)
+        // contracts λs over the rows, output jk sums its G2 + 1 items in order
+        for (int q = t; q < HB * (G2 + 1); q += kPA) {
+            const int jk = q / (G2 + 1), g = q - jk * (G2 + 1), j = jk % H, k = jk / H;
+            double c = 0.0, f = 0.0;
+            if (g < G2) {
                 for (int ol = 0; ol < Sw; ++ol) c = ::fma(lsv[ol + S * k], ps[oC2 + ol + S * (g + G2 * j)], c);
-                s = ::fma(dpsi[q * G2 + g], c, s);
-            }
-            if (ub2) {
-                double c = 0.0;
+                f = dpsi[jk * G2 + g];
+            } else if (ub2) {
                 for (int ol = 0; ol < Sw; ++ol) c = ::fma(lsv[ol + S * k], ps[oW2 + ol + S * j], c);
-                s = ::fma(dsw2[q], c, s);
+                f = dsw2[jk];
             }
-            part[q] = s;
+            wsp[q] = f * c;
         }
         // layer 2's parameter cotangents (own rows): dC2[o, g + G2 j] = Σ_k λs_ok ψ_g(h_jk)
         double* kmm = km + (int64_t)mslot * Pw;
         for (int64_t q = t; q < (int64_t)S * G2 * H; q += kPA) {
             const int ol = (int)(q % S), c = (int)(q / S), g = c % G2, j = c / G2;
-            double s = 0.0;
-            for (int k = 0; k < (int)B; ++k) s = ::fma(lsv[ol + S * k], psi[(j + H * k) * G2 + g], s);
-            kmm[oC2 + q] = ol < Sw ? s : 0.0;
+            double sm = 0.0;
+            for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], psi[(j + H * k) * G2 + g], sm);
+            kmm[oC2 + q] = ol < Sw ? sm : 0.0;
         }
         if (ub2)
             for (int q = t; q < S * H; q += kPA) {
                 const int ol = q % S, j = q / S;
-                double s = 0.0;
-                for (int k = 0; k < (int)B; ++k) s = ::fma(lsv[ol + S * k], sw2[j + H * k], s);
-                kmm[oW2 + q] = ol < Sw ? s : 0.0;
+                double sm = 0.0;
+                for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], sw2[j + H * k], sm);
+                kmm[oW2 + q] = ol < Sw ? sm : 0.0;
             }
         __syncthreads();
+        for (int q = t; q < HB; q += kPA) {
+            double sm = wsp[q * (G2 + 1)];
+            for (int g = 1; g <= G2; ++g) sm += wsp[q * (G2 + 1) + g];
+            part[q] = sm;
+        }
+        __syncthreads();
+        PA_MARK(5);
         if (!pa_exchange(part, HB, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag)) return false;
-        // layer 1's pullback on this slice: kλ and the input-column parameter cotangents
+        PA_MARK(6);
+        // layer 1's pullback on this slice: kλ (item (e, g), g = G1: the base term, contracts h̄ over the
+        // hidden units; entry e sums its G1 + 1 items in order) and the input-column parameter cotangents
+        const double* ph1 = phi1 + (int64_t)st * SB * G1;
+        const double* dph1 = dphi1 + (int64_t)st * SB * G1;
+        const double* sw1s = sw1 + (int64_t)st * SB;
+        const double* dsw1s = dsw1 + (int64_t)st * SB;
         double* klo = kl + (int64_t)kslot * SB;
-        for (int e = t; e < SB; e += kPA) {
-            const int il = e % S, k = e / S;
-            double s = 0.0;
+        for (int q = t; q < SB * (G1 + 1); q += kPA) {
+            const int e = q / (G1 + 1), g = q - e * (G1 + 1), il = e % S, k = e / S;
+            double c = 0.0, f = 0.0;
             if (il < Sw) {
-                for (int g = 0; g < G1; ++g) {
-                    double c = 0.0;
+                if (g < G1) {
                     for (int j = 0; j < H; ++j) c = ::fma(hbar[j + H * k], ps[oC1 + j + H * (g + G1 * il)], c);
-                    s = ::fma(dphi1[e * G1 + g], c, s);
-                }
-                if (ub1) {
-                    double c = 0.0;
+                    f = dph1[e * G1 + g];
+                } else if (ub1) {
                     for (int j = 0; j < H; ++j) c = ::fma(hbar[j + H * k], ps[oW1 + j + H * il], c);
-                    s = ::fma(dsw1[e], c, s);
+                    f = dsw1s[e];
                 }
             }
-            klo[e] = s;
+            wsp[q] = f * c;
         }
         for (int64_t q = t; q < (int64_t)H * G1 * S; q += kPA) {
             const int j = (int)(q % H), c = (int)(q / H), g = c % G1, il = c / G1;
-            double s = 0.0;
-            for (int k = 0; k < (int)B; ++k) s = ::fma(hbar[j + H * k], phi1[(il + S * k) * G1 + g], s);
-            kmm[oC1 + q] = s;
+            double sm = 0.0;
+            for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar[j + H * k], ph1[(il + S * k) * G1 + g], sm);
+            kmm[oC1 + q] = sm;
         }
         if (ub1)
             for (int q = t; q < H * S; q += kPA) {
                 const int j = q % H, il = q / H;
-                double s = 0.0;
-                for (int k = 0; k < (int)B; ++k) s = ::fma(hbar[j + H * k], sw1[il + S * k], s);
-                kmm[oW1 + q] = s;
+                double sm = 0.0;
+                for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar[j + H * k], sw1s[il + S * k], sm);
+                kmm[oW1 + q] = sm;
             }
         __syncthreads();
+        for (int e = t; e < SB; e += kPA) {
+            double sm = wsp[e * (G1 + 1)];
+            for (int g = 1; g <= G1; ++g) sm += wsp[e * (G1 + 1) + g];
+            klo[e] = sm;
+        }
+        __syncthreads();
+        PA_MARK(7);
         return true;
     };
 
@@ -407,9 +487,11 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     int k0 = 0;   // km / kl slot of the FSAL stage value
     int64_t si = 0;
     double tau = 0.0;
+    double taus[kPANS];
     if (dl) add_rows(0);
     set_ls(lam);
-    alive = adj(0.0, 0, 0);
+    taus[0] = 0.0;
+    alive = fwd_stages(taus, 1) && back_stage(0, 0, 0);
     nf = 1;
     if (alive && a.adaptive && !(a.dt > 0)) {   // Hairer-Wanner on [λ; μ]
         double s0 = 0.0, s1 = 0.0;
@@ -427,21 +509,22 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             s0 += r0 * r0;
             s1 += r1 * r1;
         }
-        part[0] = pa_bsum(s0, red);
-        part[1] = pa_bsum(s1, red);
+        const double b0 = pa_bsum(s0, red), b1 = pa_bsum(s1, red);
+        if (t == 0) {
+            part[0] = b0;
+            part[1] = b1;
+        }
         __syncthreads();
-        double tot[2];
-        alive = pa_exchange(part, 2, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
+        alive = pa_exchange(part, 2, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
         if (alive) {
-            tot[0] = hid[0];
-            tot[1] = hid[1];
+            const double d0 = ::sqrt(hbar[0] / ntot), d1 = ::sqrt(hbar[1] / ntot);
             __syncthreads();
-            const double d0 = ::sqrt(tot[0] / ntot), d1 = ::sqrt(tot[1] / ntot);
             double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
             h0 = ::fmin(h0, TT);
             for (int e = t; e < SB; e += kPA) lsv[e] = ::fma(h0, kl[e], lam[e]);
             __syncthreads();
-            alive = adj(h0, 1, 1);
+            taus[0] = h0;
+            alive = fwd_stages(taus, 1) && back_stage(0, 1, 1);
             ++nf;
             if (alive) {
                 double s2 = 0.0;
@@ -456,11 +539,12 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                     const double ee = ::fma(-1.0, km[q], km[Pw + q]) / sk;
                     s2 += ee * ee;
                 }
-                part[0] = pa_bsum(s2, red);
+                const double b2 = pa_bsum(s2, red);
+                if (t == 0) part[0] = b2;
                 __syncthreads();
-                alive = pa_exchange(part, 1, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
+                alive = pa_exchange(part, 1, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
                 if (alive) {
-                    const double d2 = ::sqrt(hid[0] / ntot) / h0;
+                    const double d2 = ::sqrt(hbar[0] / ntot) / h0;
                     __syncthreads();
                     const double mx = ::fmax(d1, d2);
                     const double h1 = mx <= 1e-15 ? ::fmax(1e-6, h0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
@@ -478,6 +562,9 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
 #pragma unroll
         for (int m = 1; m < 6; ++m) ks[m] = m;
         ks[6] = k0 == 0 ? 6 : 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) taus[i] = i == 5 ? tau + h : tau + TC[i] * h;
+        alive = fwd_stages(taus, 6);
         for (int i = 0; i < 6 && alive; ++i) {
             for (int e = t; e < SB; e += kPA) {
                 double l = lam[e];
@@ -485,14 +572,14 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 lsv[e] = l;
             }
             __syncthreads();
-            alive = adj(i == 5 ? tau + h : tau + TC[i] * h, ks[i + 1], ks[i + 1]);
+            alive = back_stage(i, ks[i + 1], ks[i + 1]);
         }
         if (!alive) break;
         nf += 6;
         // μ_new = μ + h Σ a_6j kμ_j and the error terms over this workgroup's λ and μ entries
         double* mu0 = mu + (int64_t)mc * Pw;
         double* mu1 = mu + (int64_t)(mc ^ 1) * Pw;
-        double s = 0.0;
+        double sacc = 0.0;
         for (int64_t q = t; q < Pw; q += kPA) {
             double v = mu0[q];
 #pragma unroll
@@ -504,7 +591,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], km[(int64_t)ks[m] * Pw + q], ev);
                 const double ee = ::fma(h * BT[6], km[(int64_t)ks[6] * Pw + q], ev);
                 const double sk = ::fma(a.reltol, ::fmax(kabs(mu0[q]), kabs(v)), a.abstol);
-                s += (ee / sk) * (ee / sk);
+                sacc += (ee / sk) * (ee / sk);
             }
         }
         double hnew = h;
@@ -516,13 +603,16 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], kl[(int64_t)ks[m] * SB + e], ev);
                 const double ee = ::fma(h * BT[6], kl[(int64_t)ks[6] * SB + e], ev);
                 const double sk = ::fma(a.reltol, ::fmax(kabs(lam[e]), kabs(lsv[e])), a.abstol);
-                s += (ee / sk) * (ee / sk);
+                sacc += (ee / sk) * (ee / sk);
             }
-            part[0] = pa_bsum(s, red);
+            const double bs = pa_bsum(sacc, red);
+            if (t == 0) part[0] = bs;
             __syncthreads();
-            alive = pa_exchange(part, 1, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
+            PA_MARK(8);
+            alive = pa_exchange(part, 1, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
+            PA_MARK(9);
             if (!alive) break;
-            const double eest = ::sqrt(hid[0] / ntot);
+            const double eest = ::sqrt(hbar[0] / ntot);
             __syncthreads();
             const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
             if (eest > 1.0 && h > a.dtmin) {
@@ -549,7 +639,9 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 if (dl && a.joff[si + 2] > a.joff[si + 1]) {
                     add_rows((int)si + 1);               // callback: λ += ∂L/∂u(t_j)
                     set_ls(lam);
-                    alive = adj(tau, k0, k0);            // u_modified!: FSAL re-evaluated
+                    // u_modified!: FSAL re-evaluated at τ, the time of the last stage (slot 5: its forward
+                    // half, hidden activations included, is still in place)
+                    alive = back_stage(5, k0, k0);
                     ++nf;
                 }
             }
@@ -583,6 +675,11 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             }
         }
     }
+#ifdef KAN_PA_PROF
+    PA_MARK(10);
+    if (blockIdx.x == 0 && t == 0)
+        for (int i = 0; i < 16; ++i) g_pa_prof[i] = prof_acc[i];
+#endif
     if (blockIdx.x == 0 && t == 0) {
         a.out[0] = naccept;
         a.out[1] = nreject;
@@ -603,7 +700,7 @@ hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, c
                                   PairAdjArgs pa, hipStream_t st) {
     if (pa.S <= 0) pa.S = 8;
     const LayerConst &L1 = hl[0], &L2 = hl[1];
-    if (L1.O != L2.I || L2.O != L1.I || B < 1 || (int64_t)L1.O * B > kPAMaxXW || L1.G > kMaxGrid ||
+    if (L1.O != L2.I || L2.O != L1.I || B < 1 || (int64_t)kPANS * L1.O * B > kPAMaxXW || L1.G > kMaxGrid ||
         L2.G > kMaxGrid)
         return hipErrorNotSupported;
     const int nwg = pair_adjoint_workgroups(hl, B, pa.S);
@@ -620,3 +717,15 @@ hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, c
 }
 
 }  // namespace kan
+
+#ifdef KAN_PA_PROF
+// variant builds only: the phase ticks of the last launch (workgroup 0) in µs -> out[16]
+extern "C" int kanode_debug_pair_profile(double* out) {
+    unsigned long long v[16];
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(kan::g_pa_prof), sizeof(v)) != hipSuccess) return 1;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess || khz <= 0) return 2;
+    for (int i = 0; i < 16; ++i) out[i] = (double)v[i] / (double)khz * 1e3;
+    return 0;
+}
+#endif

@@ -1326,7 +1326,7 @@ kanode_status adjoint_pair_t(kanode_handle* h, const void* p, kanode_solution* s
     SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, pa.c));
     const size_t tab = (size_t)nsteps * sizeof(double), off_tab = 256, off_ts = off_tab + tab, off_dts = off_ts + tab;
     const size_t off_x = (off_dts + tab + 255) / 256 * 256;
-    const size_t need = off_x + (size_t)2 * nwg * 256 * sizeof(double);
+    const size_t need = off_x + (size_t)2 * nwg * kan::kPairAdjXW * sizeof(double);
     if (s->padj_bytes < need) {
         if (s->padj) SOLVE_HIP(h, hipFree(s->padj));
         s->padj = nullptr;
