@@ -54,15 +54,20 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 // All nwg workgroups publish `cnt` values (vals[0..cnt) in LDS) as exchange e, then every workgroup
 // forms out[q] = Σ_{w = 0..nwg-1} partial_w[q] in that order (the same bits everywhere).
 // Returns false when the exchange was abandoned (abort raised / time-out): the caller exits.
-__device__ bool pa_exchange(const double* vals, int cnt, double* out, double* xbuf, unsigned* ctr, unsigned* abrt,
-                            int nwg, unsigned e, double* tmp /* LDS, >= kPA */, int* flag /* LDS */) {
+// The two halves of an exchange: pa_publish stores this workgroup's partials and arrives; work that does
+// not need the exchange's result may run before pa_collect waits for the other workgroups and sums.
+__device__ void pa_publish(const double* vals, int cnt, double* xbuf, unsigned* ctr, int nwg, unsigned e) {
     double* slot = xbuf + (size_t)(e & 1u) * nwg * kPAMaxXW;
     const int w = blockIdx.x;
     for (int q = threadIdx.x; q < cnt; q += kPA) st_agent(slot + (size_t)w * kPAMaxXW + q, vals[q]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
     __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ bool pa_collect(int cnt, double* out, double* xbuf, unsigned* ctr, unsigned* abrt, int nwg, unsigned e,
+                           double* tmp /* LDS, >= max(kPA, cnt) */, int* flag /* LDS */) {
+    double* slot = xbuf + (size_t)(e & 1u) * nwg * kPAMaxXW;
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned target = (unsigned)nwg * (e + 1u);
         int ok = 1;
         for (unsigned spins = 0;; ++spins) {
@@ -106,6 +111,11 @@ __device__ bool pa_exchange(const double* vals, int cnt, double* out, double* xb
     __syncthreads();
     return true;
 }
+__device__ bool pa_exchange(const double* vals, int cnt, double* out, double* xbuf, unsigned* ctr, unsigned* abrt,
+                            int nwg, unsigned e, double* tmp, int* flag) {
+    pa_publish(vals, cnt, xbuf, ctr, nwg, e);
+    return pa_collect(cnt, out, xbuf, ctr, abrt, nwg, e, tmp, flag);
+}
 
 #ifdef KAN_PA_PROF
 // phase timing of workgroup 0 (variant builds only, tools/build_var.sh -DKAN_PA_PROF): wall-clock ticks
@@ -140,10 +150,11 @@ __device__ __forceinline__ double pa_bsum(double v, double* red) {
 }  // namespace
 
 // LDS carve (doubles), S points per workgroup, B columns, H hidden, G1 / G2 knots, NS = 6 stage slots:
-//   ps[Pw] | mu[2][Pw] | km[7][Pw] | dens[8][S·B] | lam[S·B] | kl[7][S·B] | yv[S·B] | lsv[S·B] |
-//   phi1[NS][S·B·G1] | dphi1[NS][S·B·G1] | sw1[NS][S·B] | dsw1[NS][S·B] | hid[NS][H·B] | hbar[H·B] |
-//   psi[H·B·G2] | dpsi[H·B·G2] | sw2[H·B] | dsw2[H·B] | part[NS·H·B] | tmp[max(kPA, NS·H·B)] | red[4] |
-//   exp table[256] | wsp[max(NS·H·B·S, H·B·(G2+1), S·B·(G1+1))] (per-item terms of the contractions)
+//   ps[Pw] | mu[2][Pw] | km[7][Pw] | dens[8][S·B] | lam[S·B] | kl[7][S·B] | yv[NS][S·B] | lsv[S·B] |
+//   phi1[NS][S·B·G1] | dphi1[NS][S·B·G1] | sw1[NS][S·B] | dsw1[NS][S·B] | hid[NS][H·B] | hbar[2][H·B] |
+//   psi[NS][H·B·G2] | dpsi[NS][H·B·G2] | sw2[NS][H·B] | dsw2[NS][H·B] | part[NS·H·B] |
+//   tmp[max(kPA, NS·H·B)] | red[4] | exp table[256] | wsp[max(NS·H·B·S, H·B·(G2+1), S·B·(G1+1))]
+//   (wsp: per-item terms of the contractions)
 constexpr int kPANS = 6;
 __host__ __device__ inline int64_t pair_adj_pw(int S, int H, int G1, int G2, int ub1, int ub2) {
     return (int64_t)H * G1 * S + (int64_t)H * S * ub1 + (int64_t)S * G2 * H + (int64_t)S * H * ub2;
@@ -155,10 +166,13 @@ __host__ __device__ inline int64_t pair_adj_wsp(int S, int B, int H, int G1, int
 __host__ __device__ inline int64_t pair_adj_lds_doubles(int S, int B, int H, int G1, int G2, int ub1, int ub2) {
     const int64_t Pw = pair_adj_pw(S, H, G1, G2, ub1, ub2), SB = (int64_t)S * B, HB = (int64_t)H * B;
     const int64_t nshb = (int64_t)kPANS * HB;
-    return 10 * Pw + 8 * SB + 8 * SB + 2 * SB + kPANS * (2 * SB * G1 + 2 * SB + HB) + HB + 2 * HB * G2 + 2 * HB + nshb +
-           (nshb > kPA ? nshb : kPA) + 4 + 256 + pair_adj_wsp(S, B, H, G1, G2);
+    return 10 * Pw + 8 * SB + 8 * SB + kPANS * SB + SB + kPANS * (2 * SB * G1 + 2 * SB + HB) + 2 * HB +
+           kPANS * (2 * HB * G2 + 2 * HB) + nshb + (nshb > kPA ? nshb : kPA) + 4 + 256 + pair_adj_wsp(S, B, H, G1, G2);
 }
 
+// SC: the points per workgroup, a compile-time constant so the contractions over a slice unroll (their
+// LDS loads issue together)
+template <int SC>
 __global__ void __launch_bounds__(kPA)
 kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restrict__ p, int64_t B, PairAdjArgs pa) {
     constexpr double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
@@ -187,7 +201,8 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     const LayerConst& L2 = lcs[1];
     const int N = L1.I, H = L1.O, G1 = L1.G, G2 = L2.G;
     const int ub1 = L1.use_base, ub2 = L2.use_base;
-    const int S = pa.S, nwg = (int)gridDim.x;
+    constexpr int S = SC;
+    const int nwg = (int)gridDim.x;
     const int a0 = (int)blockIdx.x * S;
     const int Sw = N - a0 < S ? N - a0 : S;          // points of this workgroup (the last may hold fewer)
     const int SB = S * (int)B, HB = H * (int)B;
@@ -207,19 +222,20 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     double* dens = km + 7 * Pw;    // [8][SB]: u_i, k_1..k_7 of the cached forward step
     double* lam = dens + 8 * SB;   // [SB]
     double* kl = lam + SB;         // [7][SB]
-    double* yv = kl + 7 * SB;
-    double* lsv = yv + SB;
+    double* yv = kl + 7 * SB;                              // [NS][SB]
+    double* lsv = yv + (int64_t)kPANS * SB;
     double* phi1 = lsv + SB;                              // [NS][SB][G1]
     double* dphi1 = phi1 + (int64_t)kPANS * SB * G1;       // [NS][SB][G1]
     double* sw1 = dphi1 + (int64_t)kPANS * SB * G1;        // [NS][SB]
     double* dsw1 = sw1 + (int64_t)kPANS * SB;              // [NS][SB]
     double* hid = dsw1 + (int64_t)kPANS * SB;              // [NS][HB]
     double* hbar = hid + (int64_t)kPANS * HB;              // [HB]
-    double* psi = hbar + HB;                               // [HB][G2]
-    double* dpsi = psi + (int64_t)HB * G2;
-    double* sw2 = dpsi + (int64_t)HB * G2;
-    double* dsw2 = sw2 + HB;
-    double* part = dsw2 + HB;                              // [NS·HB] this workgroup's partials of an exchange
+    double* hbar_p = hbar + HB;                            // [HB]: h̄ of the stage whose dC1 is pending
+    double* psi = hbar_p + HB;                             // [NS][HB][G2]
+    double* dpsi = psi + (int64_t)kPANS * HB * G2;         // [NS][HB][G2]
+    double* sw2 = dpsi + (int64_t)kPANS * HB * G2;         // [NS][HB]
+    double* dsw2 = sw2 + (int64_t)kPANS * HB;              // [NS][HB]
+    double* part = dsw2 + (int64_t)kPANS * HB;             // [NS·HB] this workgroup's partials of an exchange
     double* tmp = part + (int64_t)kPANS * HB;              // [max(kPA, NS·HB)]
     double* red = tmp + (kPANS * HB > kPA ? kPANS * HB : kPA);   // [4]
     double* tab = red + 4;                                 // [256] exp table
@@ -273,17 +289,45 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         __syncthreads();
     };
 
+    // The layer-1 parameter cotangents of the last back_stage (dC1[j, g + G1 i] = Σ_k h̄_jk φ_g(y_ik), dW1), left
+    // pending because nothing on λ's path needs them: formed inside the next stage's exchange window, or
+    // before anything reads kμ or overwrites that stage's forward half (fwd_stages, the μ update).
+    int pend_st = -1, pend_m = 0;
+    auto flush_pending = [&](bool sync) {
+        if (pend_st < 0) return;
+        const double* ph1 = phi1 + (int64_t)pend_st * SB * G1;
+        const double* sw1s = sw1 + (int64_t)pend_st * SB;
+        double* kmm = km + (int64_t)pend_m * Pw;
+        for (int64_t q = t; q < (int64_t)H * G1 * S; q += kPA) {
+            const int j = (int)(q % H), c = (int)(q / H), g = c % G1, il = c / G1;
+            double sm = 0.0;
+            for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar_p[j + H * k], ph1[(il + S * k) * G1 + g], sm);
+            kmm[oC1 + q] = sm;
+        }
+        if (ub1)
+            for (int q = t; q < H * S; q += kPA) {
+                const int j = q % H, il = q / H;
+                double sm = 0.0;
+                for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar_p[j + H * k], sw1s[il + S * k], sm);
+                kmm[oW1 + q] = sm;
+            }
+        pend_st = -1;
+        if (sync) __syncthreads();
+    };
+
     // The forward half of ns adjoint stages at the times taus[0..ns): the interpolated forward state
     // y(tf - τ) = u_i + Σ_m (dt b_m(θ)) k_m (stage_lincomb order) over this slice, layer 1's basis per
     // (point, column, knot) -> stage slot s, and the hidden pre-activations of every stage in ONE exchange
     // (they do not depend on λ, so all stages of a step share it) -> hid[s].
     auto fwd_stages = [&](const double* taus, int ns) -> bool {
+        flush_pending(true);   // (its stage's forward half is about to be overwritten)
         PA_MARK(0);
         for (int st = 0; st < ns; ++st) {
             const double tt = tf - taus[st];
             while (cur > 0 && a.ts[cur] > tt) --cur;
             while (cur + 1 < a.nsteps && a.ts[cur + 1] <= tt) ++cur;
             if (cur != cached) {       // the forward step's u_i, k_1..k_7 over this slice
+                __syncthreads();       // (earlier stages' y read the previous step's values)
                 const double* base = reinterpret_cast<const double*>(slots[cur]);
                 const double* k1 = cur == 0 ? reinterpret_cast<const double*>(a.k1_0)
                                             : reinterpret_cast<const double*>(slots[cur - 1]) + 6 * n;
@@ -317,65 +361,62 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 double y = dens[e];
 #pragma unroll
                 for (int m = 0; m < 7; ++m) y = ::fma(cw[m], dens[(m + 1) * SB + e], y);
-                yv[e] = y;
+                yv[st * SB + e] = y;
             }
-            __syncthreads();
-            double* ph1 = phi1 + (int64_t)st * SB * G1;
-            double* dph1 = dphi1 + (int64_t)st * SB * G1;
-            for (int q = t; q < SB * G1; q += kPA) {
-                const int e = q / G1, g = q - e * G1;
-                const double y = yv[e];
-                const double nn = normalize<NORM_RUNTIME, double>(M, L1.norm, y);
-                const double z = (nn - (double)L1.grid[g]) * (double)L1.invh;
-                double aux = 0.0;
-                const double ph = basis_direct<double>(M, L1.basis, z, aux);
-                ph1[q] = act_e(e) ? ph : 0.0;
-                dph1[q] = act_e(e) ? dnormalize<NORM_RUNTIME, double>(L1.norm, nn) *
-                                         (basis_pull<double>(L1.basis, L1.iqf_quirk, z, ph, aux, 1.0) * (double)L1.invh)
-                                   : 0.0;
-                if (g == 0) {
-                    double sw = 0.0, dsw = 0.0;
-                    if (ub1) swish_and_grad<double>(M, y, sw, dsw);
-                    sw1[st * SB + e] = act_e(e) ? sw : 0.0;
-                    dsw1[st * SB + e] = act_e(e) ? dsw : 0.0;
-                }
-            }
-            __syncthreads();
         }
+        __syncthreads();
+        // layer 1's basis of every stage, per (stage, point, column, knot)
+        for (int q = t; q < ns * SB * G1; q += kPA) {
+            const int se = q / G1, g = q - se * G1, e = se % SB;
+            const double y = yv[se];
+            const double nn = normalize<NORM_RUNTIME, double>(M, L1.norm, y);
+            const double z = (nn - (double)L1.grid[g]) * (double)L1.invh;
+            double aux = 0.0;
+            const double ph = basis_direct<double>(M, L1.basis, z, aux);
+            phi1[q] = act_e(e) ? ph : 0.0;
+            dphi1[q] = act_e(e) ? dnormalize<NORM_RUNTIME, double>(L1.norm, nn) *
+                                      (basis_pull<double>(L1.basis, L1.iqf_quirk, z, ph, aux, 1.0) * (double)L1.invh)
+                                : 0.0;
+            if (g == 0) {
+                double sw = 0.0, dsw = 0.0;
+                if (ub1) swish_and_grad<double>(M, y, sw, dsw);
+                sw1[se] = act_e(e) ? sw : 0.0;
+                dsw1[se] = act_e(e) ? dsw : 0.0;
+            }
+        }
+        __syncthreads();
         // partial pre-activations of every stage over this slice: item (st, jk, il) forms one input's
         // terms, then output (st, jk) sums its S items in order
         for (int q = t; q < ns * HB * S; q += kPA) {
             const int sjk = q / S, il = q - sjk * S, st = sjk / HB, jk = sjk - st * HB, j = jk % H, k = jk / H;
             double sm = 0.0;
             if (il < Sw) {
-                const int e = il + S * k;
-                const double* ph1 = phi1 + (int64_t)st * SB * G1;
-                for (int g = 0; g < G1; ++g) sm = ::fma(ps[oC1 + j + H * (g + G1 * il)], ph1[e * G1 + g], sm);
-                if (ub1) sm = ::fma(ps[oW1 + j + H * il], sw1[st * SB + e], sm);
+                const int se = st * SB + il + S * k;
+#pragma unroll 5
+                for (int g = 0; g < G1; ++g) sm = ::fma(ps[oC1 + j + H * (g + G1 * il)], phi1[se * G1 + g], sm);
+                if (ub1) sm = ::fma(ps[oW1 + j + H * il], sw1[se], sm);
             }
             wsp[q] = sm;
         }
         __syncthreads();
         for (int q = t; q < ns * HB; q += kPA) {
-            double sm = wsp[q * S];
-            for (int il = 1; il < Sw; ++il) sm += wsp[q * S + il];
+            double v[S];
+#pragma unroll
+            for (int il = 0; il < S; ++il) v[il] = wsp[q * S + il];
+            double sm = v[0];
+#pragma unroll
+            for (int il = 1; il < S; ++il)
+                if (il < Sw) sm += v[il];
             part[q] = sm;
         }
         __syncthreads();
         PA_MARK(2);
         if (!pa_exchange(part, ns * HB, hid, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag)) return false;
         PA_MARK(3);
-        return true;
-    };
-
-    // The backward half of the stage in slot st with the adjoint stage input λs (lsv): layer 2 at the hidden
-    // activations hid[st], the hidden cotangents in one exchange, layer 1's pullback on this slice:
-    // kλ -> kl[kslot], kμ -> km[mslot]
-    auto back_stage = [&](int st, int kslot, int mslot) -> bool {
-        const double* hs = hid + (int64_t)st * HB;
-        for (int q = t; q < HB * G2; q += kPA) {
-            const int jk = q / G2, g = q - jk * G2;
-            const double h = hs[jk];
+        // layer 2 at every stage's hidden activations (every workgroup: the same values)
+        for (int q = t; q < ns * HB * G2; q += kPA) {
+            const int sjk = q / G2, g = q - sjk * G2;
+            const double h = hid[sjk];
             const double mm = normalize<NORM_RUNTIME, double>(M, L2.norm, h);
             const double z = (mm - (double)L2.grid[g]) * (double)L2.invh;
             double aux = 0.0;
@@ -386,56 +427,66 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             if (g == 0) {
                 double sw = 0.0, dsw = 0.0;
                 if (ub2) swish_and_grad<double>(M, h, sw, dsw);
-                sw2[jk] = sw;
-                dsw2[jk] = dsw;
+                sw2[sjk] = sw;
+                dsw2[sjk] = dsw;
             }
         }
         __syncthreads();
         PA_MARK(4);
-        // partial hidden cotangents over this slice's output rows: item (jk, g) (g = G2: the base term)
-        // contracts λs over the rows, output jk sums its G2 + 1 items in order
+        return true;
+    };
+
+    // Partial hidden cotangents of stage slot st over this slice's output rows (λs in lsv) -> outp[0..HB):
+    // item (jk, g) (g = G2: the base term) contracts λs over the rows, output jk sums its G2 + 1 items
+    auto part_b = [&](int st, double* outp) {
+        const double* dpsis = dpsi + (int64_t)st * HB * G2;
+        const double* dsw2s = dsw2 + (int64_t)st * HB;
         for (int q = t; q < HB * (G2 + 1); q += kPA) {
             const int jk = q / (G2 + 1), g = q - jk * (G2 + 1), j = jk % H, k = jk / H;
-            double c = 0.0, f = 0.0;
-            if (g < G2) {
-                for (int ol = 0; ol < Sw; ++ol) c = ::fma(lsv[ol + S * k], ps[oC2 + ol + S * (g + G2 * j)], c);
-                f = dpsi[jk * G2 + g];
-            } else if (ub2) {
-                for (int ol = 0; ol < Sw; ++ol) c = ::fma(lsv[ol + S * k], ps[oW2 + ol + S * j], c);
-                f = dsw2[jk];
-            }
+            const bool base = g == G2;
+            const int64_t off = base ? oW2 + S * j : oC2 + S * (g + G2 * j);
+            double c = 0.0;
+#pragma unroll
+            for (int ol = 0; ol < S; ++ol)
+                if (ol < Sw) c = ::fma(lsv[ol + S * k], ps[off + ol], c);
+            const double f = base ? (ub2 ? dsw2s[jk] : 0.0) : dpsis[jk * G2 + g];
             wsp[q] = f * c;
         }
-        // layer 2's parameter cotangents (own rows): dC2[o, g + G2 j] = Σ_k λs_ok ψ_g(h_jk)
+        __syncthreads();
+        for (int q = t; q < HB; q += kPA) {
+            double sm = wsp[q * (G2 + 1)];
+            for (int g = 1; g <= G2; ++g) sm += wsp[q * (G2 + 1) + g];
+            outp[q] = sm;
+        }
+        __syncthreads();
+        PA_MARK(5);
+    };
+    // While the other workgroups arrive: the previous stage's layer-1 parameter cotangents and this stage's
+    // layer-2 ones (own rows): dC2[o, g + G2 j] = Σ_k λs_ok ψ_g(h_jk) (neither is on λ's path)
+    auto dc2 = [&](int st, int mslot) {
+        flush_pending(false);
+        const double* psis = psi + (int64_t)st * HB * G2;
+        const double* sw2s = sw2 + (int64_t)st * HB;
         double* kmm = km + (int64_t)mslot * Pw;
         for (int64_t q = t; q < (int64_t)S * G2 * H; q += kPA) {
             const int ol = (int)(q % S), c = (int)(q / S), g = c % G2, j = c / G2;
             double sm = 0.0;
-            for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], psi[(j + H * k) * G2 + g], sm);
+            for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], psis[(j + H * k) * G2 + g], sm);
             kmm[oC2 + q] = ol < Sw ? sm : 0.0;
         }
         if (ub2)
             for (int q = t; q < S * H; q += kPA) {
                 const int ol = q % S, j = q / S;
                 double sm = 0.0;
-                for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], sw2[j + H * k], sm);
+                for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], sw2s[j + H * k], sm);
                 kmm[oW2 + q] = ol < Sw ? sm : 0.0;
             }
-        __syncthreads();
-        for (int q = t; q < HB; q += kPA) {
-            double sm = wsp[q * (G2 + 1)];
-            for (int g = 1; g <= G2; ++g) sm += wsp[q * (G2 + 1) + g];
-            part[q] = sm;
-        }
-        __syncthreads();
-        PA_MARK(5);
-        if (!pa_exchange(part, HB, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag)) return false;
-        PA_MARK(6);
-        // layer 1's pullback on this slice: kλ (item (e, g), g = G1: the base term, contracts h̄ over the
-        // hidden units; entry e sums its G1 + 1 items in order) and the input-column parameter cotangents
-        const double* ph1 = phi1 + (int64_t)st * SB * G1;
+    };
+    // Layer 1's pullback on this slice with h̄ (hbar): kλ -> kl[kslot] (item (e, g), g = G1: the base term,
+    // contracts h̄ over the hidden units; entry e sums its G1 + 1 items in order); the parameter cotangents
+    // are left pending (flush_pending)
+    auto xbar = [&](int st, int kslot, int mslot) {
         const double* dph1 = dphi1 + (int64_t)st * SB * G1;
-        const double* sw1s = sw1 + (int64_t)st * SB;
         const double* dsw1s = dsw1 + (int64_t)st * SB;
         double* klo = kl + (int64_t)kslot * SB;
         for (int q = t; q < SB * (G1 + 1); q += kPA) {
@@ -443,36 +494,42 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             double c = 0.0, f = 0.0;
             if (il < Sw) {
                 if (g < G1) {
-                    for (int j = 0; j < H; ++j) c = ::fma(hbar[j + H * k], ps[oC1 + j + H * (g + G1 * il)], c);
+#pragma unroll
+                    for (int j = 0; j < kWideOMax; ++j)
+                        if (j < H) c = ::fma(hbar[j + H * k], ps[oC1 + j + H * (g + G1 * il)], c);
                     f = dph1[e * G1 + g];
                 } else if (ub1) {
-                    for (int j = 0; j < H; ++j) c = ::fma(hbar[j + H * k], ps[oW1 + j + H * il], c);
+#pragma unroll
+                    for (int j = 0; j < kWideOMax; ++j)
+                        if (j < H) c = ::fma(hbar[j + H * k], ps[oW1 + j + H * il], c);
                     f = dsw1s[e];
                 }
             }
             wsp[q] = f * c;
         }
-        for (int64_t q = t; q < (int64_t)H * G1 * S; q += kPA) {
-            const int j = (int)(q % H), c = (int)(q / H), g = c % G1, il = c / G1;
-            double sm = 0.0;
-            for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar[j + H * k], ph1[(il + S * k) * G1 + g], sm);
-            kmm[oC1 + q] = sm;
-        }
-        if (ub1)
-            for (int q = t; q < H * S; q += kPA) {
-                const int j = q % H, il = q / H;
-                double sm = 0.0;
-                for (int k = 0; k < (int)B; ++k) sm = ::fma(hbar[j + H * k], sw1s[il + S * k], sm);
-                kmm[oW1 + q] = sm;
-            }
         __syncthreads();
         for (int e = t; e < SB; e += kPA) {
             double sm = wsp[e * (G1 + 1)];
             for (int g = 1; g <= G1; ++g) sm += wsp[e * (G1 + 1) + g];
             klo[e] = sm;
         }
+        for (int q = t; q < HB; q += kPA) hbar_p[q] = hbar[q];
+        pend_st = st;
+        pend_m = mslot;
         __syncthreads();
         PA_MARK(7);
+    };
+    // The backward half of the stage in slot st with the adjoint stage input λs (lsv): layer 2 at the hidden
+    // activations hid[st], the hidden cotangents in one exchange, layer 1's pullback on this slice:
+    // kλ -> kl[kslot], kμ -> km[mslot]
+    auto back_stage = [&](int st, int kslot, int mslot) -> bool {
+        part_b(st, part);
+        const unsigned eB = ex++;
+        pa_publish(part, HB, pa.xbuf, pa.ctr, nwg, eB);
+        dc2(st, mslot);
+        if (!pa_collect(HB, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, eB, tmp, &xflag)) return false;
+        PA_MARK(6);
+        xbar(st, kslot, mslot);
         return true;
     };
 
@@ -492,6 +549,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     set_ls(lam);
     taus[0] = 0.0;
     alive = fwd_stages(taus, 1) && back_stage(0, 0, 0);
+    flush_pending(true);
     nf = 1;
     if (alive && a.adaptive && !(a.dt > 0)) {   // Hairer-Wanner on [λ; μ]
         double s0 = 0.0, s1 = 0.0;
@@ -525,6 +583,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             __syncthreads();
             taus[0] = h0;
             alive = fwd_stages(taus, 1) && back_stage(0, 1, 1);
+            flush_pending(true);
             ++nf;
             if (alive) {
                 double s2 = 0.0;
@@ -575,6 +634,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             alive = back_stage(i, ks[i + 1], ks[i + 1]);
         }
         if (!alive) break;
+        flush_pending(true);
         nf += 6;
         // μ_new = μ + h Σ a_6j kμ_j and the error terms over this workgroup's λ and μ entries
         double* mu0 = mu + (int64_t)mc * Pw;
@@ -606,18 +666,38 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 sacc += (ee / sk) * (ee / sk);
             }
             const double bs = pa_bsum(sacc, red);
+            // A step that lands on a saveat stop re-evaluates the FSAL stage after the jump λ += ∂L/∂u (below).
+            // Its partial hidden cotangents do not depend on the accept/reject decision, so they ride in the
+            // error's exchange (speculatively: discarded when the step is rejected).  λs = λ_new + jump rows
+            // (add_rows' order) overwrites lsv, which a rejected step recomputes anyway.
+            const int64_t sj = si + 1;
+            const bool spec = dl && ::fabs((tau + h) - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT) && sj < a.nstops &&
+                              a.joff[sj + 1] > a.joff[sj];
+            if (spec) {
+                for (int e = t; e < SB; e += kPA) {
+                    if (!act_e(e)) continue;
+                    double l = lsv[e];
+                    for (int32_t q = a.joff[sj]; q < a.joff[sj + 1]; ++q) l = l + dl[(int64_t)a.jrows[q] * n + gidx(e)];
+                    lsv[e] = l;
+                }
+                __syncthreads();
+                part_b(5, part + 1);
+            }
             if (t == 0) part[0] = bs;
             __syncthreads();
             PA_MARK(8);
-            alive = pa_exchange(part, 1, hbar, pa.xbuf, pa.ctr, pa.abrt, nwg, ex++, tmp, &xflag);
+            const unsigned eE = ex++;
+            pa_publish(part, spec ? 1 + HB : 1, pa.xbuf, pa.ctr, nwg, eE);
+            if (spec) dc2(5, ks[6]);   // kμ_7 of this step was consumed above (μ update, error terms)
+            alive = pa_collect(spec ? 1 + HB : 1, wsp, pa.xbuf, pa.ctr, pa.abrt, nwg, eE, tmp, &xflag);
             PA_MARK(9);
             if (!alive) break;
-            const double eest = ::sqrt(hbar[0] / ntot);
-            __syncthreads();
+            const double eest = ::sqrt(wsp[0] / ntot);
             const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
             if (eest > 1.0 && h > a.dtmin) {
                 ++nreject;
                 h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
+                __syncthreads();
                 continue;
             }
             double q = q11 / ::pow(qold, a.beta2);
@@ -625,6 +705,20 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             if (1.0 <= q && q <= 1.0) q = 1.0;
             hnew = q > 0 ? h / q : h * a.qmax;
             qold = ::fmax(eest, a.qoldinit);
+            if (spec) {
+                for (int q2 = t; q2 < HB; q2 += kPA) hbar[q2] = wsp[1 + q2];
+                __syncthreads();
+                tau = a.stops[si];                                   // lands on the stop (checked above)
+                for (int e = t; e < SB; e += kPA) lam[e] = lsv[e];   // λ <- λ_new + ∂L/∂u(t_j)
+                mc ^= 1;
+                k0 = ks[6];
+                ++naccept;
+                xbar(5, k0, k0);   // u_modified!: FSAL re-evaluated at τ (stage slot 5's forward half)
+                ++nf;
+                si = sj < a.nstops ? sj : a.nstops - 1;
+                h = hnew;
+                continue;
+            }
         }
         __syncthreads();   // mu1 complete
         tau = tau + h;
@@ -700,19 +794,23 @@ hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, c
                                   PairAdjArgs pa, hipStream_t st) {
     if (pa.S <= 0) pa.S = 8;
     const LayerConst &L1 = hl[0], &L2 = hl[1];
-    if (L1.O != L2.I || L2.O != L1.I || B < 1 || (int64_t)kPANS * L1.O * B > kPAMaxXW || L1.G > kMaxGrid ||
-        L2.G > kMaxGrid)
+    if (L1.O != L2.I || L2.O != L1.I || L1.O > kWideOMax || B < 1 || (int64_t)kPANS * L1.O * B > kPAMaxXW || L1.G > kMaxGrid ||
+        L2.G > kMaxGrid || (pa.S != 4 && pa.S != 8 && pa.S != 16))
         return hipErrorNotSupported;
     const int nwg = pair_adjoint_workgroups(hl, B, pa.S);
     const size_t lds = sizeof(double) * (size_t)pair_adj_lds_doubles(pa.S, (int)B, L1.O, L1.G, L2.G, L1.use_base,
                                                                         L2.use_base);
-    if (nwg < 1 || nwg > 256 || lds > 150 * 1024) return hipErrorNotSupported;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&kd_pair_adjoint_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (nwg < 1 || nwg > 256 || lds > 158 * 1024) return hipErrorNotSupported;
+    const void* fn = pa.S == 4    ? reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<4>)
+                     : pa.S == 8 ? reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<8>)
+                                 : reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<16>);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(pa.ctr, 0, 16, st);   // the arrival counter and the abort word
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kd_pair_adjoint_kernel, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
+    if (pa.S == 4) hipLaunchKernelGGL(kd_pair_adjoint_kernel<4>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
+    else if (pa.S == 8) hipLaunchKernelGGL(kd_pair_adjoint_kernel<8>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
+    else hipLaunchKernelGGL(kd_pair_adjoint_kernel<16>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
     return hipGetLastError();
 }
 

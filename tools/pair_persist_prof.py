@@ -45,6 +45,9 @@ def main():
     print(f"S={S}: loss_and_grad {wall * 1e3:.2f} ms; adjoint steps {st['naccept']} rejects {st['nreject']} "
           f"evaluations {st['nf']} (rc {rc})")
     tot = sum(out[i] for i in range(len(PHASES)))
+    if tot <= 0:
+        print("  (the persistent adjoint did not run for this shape: the launch path took it)")
+        return
     for i, name in enumerate(PHASES):
         print(f"  {name:42s} {out[i] / 1e3:8.3f} ms  {out[i] / max(1, st['nf']):7.2f} us/eval  {100 * out[i] / tot:5.1f} %")
 
