@@ -167,11 +167,13 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     stage's second launch until the next stage is issued and run the two in one launch (the
  *     x̄ block of stage s forms stage s+1's input λs over its own chunk); 0 = two launches per
  *     stage.  Bitwise equal.
- *   KANODE_OPT_PAIR_PERSIST (default 0): kanode_adjoint_tsit5 of such a chain (fp64, after a
- *     host-loop forward solve) runs the whole InterpolatingAdjoint as ONE launch: the grid split
- *     over workgroups of KANODE_OPT_PAIR_PERSIST_S points (default 8), two exchanges of the H·B
- *     hidden partials between workgroups per adjoint stage, μ and its stage vectors resident in
- *     LDS, the step control on the device.  Same algorithm; sums in another fixed order.
+ *   KANODE_OPT_PAIR_PERSIST (default 1): kanode_adjoint_tsit5 of such a chain (fp64, after a
+ *     host-loop forward solve) runs the whole InterpolatingAdjoint as ONE launch where its LDS
+ *     carve fits (e.g. Burgers [512, 10, 512] with up to 8 trajectories): the grid split over
+ *     workgroups of KANODE_OPT_PAIR_PERSIST_S points (4, 8 or 16; 0 = 8), one exchange of the
+ *     hidden pre-activations per step and one of the hidden cotangents per adjoint stage between
+ *     workgroups, μ and its stage vectors resident in LDS, the step control on the device; other
+ *     shapes take the launch-per-stage path.  Same algorithm; sums in another fixed order.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {

@@ -208,6 +208,9 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     const int SB = S * (int)B, HB = H * (int)B;
     const int64_t n = (int64_t)N * B;
     const int64_t Pw = pair_adj_pw(S, H, G1, G2, ub1, ub2);
+    // local parameter slice: C1 [j + H(g + G1 il)] | W1 [j + H il] | C2 [c + GH2 ol], c = g + G2 j | W2 [j + H ol]
+    // (layer 2 row-transposed: the lanes of a wave then read consecutive entries)
+    const int GH2 = G2 * H;
     const int64_t oC1 = 0, oW1 = (int64_t)H * G1 * S, oC2 = oW1 + (int64_t)H * S * ub1,
                   oW2 = oC2 + (int64_t)S * G2 * H;
 
@@ -251,14 +254,14 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         if (q < oW1) g = L1.p_off + (int64_t)H * G1 * a0 + q;                           // C1[j, g + G1 i]
         else if (q < oC2) g = L1.w_off + (int64_t)H * a0 + (q - oW1);                     // W1[j, i]
         else if (q < oW2) {                                                               // C2[o, g + G2 j]
-            const int64_t r = q - oC2, ol = r % S, c = r / S;
+            const int64_t r = q - oC2, c = r % GH2, ol = r / GH2;
             g = L2.p_off + a0 + ol + (int64_t)N2 * c;
         } else {                                                                          // W2[o, j]
-            const int64_t r = q - oW2, ol = r % S, j = r / S;
+            const int64_t r = q - oW2, j = r % H, ol = r / H;
             g = L2.w_off + a0 + ol + (int64_t)N2 * j;
         }
         const bool live = (q < oC2) ? ((q < oW1 ? (q / (H * G1)) : ((q - oW1) / H)) < Sw)
-                                    : (((q < oW2 ? (q - oC2) : (q - oW2)) % S) < Sw);
+                                    : ((q < oW2 ? (q - oC2) / GH2 : (q - oW2) / H) < Sw);
         ps[q] = live ? p[g] : 0.0;
         mu[q] = 0.0;
         mu[Pw + q] = 0.0;
@@ -387,8 +390,8 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         __syncthreads();
         // partial pre-activations of every stage over this slice: item (st, jk, il) forms one input's
         // terms, then output (st, jk) sums its S items in order
-        for (int q = t; q < ns * HB * S; q += kPA) {
-            const int sjk = q / S, il = q - sjk * S, st = sjk / HB, jk = sjk - st * HB, j = jk % H, k = jk / H;
+        for (int q = t; q < ns * HB * S; q += kPA) {   // item (st, k, il, j), j fastest (consecutive C1 entries)
+            const int j = q % H, r = q / H, il = r % S, sk = r / S, k = sk % (int)B, st = sk / (int)B;
             double sm = 0.0;
             if (il < Sw) {
                 const int se = st * SB + il + S * k;
@@ -396,7 +399,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 for (int g = 0; g < G1; ++g) sm = ::fma(ps[oC1 + j + H * (g + G1 * il)], phi1[se * G1 + g], sm);
                 if (ub1) sm = ::fma(ps[oW1 + j + H * il], sw1[se], sm);
             }
-            wsp[q] = sm;
+            wsp[((int64_t)st * HB + j + H * k) * S + il] = sm;
         }
         __syncthreads();
         for (int q = t; q < ns * HB; q += kPA) {
@@ -441,21 +444,31 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
     auto part_b = [&](int st, double* outp) {
         const double* dpsis = dpsi + (int64_t)st * HB * G2;
         const double* dsw2s = dsw2 + (int64_t)st * HB;
-        for (int q = t; q < HB * (G2 + 1); q += kPA) {
-            const int jk = q / (G2 + 1), g = q - jk * (G2 + 1), j = jk % H, k = jk / H;
-            const bool base = g == G2;
-            const int64_t off = base ? oW2 + S * j : oC2 + S * (g + G2 * j);
-            double c = 0.0;
+        const int nC = (int)B * GH2, nW = ub2 ? HB : 0;
+        for (int q = t; q < nC + nW; q += kPA) {
+            double c = 0.0, f;
+            if (q < nC) {                       // (k, c = g + G2 j)
+                const int k = q / GH2, cc = q - k * GH2;
 #pragma unroll
-            for (int ol = 0; ol < S; ++ol)
-                if (ol < Sw) c = ::fma(lsv[ol + S * k], ps[off + ol], c);
-            const double f = base ? (ub2 ? dsw2s[jk] : 0.0) : dpsis[jk * G2 + g];
+                for (int ol = 0; ol < S; ++ol)
+                    if (ol < Sw) c = ::fma(lsv[ol + S * k], ps[oC2 + cc + GH2 * ol], c);
+                f = dpsis[q];                   // dψ at (j + H k)·G2 + g == cc + GH2·k == q
+            } else {                            // (k, j): the base term
+                const int r = q - nC, k = r / H, j = r - k * H;
+#pragma unroll
+                for (int ol = 0; ol < S; ++ol)
+                    if (ol < Sw) c = ::fma(lsv[ol + S * k], ps[oW2 + j + H * ol], c);
+                f = dsw2s[r];
+            }
             wsp[q] = f * c;
         }
         __syncthreads();
         for (int q = t; q < HB; q += kPA) {
-            double sm = wsp[q * (G2 + 1)];
-            for (int g = 1; g <= G2; ++g) sm += wsp[q * (G2 + 1) + g];
+            const int j = q % H, k = q / H;
+            const double* w = wsp + (int64_t)k * GH2 + (int64_t)G2 * j;
+            double sm = w[0];
+            for (int g = 1; g < G2; ++g) sm += w[g];
+            if (ub2) sm += wsp[nC + q];
             outp[q] = sm;
         }
         __syncthreads();
@@ -468,15 +481,15 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         const double* psis = psi + (int64_t)st * HB * G2;
         const double* sw2s = sw2 + (int64_t)st * HB;
         double* kmm = km + (int64_t)mslot * Pw;
-        for (int64_t q = t; q < (int64_t)S * G2 * H; q += kPA) {
-            const int ol = (int)(q % S), c = (int)(q / S), g = c % G2, j = c / G2;
+        for (int64_t q = t; q < (int64_t)S * GH2; q += kPA) {
+            const int cc = (int)(q % GH2), ol = (int)(q / GH2);
             double sm = 0.0;
-            for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], psis[(j + H * k) * G2 + g], sm);
+            for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], psis[cc + (int64_t)GH2 * k], sm);
             kmm[oC2 + q] = ol < Sw ? sm : 0.0;
         }
         if (ub2)
             for (int q = t; q < S * H; q += kPA) {
-                const int ol = q % S, j = q / S;
+                const int j = q % H, ol = q / H;
                 double sm = 0.0;
                 for (int k = 0; k < (int)B; ++k) sm = ::fma(lsv[ol + S * k], sw2s[j + H * k], sm);
                 kmm[oW2 + q] = ol < Sw ? sm : 0.0;
@@ -489,28 +502,21 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         const double* dph1 = dphi1 + (int64_t)st * SB * G1;
         const double* dsw1s = dsw1 + (int64_t)st * SB;
         double* klo = kl + (int64_t)kslot * SB;
-        for (int q = t; q < SB * (G1 + 1); q += kPA) {
-            const int e = q / (G1 + 1), g = q - e * (G1 + 1), il = e % S, k = e / S;
-            double c = 0.0, f = 0.0;
+        // item (e, j): h̄_jk · (Σ_g dφ_g(y_e) C1[j, g, il] + swish'(y_e) W1[j, il]); entry e sums its H items
+        for (int q = t; q < SB * H; q += kPA) {
+            const int e = q / H, j = q - e * H, il = e % S, k = e / S;
+            double c = 0.0;
             if (il < Sw) {
-                if (g < G1) {
-#pragma unroll
-                    for (int j = 0; j < kWideOMax; ++j)
-                        if (j < H) c = ::fma(hbar[j + H * k], ps[oC1 + j + H * (g + G1 * il)], c);
-                    f = dph1[e * G1 + g];
-                } else if (ub1) {
-#pragma unroll
-                    for (int j = 0; j < kWideOMax; ++j)
-                        if (j < H) c = ::fma(hbar[j + H * k], ps[oW1 + j + H * il], c);
-                    f = dsw1s[e];
-                }
+#pragma unroll 5
+                for (int g = 0; g < G1; ++g) c = ::fma(dph1[e * G1 + g], ps[oC1 + j + H * (g + G1 * il)], c);
+                if (ub1) c = ::fma(dsw1s[e], ps[oW1 + j + H * il], c);
             }
-            wsp[q] = f * c;
+            wsp[q] = hbar[j + H * k] * c;
         }
         __syncthreads();
         for (int e = t; e < SB; e += kPA) {
-            double sm = wsp[e * (G1 + 1)];
-            for (int g = 1; g <= G1; ++g) sm += wsp[e * (G1 + 1) + g];
+            double sm = wsp[e * H];
+            for (int j = 1; j < H; ++j) sm += wsp[e * H + j];
             klo[e] = sm;
         }
         for (int q = t; q < HB; q += kPA) hbar_p[q] = hbar[q];
@@ -761,10 +767,10 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
             } else if (q < oC2) {
                 if ((q - oW1) / H < Sw) dp[L1.w_off + (int64_t)H * a0 + (q - oW1)] = m[q];
             } else if (q < oW2) {
-                const int64_t r = q - oC2, ol = r % S, c = r / S;
+                const int64_t r = q - oC2, c = r % GH2, ol = r / GH2;
                 if (ol < Sw) dp[L2.p_off + a0 + ol + (int64_t)N2 * c] = m[q];
             } else {
-                const int64_t r = q - oW2, ol = r % S, j = r / S;
+                const int64_t r = q - oW2, j = r % H, ol = r / H;
                 if (ol < Sw) dp[L2.w_off + a0 + ol + (int64_t)N2 * j] = m[q];
             }
         }

@@ -64,7 +64,7 @@ struct kanode_handle {
     bool fused_solve = true;          // KANODE_OPT_FUSED_SOLVE
     bool pair_vjp = true;             // KANODE_OPT_PAIR_VJP
     bool pair_fuse = true;            // KANODE_OPT_PAIR_FUSE
-    bool pair_persist = false;        // KANODE_OPT_PAIR_PERSIST
+    bool pair_persist = true;         // KANODE_OPT_PAIR_PERSIST
     int pair_persist_s = 0;           // KANODE_OPT_PAIR_PERSIST_S (0: the kernel's default)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
     // (then both run as kd_vjp_pair_ba_kernel) or kanode_internal_vjp_flush; pair_par picks the buffers of

@@ -220,6 +220,7 @@ def test_native_surrogate_fused_pair_stages_bitwise(N, G, B):
     ts = [0.0, 0.01, 0.02, 0.035, 0.05]
     w = torch.as_tensor(np.random.default_rng(2).normal(size=(len(ts),) + tuple(u0.shape)), device=device())
     out = {}
+    rhs.hd.set_option("pair_persist", 0)     # the launch-per-stage adjoint (its lazy / two-launch stages)
     for fuse in (1, 0):
         with rhs.hd.options(pair_fuse=fuse):
             p = p0.detach().clone().requires_grad_(True)
@@ -647,6 +648,7 @@ def test_failed_adjoint_leaves_no_pending_stage():
     opt = kanode.Tsit5Options()
     for r in (rhs, fresh):
         r.hd.set_option("pair_fuse", 1)
+        r.hd.set_option("pair_persist", 0)   # the launch-per-stage adjoint, whose lazy stages this is about
     _, _, dense = rhs.hd.solve_tsit5(p, u0, 0.0, 0.05, ts, opt.to_c(), keep_dense=True)
     bad = opt.to_c()
     bad.maxiters = 2
@@ -676,13 +678,16 @@ def _surrogate_ics(name, N, B, seed):
     return np.concatenate([env * np.cos(th), env * np.sin(th)], axis=1)
 
 
-@pytest.mark.parametrize("name,N,G,B", [("burgers512", 512, 5, 4), ("schrodinger1024", 2048, 10, 8)])
+@pytest.mark.parametrize("name,N,G,B,persist", [("burgers512", 512, 5, 4, 1), ("burgers512", 512, 5, 4, 0),
+                                                ("schrodinger1024", 2048, 10, 8, 1)])
 @pytest.mark.parametrize("adaptive", [False, True])
-def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, adaptive):
+def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, persist, adaptive):
     """the BASELINE configs[3]/[4] surrogates at their bench sizes (Burgers KAN [512, 10, 512]
     G=5, 4 ICs; Schrödinger KAN [2048, 10, 2048] G=10, 8 ICs; Burgers_Surrogate.jl:85-107,187-206,
-    Schrodinger_Surrogate.jl:93-104,198-217), native solve + InterpolatingAdjoint (the pair pullback; at the
-    Burgers shape the fused kd_vjp_pair_ba_kernel stages) against the Python driver over the C oracle chain.
+    Schrodinger_Surrogate.jl:93-104,198-217), native solve + InterpolatingAdjoint against the Python driver over
+    the C oracle chain: at the Burgers shape both the one-launch adjoint (kd_pair_adjoint_kernel, the default)
+    and the launch-per-stage one (fused kd_vjp_pair_ba_kernel stages); Schrödinger's LDS carve does not fit
+    the one-launch kernel, so it runs per stage either way.
 
     Bars.  Fixed steps (same step sequence by construction): every RHS / VJP the GPU evaluates is within
     1e-13 of its Σ|terms| scale of the oracle's (test_gpu_surrogate.py); the solution is a sum of
@@ -695,6 +700,7 @@ def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, adaptive)
     specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
     chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
     rhs = kanode.ChainRHS(chain, device=device())
+    rhs.hd.set_option("pair_persist", persist)   # 1: the one-launch adjoint where it fits (Burgers), else per stage
     u0 = t(_surrogate_ics(name, N, B, 11))
     p0 = t(chain.setup(np.random.default_rng(0))[0].astype(np.float64))
     T = 0.05
