@@ -209,7 +209,7 @@ def fk_trained_like_params() -> np.ndarray:
     return np.linalg.solve(A.T @ A + 1e-4 * np.eye(11), A.T @ (u * (1.0 - u)))
 
 
-def epoch_adaptive_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, reps: int = 1):
+def epoch_adaptive_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, reps: int = 1, hd_opts=None):
     """The reference's Fisher-KPP training epoch as written (Fisher-KPP_Source.jl:38-44,101-109,198-201):
     T = 5, saveat every 0.5 (11 points), solve(prob, Tsit5()) at the default tolerances (abstol 1e-6,
     reltol 1e-3, adaptive), the gradient by the InterpolatingAdjoint, one Adam step; here at Nx = 256
@@ -223,6 +223,8 @@ def epoch_adaptive_bench(dev, p_np, nx, dx, D, B_gpu: int, B_cpu: int, reps: int
     u0 = fk_ics(B_gpu, nx, dx, seed=17, device=dev)
     target = (0.9 * u0).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
     tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, target, torch.as_tensor(p_np, device=dev), eta=1e-2, solver=solver)
+    for k, v in (hd_opts or {}).items():      # (A/B experiments: tools/epoch_adaptive_ab.py)
+        rhs.hd.set_option(k, v)
     tr.step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

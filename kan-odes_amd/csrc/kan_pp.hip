@@ -1091,18 +1091,35 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_NORED
 #define KAN_VROWS_NORED 0
 #endif
-template <int NORM, int PATH, int GT, int NP, int CMB>
-__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
+//
+// SPLIT = 2 (round 4): the row is split over the two waves of a wave pair, each keeping NP·128 points
+// (lane pairs at 128·NP·half + 2·lane): half the per-wave state (148 instead of 233 VGPRs), so 3 waves
+// per SIMD instead of 2 hide the fp64 dependency chains and LDS latencies that left the one-wave-per-row
+// kernel 37 % parked and 21 % issue-stalled (profiles/r04/pmc/epoch_adaptive_stall_summary.txt).  The
+// two stencil neighbours that cross the halves (points 128·NP·half − 1 and + 128·NP) arrive through LDS,
+// one block barrier per stage; every point's arithmetic is the one-wave kernel's, so λᵀJ, λ_new and kλ_7
+// are bitwise equal to it (the moment partials are block-summed over other threads, so dp differs in the
+// last bits of the reduction order).  NI > 0: the table's interval count compiled in (immediate LDS
+// offsets, as fk_vjp_pp_wave_kernel).
+template <int NORM, int PATH, int GT, int NP, int CMB, int SPLIT = 1, int NI = 0, int BT = kVjpBlock>
+__global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(SPLIT == 2 ? 3 : KAN_VROWS_WPE)))
 fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
-                        const double2* __restrict__ tables, int ni, double inv_w, double x0, double cd, double co,
+                        const double2* __restrict__ tables, int ni_rt, double inv_w, double x0, double cd, double co,
                         int64_t B, AdjStepArgs a) {
-    constexpr int Nx = 128 * NP;
+    static_assert(SPLIT == 1 || (SPLIT == 2 && NP == 1), "one wave per row, or two waves of 128 points");
+    constexpr int Nx = 128 * NP * SPLIT;   // the row
+    constexpr int kRowsPerBlock = (BT / kWave) / SPLIT;
+    const int ni = NI > 0 ? NI : ni_rt;
     extern __shared__ double2 tl[];
-    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
+    __shared__ double red[(BT / kWave) * (GT + 1)];
+    __shared__ double halo[SPLIT == 2 ? 2 * (BT / kWave) * 2 : 1];   // [stage parity][wave][left, right]
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6);
+    const int wv = threadIdx.x >> 6;
+    const int half = SPLIT == 2 ? (wv & 1) : 0;
+    const int64_t b = (int64_t)blockIdx.x * kRowsPerBlock + wv / SPLIT;
     const bool live = b < B;
-    const int64_t rb = (live ? b : 0) * Nx + 2 * lane;
+    const int poff = 128 * NP * half;      // the wave's first point in the row
+    const int64_t rb = (live ? b : 0) * Nx + poff + 2 * lane;
     // the row's loads are in flight while the block stages its tables
     kd2 lam0[NP], kl[6][NP], ui[NP], qi[4][NP];
 #pragma unroll
@@ -1124,7 +1141,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         }
     }
     const int tsz = (kPPCoef / 2) * ni;
-    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
+    for (int i = threadIdx.x; i < tsz; i += BT) {
         tl[i] = tables[PP_DPHI * tsz + i];
         tl[tsz + i] = tables[PP_SWISH * tsz + i];
     }
@@ -1142,11 +1159,12 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
     for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
     // CMB == 2: the μ error combination E is accumulated in this thread's LDS column (in registers it
-    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch)
-    __shared__ double combe[CMB == 2 ? (GT + 1) * kVjpBlock : 1];
+    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch), in the dynamic LDS after the two tables
+    // (11·BT doubles: the launcher sizes it; above 64 KB with the opt-in attribute)
+    double* __restrict__ combe = reinterpret_cast<double*>(tl + 2 * tsz);
     if constexpr (CMB == 2) {
 #pragma unroll
-        for (int j = 0; j <= GT; ++j) combe[j * kVjpBlock + threadIdx.x] = 0.0;
+        for (int j = 0; j <= GT; ++j) combe[j * BT + threadIdx.x] = 0.0;
     }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
@@ -1160,8 +1178,10 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         double dW = 0.0;
         const bool last = s == 5;
         const bool want_err = last && a.err_slab != nullptr;
-        if (live) {
-            if (s > 0 && a.reload[s]) {
+        // (a wave pair's idle half-row past B still runs the stage, on zeros, for the halo barrier: its
+        // λ = 0 adds exact zeros to the moments and the error)
+        if (live || SPLIT == 2) {
+            if (live && s > 0 && a.reload[s]) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
                     ui[k] = ld_vstep(a.su_u[s] + rb + 128 * k);
@@ -1198,7 +1218,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 lv[k].y = ::fma(1.0, t.y, lam0[k].y);
                 ev[k] = e;
             }
-            if (last && a.lam_out) {
+            if (live && last && a.lam_out) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + 128 * k, lv[k]);
             }
@@ -1208,12 +1228,21 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 rr[k] = wave_ror1(lv[k].y);
                 rl[k] = wave_rol1(lv[k].x);
             }
+            if constexpr (SPLIT == 2) {   // the halves' edge values: lane 0 takes the partner's last point,
+                                          // lane 63 its first (periodic at the row ends alike)
+                double* hx = halo + (s & 1) * 2 * (BT / kWave);
+                if (lane == kWave - 1) hx[2 * wv] = lv[NP - 1].y;
+                if (lane == 0) hx[2 * wv + 1] = lv[0].x;
+                __syncthreads();
+                if (lane == 0) rr[0] = hx[2 * (wv ^ 1)];
+                if (lane == kWave - 1) rl[NP - 1] = hx[2 * (wv ^ 1) + 1];
+            }
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
-                const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
-                const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
+                const double lm = lane == 0 && SPLIT == 1 ? rr[(k + NP - 1) % NP] : rr[k];
+                const double lp = lane == kWave - 1 && SPLIT == 1 ? rl[(k + 1) % NP] : rl[k];
                 double a0, a1;
-                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, a0, a1);
+                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, poff + 128 * k + 2 * lane, Nx, cd, co, a0, a1);
 #if KAN_VROWS_SB
                 __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1230,7 +1259,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 if (!last) {
                     kl[s + 1 < 6 ? s + 1 : 5][k] = o;
                 } else {
-                    st_vstep(a.kl[6] + rb + 128 * k, o);
+                    if (live) st_vstep(a.kl[6] + rb + 128 * k, o);
                     if (want_err) {
                         const double en = a.ec[6];
                         const double ex = ::fma(en, o.x, ev[k].x), ey = ::fma(en, o.y, ev[k].y);
@@ -1262,7 +1291,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         if constexpr (CMB == 2) {   // the μ error combination over all six stages
 #pragma unroll
             for (int j = 0; j <= GT; ++j)
-                combe[j * kVjpBlock + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * kVjpBlock + threadIdx.x]);
+                combe[j * BT + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * BT + threadIdx.x]);
         }
         if (combine && s < 5) {
 #pragma unroll
@@ -1279,7 +1308,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     if constexpr (CMB == 2) {
         double ce[GT + 1];
 #pragma unroll
-        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
+        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * BT + threadIdx.x];
         __syncthreads();
         block_sum_to<double, GT + 1>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
     }
@@ -1885,7 +1914,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
-                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows,
+                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, int rows,
                                  int* combined_out) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
@@ -1897,9 +1926,18 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     int grid = 0;
     // one row per wave, the row's stages in registers, where the grid of one row per wave fits the slab
     const bool use_rows = rows && grid_ovr == 0 && Nx <= 256 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks;
+    // two waves per row (rows >= 2): Nx = 256 with the 256-interval table (immediate LDS offsets), where
+    // the grid fits the slab.  rows = 2: 768-thread blocks (6 rows: the tables staged once per CU next to
+    // the 11·768 error-combination column, 3 waves/SIMD); 3: 256-thread blocks without the deferred
+    // combinations (6 stage reductions per step, 42 KB of LDS: 3 blocks per CU); 4: 256-thread blocks
+    // with them (65 KB: 2 blocks per CU)
+    const int split_bt = rows == 2 ? 768 : 256;
+    const bool split = use_rows && rows >= 2 && Nx == 256 && hpc.ni == 256 &&
+                       B <= (int64_t)(split_bt / kWave / 2) * slab_blocks;
     // only the rows kernel combines: fixed steps (1) through A alone, adaptive steps (2) through A and the
     // μ error combination E (the caller asks for 2 with the error slab)
-    if (!use_rows || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2)) a.combine = 0;
+    if (!use_rows || (split && rows == 3) || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2))
+        a.combine = 0;
     if (combined_out) *combined_out = a.combine;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
@@ -1907,16 +1945,44 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
         for (int m = 0; m < 4; ++m) same = same && a.su_q[s][m] == a.su_q[s - 1][m];
         a.reload[s] = same ? 0 : 1;
     }
+// (dynamic LDS above 64 KB needs the per-kernel opt-in, set once per instantiation)
+#define KAN_VSPLIT_GO(KERN, BTHREADS)                                                                            \
+    do {                                                                                                         \
+        static size_t lds_set = 0;                                                                               \
+        if (lds_s > 65536 && lds_s > lds_set) {                                                                  \
+            if (hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s) != \
+                hipSuccess)                                                                                      \
+                return hipErrorInvalidValue;                                                                     \
+            lds_set = lds_s;                                                                                     \
+        }                                                                                                        \
+        hipLaunchKernelGGL(KERN, dim3(grid), dim3(BTHREADS), lds_s, st, lc, p, (const double2*)tables, hpc.ni,   \
+                           hpc.inv_w, hpc.x0, cd, co, B, a);                                                     \
+    } while (0)
 #define KAN_VSTEP(NORM, PATH, GT, NP)                                                                              \
     do {                                                                                                         \
+        if (split && NP == 2) {                                                                                  \
+            const size_t lds_s = lds + (a.combine == 2 ? (size_t)(GT + 1) * split_bt * sizeof(double) : 0);      \
+            grid = grid_for(B, split_bt / kWave / 2, slab_blocks);                                               \
+            for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
+            if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
+            if (split_bt == 768 && a.combine == 2)                                                               \
+                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 2, 2, 256, 768>), 768);                 \
+            else if (split_bt == 768)                                                                            \
+                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 0, 2, 256, 768>), 768);                 \
+            else if (a.combine == 2)                                                                             \
+                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 2, 2, 256, 256>), 256);                 \
+            else                                                                                                 \
+                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 0, 2, 256, 256>), 256);                 \
+            break;                                                                                               \
+        }                                                                                                        \
         if (use_rows) {                                                                                          \
             grid = grid_for(B, kVjpBlock / kWave, slab_blocks);                                                  \
             for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
             if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
             if (a.combine == 2)                                                                                  \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 2>), dim3(grid),    \
-                                   dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
-                                   hpc.x0, cd, co, B, a);                                                        \
+                                   dim3(kVjpBlock), lds + (size_t)(GT + 1) * kVjpBlock * sizeof(double), st, lc, p, \
+                                   (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, B, a);             \
             else                                                                                                 \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 0>), dim3(grid),    \
                                    dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
@@ -1951,6 +2017,7 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     }
 #undef KAN_VSTEP_NP
 #undef KAN_VSTEP
+#undef KAN_VSPLIT_GO
     *grid_out = grid;
     return hipGetLastError();
 }

@@ -117,7 +117,7 @@ def _progress(msg: str) -> None:
 
 
 def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: int = 100, dev="cuda:0",
-               loss_every: int = 0, out_path: str | None = None) -> dict:
+               loss_every: int = 0, out_path: str | None = None, max_seconds: float = 0.0) -> dict:
     dev = torch.device(dev)
     pr = source_problem(which)
     iters = int(iters or pr["iters"])
@@ -141,14 +141,19 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
     curve = [(0, post_loss(tr.p))]
     t0 = time.perf_counter()
     last = t0
+    done = 0
     for i in range(1, iters + 1):
         tr.step()
+        done = i
         if i % log_every == 0 or i == iters:
             curve.append((i, post_loss(tr.p)))           # l[end] = loss(p) after update! (:204)
             now = time.perf_counter()
             if now - last > 30 or i == iters:
                 _progress(f"{pr['name']}: iteration {i}/{iters} loss {curve[-1][1]:.4e} ({now - t0:.0f} s)")
                 last = now
+            if max_seconds and now - t0 > max_seconds:    # time budget of the GPU call: stop at a log point
+                _progress(f"{pr['name']}: stopping at iteration {i} (time budget {max_seconds:.0f} s)")
+                break
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     lr = learned(tr.p)
@@ -157,9 +162,10 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
     scale = float(np.max(np.abs(fit)))
     _, _, sol = tr.loss_and_grad()
     out = {
-        "anchor": pr["name"], "reference": pr["ref"], "iters": iters, "eta": pr["eta"], "seed": seed,
+        "anchor": pr["name"], "reference": pr["ref"], "iters": done, "iters_requested": iters, "eta": pr["eta"],
+        "seed": seed,
         "nx": pr["nx"], "dx": pr["dx"], "D": pr["D"], "tspan": list(pr["tspan"]), "n_saveat": len(pr["saveat"]),
-        "wall_s": wall, "ms_per_iteration": wall / iters * 1e3,
+        "wall_s": wall, "ms_per_iteration": wall / max(done, 1) * 1e3,
         "what": "Trainer.step per iteration (native Tsit5 + InterpolatingAdjoint + FusedAdam); wall_s includes the "
                 "logged loss, a forward solve after the update every log_every iterations",
         "log_every": log_every,
@@ -236,6 +242,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log-every", type=int, default=100)
     ap.add_argument("--out", default="gpurun_out/anchors")
+    ap.add_argument("--max-seconds", type=float, default=0.0, help="stop at the first log point past this")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     path = os.path.join(a.out, f"{a.problem}.json")
@@ -244,7 +251,7 @@ def main() -> None:
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_train_final",
                                             "loss_train_min", "loss_test_final", "recorded_converged_loss")}))
     else:
-        o = run_source(a.problem, a.iters or None, a.seed, a.log_every, out_path=path)
+        o = run_source(a.problem, a.iters or None, a.seed, a.log_every, out_path=path, max_seconds=a.max_seconds)
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_final",
                                             "max_abs_dev_from_recorded_fit", "max_abs_dev_from_true_source")}))
 

@@ -15,4 +15,5 @@ run p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_
 run p2 SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
 run p3 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_TRANS_F64 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA
 run p4 SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_WAVES
-python3 tools/pmc_stall.py $OUT > $OUT/stall_summary.txt && cat $OUT/stall_summary.txt
+python3 tools/pmc_stall.py $OUT > $OUT/stall_summary.txt && grep -A14 "fk_vjp_step_rows_kernel" $OUT/stall_summary.txt
+rm -rf $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4   # the per-dispatch CSVs are tens of MB; the summary is what is kept
