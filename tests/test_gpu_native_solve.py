@@ -574,12 +574,14 @@ def test_adjoint_step_rows_kernel_matches_persistent_grid(nx, B, adaptive, rows)
     assert torch.equal(s1.u, s0.u)
     if adaptive:
         # μ starts at 0, so its error scale is abstol and the μ error estimate (a difference of
-        # reduced sums) carries the reductions' rounding: the two kernels' step sequences can part
-        # on last-bit differences (as in test_native_adjoint_matches_python_adjoint); both then
-        # solve the same adjoint to the tolerance
+        # reduced sums) carries the reductions' rounding: the two kernels' step sizes can part on
+        # last-bit differences (as in test_native_adjoint_matches_python_adjoint), with equal step
+        # counts or not (measured: the split rows kernel at B = 37, equal counts, 3.2e-9 of max|dL/du0|);
+        # both then solve the same adjoint to the tolerance.  The fixed-step cases below are the
+        # arithmetic check (λ bitwise)
         na, nb = s1.stats["adjoint"]["naccept"], s0.stats["adjoint"]["naccept"]
         assert abs(na - nb) <= 0.01 * nb
-        tol = 1e-9 if na == nb else 50 * opt.reltol
+        tol = 50 * opt.reltol
         assert (g1 - g0).abs().max().item() <= tol * g0.abs().max().item()
         assert (gu1 - gu0).abs().max().item() <= tol * gu0.abs().max().item()
     else:

@@ -4,6 +4,7 @@ saveat 0.5, default tolerances, 4,096 trajectories; native Tsit5 + Interpolating
     python3 tools/epoch_adaptive_ab.py --variants "adj_step_rows=1;adj_step_rows=2" --rounds 3
 Each round runs every variant once (a fresh Trainer, one warm-up epoch, `reps` timed epochs)."""
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -37,6 +38,8 @@ for r in range(a.rounds):
         res[v].append(out["gpu"] * 1e3)
         steps[v] = (out["forward_steps"], out["adjoint_steps"], out["adjoint_rejects"])
         print(f"round {r} {v}: {out['gpu'] * 1e3:.1f} ms/epoch  steps {steps[v]}", flush=True)
+        gc.collect()               # the previous handle's dense output (~180 GB at 3,707 steps) goes first
+        torch.cuda.empty_cache()
 for v in variants:
     print(json.dumps({"variant": v, "median_ms": statistics.median(res[v]), "all_ms": res[v],
                       "forward_adjoint_rejects": steps[v]}))

@@ -1,10 +1,12 @@
 #!/bin/bash
-# Round 4: the short anchor test, then the Allen-Cahn source anchor (N_iter = 5e4 at ~17 ms per iteration,
+# Round 4: the persistent pair adjoint's phase profile (final kernel), the short anchor test, then the Allen-Cahn source anchor (N_iter = 5e4 at ~17 ms per iteration,
 # two initialisations side by side, each stopping at its time budget if the call's limit comes first).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r4/anchors_ac
-mkdir -p $O/s0 $O/s1
+mkdir -p $O/s0 $O/s1 $R/gpurun_out/r4/persist
+KANODE_LIB=$R/tools/bin/var/paprof.so timeout -k 10 120 python -u tools/pair_persist_prof.py 0 \
+    > $R/gpurun_out/r4/persist/prof_s8_final.txt 2>&1 || exit 3
 timeout -k 10 200 python -u -m pytest -x -v --timeout 180 --timeout-method thread -s tests/test_gpu_anchors.py \
     > $O/pytest_anchors.txt 2>&1
 rc=$?

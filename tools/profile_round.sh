@@ -47,3 +47,5 @@ done
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 BATCH=${BATCH:-1048576} python3 tools/traffic.py $OUT > $OUT/traffic.json
 cat $OUT/pmc_summary.txt $OUT/traffic.json
+# the per-dispatch CSVs are tens of MB (gpurun returns at most 64 MiB): keep the summaries only
+find $OUT -mindepth 1 -maxdepth 1 -type d -exec rm -rf {} +
