@@ -156,12 +156,10 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     adjoint stage / one-launch adjoint step (0 = occupancy-derived).
  *     Tuning only: the grid fixes the order of the dp reduction, so gradients are
  *     bitwise reproducible for a given grid, not across grids.
- *   KANODE_OPT_ADJ_STEP_ROWS (default 2): the one-launch Fisher-KPP adjoint step keeps each
- *     trajectory row's stage values in registers (batches up to 8192 rows of <= 256 points,
- *     GRID_ADJ_STEP unset): 1 = one wave per row; 2 = in addition, 256-point rows with the
- *     256-interval table split over two waves (batches up to 4096; round 4); 0 = the
- *     persistent-grid step kernel, whose stages pass kλ through memory.  Same λᵀJ and λ
- *     bitwise in all three; dp to the reduction order.
+ *   KANODE_OPT_ADJ_STEP_ROWS (default 1): the one-launch Fisher-KPP adjoint step keeps each
+ *     trajectory row's stage values in the registers of one wave (batches up to 8192 rows
+ *     of <= 256 points, GRID_ADJ_STEP unset); 0 = the persistent-grid step kernel, whose
+ *     stages pass kλ through memory.  Same λᵀJ and λ bitwise; dp to the reduction order.
  *   KANODE_OPT_PAIR_VJP (default 1): the VJP / adjoint stage of a surrogate chain KAN [N, H, N]
  *     (wide-in then wide-out layer) runs as two launches (batches up to 64); 0 = the four-launch
  *     path.  Equal to the summation order of the wide-out dot products (both fixed-order).

@@ -91,7 +91,7 @@ hipError_t launch_adam_step(T* x, T* m, T* v, const T* g, int64_t n, const AdamA
 // occupancy-derived default).  Tuning sweeps only: the grid fixes the dp reduction order.
 struct GridOverride {
     int rhs = 0, vjp = 0, vstep = 0;
-    int vstep_rows = 2;   // KANODE_OPT_ADJ_STEP_ROWS (0 off, 1 one wave per row, 2 also two waves per row)
+    bool vstep_rows = true;   // KANODE_OPT_ADJ_STEP_ROWS
 };
 hipError_t launch_fk_pp_build(const PPConst& hpc, const LayerConst* lc, const PPConst* pc, const double* p,
                               double* tables, const int* fns, int nfn, hipStream_t st);
@@ -158,8 +158,8 @@ struct AdjStepArgs {
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
-                                 hipStream_t st, bool build, int grid_ovr = 0, int rows = 2,
-                                 int* combined_out = nullptr);   // rows: 0 off, 1 one wave per row, 2 + split
+                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true,
+                                 int* combined_out = nullptr);
 constexpr int kMaxFinishJobs = 8;
 struct FinishJob {
     const double* slab;

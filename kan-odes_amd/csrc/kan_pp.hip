@@ -649,6 +649,9 @@ __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const d
     return in && (y == y) && (z == z);
 }
 
+#ifndef KAN_VJP_R2
+#define KAN_VJP_R2 0
+#endif
 // One point of the pullback: returns λ φ'(x); accumulates the dC moments and dW.
 // With v_j = λ E0 R^j and the knot correction kc_j = K_j (1 + τ' e_j + τ'² e_j²/2):
 //     Σ_points λ B_j = K_j (S0_j + e_j S1_j + e_j²/2 S2_j),
@@ -681,10 +684,26 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
     const float R2 = R32 * R32;
     const kf2 R2v = {R2, R2};
 #endif
+#if KAN_VJP_R2
+    // two independent power chains (even and odd knots advanced by R²): half the dependent multiplies
+    // in a row (the knot values differ from the single chain's in the last bits)
+    const double Rsq = R * R;
+    double vo = v * R;
+#endif
 #pragma unroll
     for (int j = 0; j < GT; ++j) {
+#if KAN_VJP_R2
+        if (j & 1) {
+            S0[j] = S0[j] + vo;
+            vo = vo * Rsq;
+        } else {
+            S0[j] = S0[j] + v;
+            v = v * Rsq;
+        }
+#else
         S0[j] = S0[j] + v;
         v = v * R;
+#endif
         if constexpr (PATH == PATH_REC_CORR) {
 #if KAN_VJP_PACKED
             const float vj = (j & 1) ? vp.y : vp.x;
@@ -1091,35 +1110,25 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_NORED
 #define KAN_VROWS_NORED 0
 #endif
-//
-// SPLIT = 2 (round 4): the row is split over the two waves of a wave pair, each keeping NP·128 points
-// (lane pairs at 128·NP·half + 2·lane): half the per-wave state (148 instead of 233 VGPRs), so 3 waves
-// per SIMD instead of 2 hide the fp64 dependency chains and LDS latencies that left the one-wave-per-row
-// kernel 37 % parked and 21 % issue-stalled (profiles/r04/pmc/epoch_adaptive_stall_summary.txt).  The
-// two stencil neighbours that cross the halves (points 128·NP·half − 1 and + 128·NP) arrive through LDS,
-// one block barrier per stage; every point's arithmetic is the one-wave kernel's, so λᵀJ, λ_new and kλ_7
-// are bitwise equal to it (the moment partials are block-summed over other threads, so dp differs in the
-// last bits of the reduction order).  NI > 0: the table's interval count compiled in (immediate LDS
-// offsets, as fk_vjp_pp_wave_kernel).
-template <int NORM, int PATH, int GT, int NP, int CMB, int SPLIT = 1, int NI = 0, int BT = kVjpBlock>
-__global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(SPLIT == 2 ? 3 : KAN_VROWS_WPE)))
+// NI > 0: the table's interval count compiled in, so the Horner coefficients' LDS offsets are instruction
+// immediates (as fk_vjp_pp_wave_kernel; round 4: the per-point address arithmetic of the runtime count
+// was ~8 VALU per point and stage)
+#ifndef KAN_VROWS_NI
+#define KAN_VROWS_NI 1
+#endif
+template <int NORM, int PATH, int GT, int NP, int CMB, int NI = 0>
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
 fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                         const double2* __restrict__ tables, int ni_rt, double inv_w, double x0, double cd, double co,
                         int64_t B, AdjStepArgs a) {
-    static_assert(SPLIT == 1 || (SPLIT == 2 && NP == 1), "one wave per row, or two waves of 128 points");
-    constexpr int Nx = 128 * NP * SPLIT;   // the row
-    constexpr int kRowsPerBlock = (BT / kWave) / SPLIT;
+    constexpr int Nx = 128 * NP;
     const int ni = NI > 0 ? NI : ni_rt;
     extern __shared__ double2 tl[];
-    __shared__ double red[(BT / kWave) * (GT + 1)];
-    __shared__ double halo[SPLIT == 2 ? 2 * (BT / kWave) * 2 : 1];   // [stage parity][wave][left, right]
+    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x >> 6;
-    const int half = SPLIT == 2 ? (wv & 1) : 0;
-    const int64_t b = (int64_t)blockIdx.x * kRowsPerBlock + wv / SPLIT;
+    const int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6);
     const bool live = b < B;
-    const int poff = 128 * NP * half;      // the wave's first point in the row
-    const int64_t rb = (live ? b : 0) * Nx + poff + 2 * lane;
+    const int64_t rb = (live ? b : 0) * Nx + 2 * lane;
     // the row's loads are in flight while the block stages its tables
     kd2 lam0[NP], kl[6][NP], ui[NP], qi[4][NP];
 #pragma unroll
@@ -1141,7 +1150,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         }
     }
     const int tsz = (kPPCoef / 2) * ni;
-    for (int i = threadIdx.x; i < tsz; i += BT) {
+    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
         tl[tsz + i] = tables[PP_SWISH * tsz + i];
     }
@@ -1159,12 +1168,11 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
     for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
     // CMB == 2: the μ error combination E is accumulated in this thread's LDS column (in registers it
-    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch), in the dynamic LDS after the two tables
-    // (11·BT doubles: the launcher sizes it; above 64 KB with the opt-in attribute)
-    double* __restrict__ combe = reinterpret_cast<double*>(tl + 2 * tsz);
+    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch)
+    __shared__ double combe[CMB == 2 ? (GT + 1) * kVjpBlock : 1];
     if constexpr (CMB == 2) {
 #pragma unroll
-        for (int j = 0; j <= GT; ++j) combe[j * BT + threadIdx.x] = 0.0;
+        for (int j = 0; j <= GT; ++j) combe[j * kVjpBlock + threadIdx.x] = 0.0;
     }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
@@ -1178,10 +1186,8 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         double dW = 0.0;
         const bool last = s == 5;
         const bool want_err = last && a.err_slab != nullptr;
-        // (a wave pair's idle half-row past B still runs the stage, on zeros, for the halo barrier: its
-        // λ = 0 adds exact zeros to the moments and the error)
-        if (live || SPLIT == 2) {
-            if (live && s > 0 && a.reload[s]) {
+        if (live) {
+            if (s > 0 && a.reload[s]) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
                     ui[k] = ld_vstep(a.su_u[s] + rb + 128 * k);
@@ -1190,17 +1196,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 }
             }
             kd2 uv[NP], lv[NP], ev[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {   // u(t_s) = u_i + Σ_m θ^m Q_m
-                kd2 t{0.0, 0.0};
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    t.x = ::fma(a.su_c[s][m], qi[m][k].x, t.x);
-                    t.y = ::fma(a.su_c[s][m], qi[m][k].y, t.y);
-                }
-                uv[k].x = ::fma(1.0, t.x, ui[k].x);
-                uv[k].y = ::fma(1.0, t.y, ui[k].y);
-            }
+            // λs first (registers only): a reloaded stage's dense output is still in flight
 #pragma unroll
             for (int k = 0; k < NP; ++k) {   // λs = λ + Σ_{j<=s} h a_sj kλ_j (and the error sum)
                 kd2 t{0.0, 0.0}, e{0.0, 0.0};
@@ -1218,7 +1214,18 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 lv[k].y = ::fma(1.0, t.y, lam0[k].y);
                 ev[k] = e;
             }
-            if (live && last && a.lam_out) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {   // u(t_s) = u_i + Σ_m θ^m Q_m
+                kd2 t{0.0, 0.0};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    t.x = ::fma(a.su_c[s][m], qi[m][k].x, t.x);
+                    t.y = ::fma(a.su_c[s][m], qi[m][k].y, t.y);
+                }
+                uv[k].x = ::fma(1.0, t.x, ui[k].x);
+                uv[k].y = ::fma(1.0, t.y, ui[k].y);
+            }
+            if (last && a.lam_out) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + 128 * k, lv[k]);
             }
@@ -1228,21 +1235,12 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 rr[k] = wave_ror1(lv[k].y);
                 rl[k] = wave_rol1(lv[k].x);
             }
-            if constexpr (SPLIT == 2) {   // the halves' edge values: lane 0 takes the partner's last point,
-                                          // lane 63 its first (periodic at the row ends alike)
-                double* hx = halo + (s & 1) * 2 * (BT / kWave);
-                if (lane == kWave - 1) hx[2 * wv] = lv[NP - 1].y;
-                if (lane == 0) hx[2 * wv + 1] = lv[0].x;
-                __syncthreads();
-                if (lane == 0) rr[0] = hx[2 * (wv ^ 1)];
-                if (lane == kWave - 1) rl[NP - 1] = hx[2 * (wv ^ 1) + 1];
-            }
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
-                const double lm = lane == 0 && SPLIT == 1 ? rr[(k + NP - 1) % NP] : rr[k];
-                const double lp = lane == kWave - 1 && SPLIT == 1 ? rl[(k + 1) % NP] : rl[k];
+                const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
+                const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
                 double a0, a1;
-                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, poff + 128 * k + 2 * lane, Nx, cd, co, a0, a1);
+                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, a0, a1);
 #if KAN_VROWS_SB
                 __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1259,7 +1257,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 if (!last) {
                     kl[s + 1 < 6 ? s + 1 : 5][k] = o;
                 } else {
-                    if (live) st_vstep(a.kl[6] + rb + 128 * k, o);
+                    st_vstep(a.kl[6] + rb + 128 * k, o);
                     if (want_err) {
                         const double en = a.ec[6];
                         const double ex = ::fma(en, o.x, ev[k].x), ey = ::fma(en, o.y, ev[k].y);
@@ -1291,7 +1289,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         if constexpr (CMB == 2) {   // the μ error combination over all six stages
 #pragma unroll
             for (int j = 0; j <= GT; ++j)
-                combe[j * BT + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * BT + threadIdx.x]);
+                combe[j * kVjpBlock + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * kVjpBlock + threadIdx.x]);
         }
         if (combine && s < 5) {
 #pragma unroll
@@ -1308,7 +1306,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     if constexpr (CMB == 2) {
         double ce[GT + 1];
 #pragma unroll
-        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * BT + threadIdx.x];
+        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
         __syncthreads();
         block_sum_to<double, GT + 1>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
     }
@@ -1379,11 +1377,8 @@ hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, 
     return hipGetLastError();
 }
 
-// 1024 threads: the slab rows of a step kernel's grid (up to 1024 blocks) are one load per slab per thread,
-// all in flight at once (with 256 threads the four grid-stride rounds of loads ran one after the other)
-constexpr int kAdjFinBlock = 1024;
-__global__ void __launch_bounds__(kAdjFinBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
-    __shared__ double red[(kAdjFinBlock / kWave) * 6];
+__global__ void __launch_bounds__(kBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
+    __shared__ double red[(kBlock / kWave) * 6];
     __shared__ double sums[6];
     const int64_t q = blockIdx.x;
     if (q == P) {   // the λ error partials
@@ -1429,7 +1424,7 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_kernel(AdjFinish f, i
 
 hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st) {
     if (f.nslab < 1 || f.nslab > 6 || P < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(adj_finish_kernel, dim3((unsigned)P + 1), dim3(kAdjFinBlock), 0, st, f, P);
+    hipLaunchKernelGGL(adj_finish_kernel, dim3((unsigned)P + 1), dim3(kBlock), 0, st, f, P);
     return hipGetLastError();
 }
 
@@ -1917,7 +1912,7 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
-                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, int rows,
+                                 int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows,
                                  int* combined_out) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
@@ -1929,18 +1924,9 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     int grid = 0;
     // one row per wave, the row's stages in registers, where the grid of one row per wave fits the slab
     const bool use_rows = rows && grid_ovr == 0 && Nx <= 256 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks;
-    // two waves per row (rows >= 2): Nx = 256 with the 256-interval table (immediate LDS offsets), where
-    // the grid fits the slab.  rows = 2: 768-thread blocks (6 rows: the tables staged once per CU next to
-    // the 11·768 error-combination column, 3 waves/SIMD); 3: 256-thread blocks without the deferred
-    // combinations (6 stage reductions per step, 42 KB of LDS: 3 blocks per CU); 4: 256-thread blocks
-    // with them (65 KB: 2 blocks per CU)
-    const int split_bt = rows == 2 ? 768 : 256;
-    const bool split = use_rows && rows >= 2 && Nx == 256 && hpc.ni == 256 &&
-                       B <= (int64_t)(split_bt / kWave / 2) * slab_blocks;
     // only the rows kernel combines: fixed steps (1) through A alone, adaptive steps (2) through A and the
     // μ error combination E (the caller asks for 2 with the error slab)
-    if (!use_rows || (split && rows == 3) || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2))
-        a.combine = 0;
+    if (!use_rows || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2)) a.combine = 0;
     if (combined_out) *combined_out = a.combine;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
@@ -1948,44 +1934,25 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
         for (int m = 0; m < 4; ++m) same = same && a.su_q[s][m] == a.su_q[s - 1][m];
         a.reload[s] = same ? 0 : 1;
     }
-// (dynamic LDS above 64 KB needs the per-kernel opt-in, set once per instantiation)
-#define KAN_VSPLIT_GO(KERN, BTHREADS)                                                                            \
-    do {                                                                                                         \
-        static size_t lds_set = 0;                                                                               \
-        if (lds_s > 65536 && lds_s > lds_set) {                                                                  \
-            if (hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s) != \
-                hipSuccess)                                                                                      \
-                return hipErrorInvalidValue;                                                                     \
-            lds_set = lds_s;                                                                                     \
-        }                                                                                                        \
-        hipLaunchKernelGGL(KERN, dim3(grid), dim3(BTHREADS), lds_s, st, lc, p, (const double2*)tables, hpc.ni,   \
-                           hpc.inv_w, hpc.x0, cd, co, B, a);                                                     \
-    } while (0)
 #define KAN_VSTEP(NORM, PATH, GT, NP)                                                                              \
     do {                                                                                                         \
-        if (split && NP == 2) {                                                                                  \
-            const size_t lds_s = lds + (a.combine == 2 ? (size_t)(GT + 1) * split_bt * sizeof(double) : 0);      \
-            grid = grid_for(B, split_bt / kWave / 2, slab_blocks);                                               \
-            for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
-            if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
-            if (split_bt == 768 && a.combine == 2)                                                               \
-                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 2, 2, 256, 768>), 768);                 \
-            else if (split_bt == 768)                                                                            \
-                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 0, 2, 256, 768>), 768);                 \
-            else if (a.combine == 2)                                                                             \
-                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 2, 2, 256, 256>), 256);                 \
-            else                                                                                                 \
-                KAN_VSPLIT_GO((fk_vjp_step_rows_kernel<NORM, PATH, GT, 1, 0, 2, 256, 256>), 256);                 \
-            break;                                                                                               \
-        }                                                                                                        \
         if (use_rows) {                                                                                          \
             grid = grid_for(B, kVjpBlock / kWave, slab_blocks);                                                  \
             for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
             if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
-            if (a.combine == 2)                                                                                  \
+            if (KAN_VROWS_NI && NP == 2 && hpc.ni == 256) {                                                     \
+                if (a.combine == 2)                                                                              \
+                    hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, 2, 2, 256>), dim3(grid),           \
+                                       dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,\
+                                       hpc.x0, cd, co, B, a);                                                    \
+                else                                                                                             \
+                    hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, 2, 0, 256>), dim3(grid),           \
+                                       dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,\
+                                       hpc.x0, cd, co, B, a);                                                    \
+            } else if (a.combine == 2)                                                                           \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 2>), dim3(grid),    \
-                                   dim3(kVjpBlock), lds + (size_t)(GT + 1) * kVjpBlock * sizeof(double), st, lc, p, \
-                                   (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0, cd, co, B, a);             \
+                                   dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
+                                   hpc.x0, cd, co, B, a);                                                        \
             else                                                                                                 \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 0>), dim3(grid),    \
                                    dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
@@ -2020,7 +1987,6 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     }
 #undef KAN_VSTEP_NP
 #undef KAN_VSTEP
-#undef KAN_VSPLIT_GO
     *grid_out = grid;
     return hipGetLastError();
 }

@@ -1063,7 +1063,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_GRID_RHS: return count(h->grid_ovr.rhs, "GRID_RHS", 1 << 24);
     case KANODE_OPT_GRID_VJP: return count(h->grid_ovr.vjp, "GRID_VJP", kSlabBlocks / 2);
     case KANODE_OPT_GRID_ADJ_STEP: return count(h->grid_ovr.vstep, "GRID_ADJ_STEP", kSlabBlocks / 2);
-    case KANODE_OPT_ADJ_STEP_ROWS: return count(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS", 4);
+    case KANODE_OPT_ADJ_STEP_ROWS: return flag(h->grid_ovr.vstep_rows, "ADJ_STEP_ROWS");
     case KANODE_OPT_PAIR_VJP: return flag(h->pair_vjp, "PAIR_VJP");
     case KANODE_OPT_PAIR_FUSE: return flag(h->pair_fuse, "PAIR_FUSE");
     case KANODE_OPT_PAIR_PERSIST: return flag(h->pair_persist, "PAIR_PERSIST");
@@ -1085,7 +1085,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_GRID_RHS: return h->grid_ovr.rhs;
     case KANODE_OPT_GRID_VJP: return h->grid_ovr.vjp;
     case KANODE_OPT_GRID_ADJ_STEP: return h->grid_ovr.vstep;
-    case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows;
+    case KANODE_OPT_ADJ_STEP_ROWS: return h->grid_ovr.vstep_rows ? 1 : 0;
     case KANODE_OPT_PAIR_VJP: return h->pair_vjp ? 1 : 0;
     case KANODE_OPT_PAIR_FUSE: return h->pair_fuse ? 1 : 0;
     case KANODE_OPT_PAIR_PERSIST: return h->pair_persist ? 1 : 0;
