@@ -602,10 +602,16 @@ __device__ __forceinline__ void pp_direct_dphi_sw(const Math<double>& M, const L
     dphi = dnormalize<NORM, double>(lc.norm, n) * s + (lc.use_base ? p[G] * dsw : 0.0);
 }
 
-// Two tables sharing one interval index: φ'(u) from td, swish(u) from ts.  The two Horner
-// chains run one after the other (a scheduling barrier between them) so only one table's
-// five 16-byte LDS reads are live at a time: register pressure, not latency, limits the
-// VJP kernels' occupancy.
+#ifndef KAN_VJP_SPLIT_HORNER
+#define KAN_VJP_SPLIT_HORNER 1
+#endif
+// Two tables sharing one interval index: φ'(u) from td, swish(u) from ts.  SPLITH: the two Horner
+// chains run one after the other (a scheduling barrier between them) so only one table's five 16-byte
+// LDS reads are live at a time (the adjoint-stage and adjoint-step kernels, where registers limit the
+// occupancy); otherwise the compiler interleaves the two independent chains (the standalone VJP, round 4:
+// 160 VGPRs, still 3 waves/SIMD; 1M trajectories 1539 -> 1481 us in one interleaved process,
+// profiles/r04/ab/vjp_interleaved_horner_ab.txt; the adjoint rows step measured 58.1 -> 58.6 us with it).
+template <bool SPLITH = (KAN_VJP_SPLIT_HORNER != 0)>
 __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const double2* __restrict__ ts, int ni,
                                          double inv_w, double x0, double u, double& d, double& s) {
     const double x = ::fma(u, inv_w, x0);
@@ -629,9 +635,7 @@ __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const d
         y = ::fma(y, t, a0.y);
         y = ::fma(y, t, a0.x);
     }
-#if KAN_VJP_SPLIT_HORNER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    if constexpr (SPLITH) __builtin_amdgcn_sched_barrier(0);
     {
         const double2 b8 = b[4 * ni], b6 = b[3 * ni], b4 = b[2 * ni], b2 = b[ni], b0 = b[0];
         z = ::fma(b8.y, t, b8.x);
@@ -649,9 +653,6 @@ __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const d
     return in && (y == y) && (z == z);
 }
 
-#ifndef KAN_VJP_R2
-#define KAN_VJP_R2 0
-#endif
 // One point of the pullback: returns λ φ'(x); accumulates the dC moments and dW.
 // With v_j = λ E0 R^j and the knot correction kc_j = K_j (1 + τ' e_j + τ'² e_j²/2):
 //     Σ_points λ B_j = K_j (S0_j + e_j S1_j + e_j²/2 S2_j),
@@ -660,14 +661,14 @@ __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const d
 // next to the rest of the kernel).  S1/S2 carry weights |τ' e_j| <= 1.1e-6 and
 // (τ' e_j)²/2 <= 6e-13 of S0 (G=10), so they run in fp32 on their own fp32 power
 // chain: their rounding reaches dC at < 1e-13 relative.
-template <int NORM, int PATH, int GT>
+template <int NORM, int PATH, int GT, bool SPLITH = (KAN_VJP_SPLIT_HORNER != 0)>
 __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const LayerConst& lc,
                                                const double* __restrict__ p, const RecScalars<double>& rc,
                                                const double2* __restrict__ td, const double2* __restrict__ ts,
                                                int ni, double inv_w, double x0, double x, double l,
                                                double (&S0)[GT], float (&S1)[GT], float (&S2)[GT], double& dW) {
     double dphi, sw;
-    if (__builtin_expect(!pp_eval2(td, ts, ni, inv_w, x0, x, dphi, sw), 0))
+    if (__builtin_expect(!pp_eval2<SPLITH>(td, ts, ni, inv_w, x0, x, dphi, sw), 0))
         pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, x, dphi, sw);
     dW = ::fma(l, sw, dW);
     const double n = normalize<NORM, double>(M, lc.norm, x);
@@ -684,26 +685,10 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
     const float R2 = R32 * R32;
     const kf2 R2v = {R2, R2};
 #endif
-#if KAN_VJP_R2
-    // two independent power chains (even and odd knots advanced by R²): half the dependent multiplies
-    // in a row (the knot values differ from the single chain's in the last bits)
-    const double Rsq = R * R;
-    double vo = v * R;
-#endif
 #pragma unroll
     for (int j = 0; j < GT; ++j) {
-#if KAN_VJP_R2
-        if (j & 1) {
-            S0[j] = S0[j] + vo;
-            vo = vo * Rsq;
-        } else {
-            S0[j] = S0[j] + v;
-            v = v * Rsq;
-        }
-#else
         S0[j] = S0[j] + v;
         v = v * R;
-#endif
         if constexpr (PATH == PATH_REC_CORR) {
 #if KAN_VJP_PACKED
             const float vj = (j & 1) ? vp.y : vp.x;
@@ -726,9 +711,6 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 // waves/SIMD (the latter spilling) 1740-1746 us.
 #ifndef KAN_VJP_BLOCK
 #define KAN_VJP_BLOCK 256
-#endif
-#ifndef KAN_VJP_SPLIT_HORNER
-#define KAN_VJP_SPLIT_HORNER 1
 #endif
 #ifndef KAN_VJP_UNROLL_PAIRS
 #define KAN_VJP_UNROLL_PAIRS 1
@@ -877,10 +859,10 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
                 }
             }
             if constexpr (kPairUnroll > 1) __builtin_amdgcn_sched_barrier(0);
-            const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0, S1,
+            const double x0b = pp_vjp_point<NORM, PATH, GT, STG>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.x, lk.x, S0, S1,
                                                            S2, dW);
             __builtin_amdgcn_sched_barrier(0);
-            const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.y, lk.y, S0, S1,
+            const double x1b = pp_vjp_point<NORM, PATH, GT, STG>(M, lc, p, rc, td, ts, ni, inv_w, x0, uk.y, lk.y, S0, S1,
                                                            S2, dW);
             kd2 o;
             o.x = a0 + x0b;
