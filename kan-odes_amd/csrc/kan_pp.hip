@@ -1359,8 +1359,14 @@ hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, 
     return hipGetLastError();
 }
 
-__global__ void __launch_bounds__(kBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
-    __shared__ double red[(kBlock / kWave) * 6];
+// KAN_ADJ_FIN_BLOCK threads: with 1024 the slab rows of a step kernel's grid (up to 1024 blocks) are one load
+// per slab per thread, all in flight at once
+#ifndef KAN_ADJ_FIN_BLOCK
+#define KAN_ADJ_FIN_BLOCK 256
+#endif
+constexpr int kAdjFinBlock = KAN_ADJ_FIN_BLOCK;
+__global__ void __launch_bounds__(kAdjFinBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
+    __shared__ double red[(kAdjFinBlock / kWave) * 6];
     __shared__ double sums[6];
     const int64_t q = blockIdx.x;
     if (q == P) {   // the λ error partials
@@ -1406,7 +1412,7 @@ __global__ void __launch_bounds__(kBlock) adj_finish_kernel(AdjFinish f, int64_t
 
 hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st) {
     if (f.nslab < 1 || f.nslab > 6 || P < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(adj_finish_kernel, dim3((unsigned)P + 1), dim3(kBlock), 0, st, f, P);
+    hipLaunchKernelGGL(adj_finish_kernel, dim3((unsigned)P + 1), dim3(kAdjFinBlock), 0, st, f, P);
     return hipGetLastError();
 }
 
