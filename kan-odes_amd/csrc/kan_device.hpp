@@ -57,6 +57,7 @@ struct LayerConst {
     double K[kMaxGrid];       // exp(-Δ_j²) · exp(tau_c·e_j)
     double e[kMaxGrid];       // Δ_j - j·δ
     double Dl[kMaxGrid];      // Δ_j
+    double h2[kMaxGrid];      // 0.5·e_j·e_j as the kernels form it, (0.5·e_j)·e_j: the 2nd-order correction weight
 };
 
 // Piecewise-polynomial form of a pointwise KDense(1,1,G) (kan_pp.hip): φ(u) on

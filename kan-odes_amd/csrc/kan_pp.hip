@@ -666,11 +666,14 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
                                                const double* __restrict__ p, const RecScalars<double>& rc,
                                                const double2* __restrict__ td, const double2* __restrict__ ts,
                                                int ni, double inv_w, double x0, double x, double l,
-                                               double (&S0)[GT], float (&S1)[GT], float (&S2)[GT], double& dW) {
+                                               double (&S0)[GT], float (&S1)[GT], float (&S2)[GT], double& dW,
+                                               bool init = false) {
+    // init: the moments and dW start at this point (the same bits as adding it to zeros; saves the
+    // zeroing of 30 accumulator registers per stage in the adjoint step kernels)
     double dphi, sw;
     if (__builtin_expect(!pp_eval2<SPLITH>(td, ts, ni, inv_w, x0, x, dphi, sw), 0))
         pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, x, dphi, sw);
-    dW = ::fma(l, sw, dW);
+    dW = init ? l * sw : ::fma(l, sw, dW);
     const double n = normalize<NORM, double>(M, lc.norm, x);
     double z0, E0, R, taup;
     rec_anchor<double>(M, rc, n, z0, E0, R, taup);
@@ -687,17 +690,17 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
 #endif
 #pragma unroll
     for (int j = 0; j < GT; ++j) {
-        S0[j] = S0[j] + v;
+        S0[j] = init ? v : S0[j] + v;
         v = v * R;
         if constexpr (PATH == PATH_REC_CORR) {
 #if KAN_VJP_PACKED
             const float vj = (j & 1) ? vp.y : vp.x;
-            S1[j] = fmaf(vj, t32, S1[j]);
-            S2[j] = fmaf(vj, t2, S2[j]);
+            S1[j] = init ? vj * t32 : fmaf(vj, t32, S1[j]);
+            S2[j] = init ? vj * t2 : fmaf(vj, t2, S2[j]);
             if (j & 1) vp = vp * R2v;
 #else
-            S1[j] = fmaf(v32, t32, S1[j]);
-            S2[j] = fmaf(v32, t2, S2[j]);
+            S1[j] = init ? v32 * t32 : fmaf(v32, t32, S1[j]);
+            S2[j] = init ? v32 * t2 : fmaf(v32, t2, S2[j]);
             v32 = v32 * R32;
 #endif
         }
@@ -884,7 +887,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
 #pragma unroll
     for (int j = 0; j < GT; ++j) {
         const double e = lc.e[j];
-        acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+        acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(lc.h2[j], (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
                                        : lc.K[j] * S0[j];
     }
     acc[GT] = dW;
@@ -1057,7 +1060,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #pragma unroll
         for (int j = 0; j < GT; ++j) {
             const double e = lc.e[j];
-            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(lc.h2[j], (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
                                            : lc.K[j] * S0[j];
         }
         acc[GT] = dW;
@@ -1158,14 +1161,9 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
-        double S0[GT];
+        double S0[GT];   // (set by the stage's first point; zeros for an idle wave)
         float S1[GT], S2[GT];
-#pragma unroll
-        for (int j = 0; j < GT; ++j) {
-            S0[j] = 0.0;
-            S1[j] = S2[j] = 0.0f;
-        }
-        double dW = 0.0;
+        double dW;
         const bool last = s == 5;
         const bool want_err = last && a.err_slab != nullptr;
         if (live) {
@@ -1227,7 +1225,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 __builtin_amdgcn_sched_barrier(0);
 #endif
                 const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].x, lv[k].x,
-                                                               S0, S1, S2, dW);
+                                                               S0, S1, S2, dW, k == 0);
 #if KAN_VROWS_SB
                 __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1252,11 +1250,19 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 }
             }
         }
+        else {
+#pragma unroll
+            for (int j = 0; j < GT; ++j) {
+                S0[j] = 0.0;
+                S1[j] = S2[j] = 0.0f;
+            }
+            dW = 0.0;
+        }
         double acc[GT + 1];
 #pragma unroll
         for (int j = 0; j < GT; ++j) {
             const double e = lc.e[j];
-            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(0.5 * e * e, (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
+            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(lc.h2[j], (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
                                            : lc.K[j] * S0[j];
         }
         acc[GT] = dW;

@@ -183,6 +183,7 @@ kanode_status make_layer_const(kanode_handle* h, const kanode_layer_spec& s, int
         const double D = ((double)lc.grid[j] - (double)lc.grid[0]) * sd;
         lc.Dl[j] = D;
         lc.e[j] = D - (double)j * lc.delta;
+        lc.h2[j] = 0.5 * lc.e[j] * lc.e[j];   // (kan_pp.hip's moment transforms read it; same order, same bits)
         const long double DL = D;
         lc.K[j] = (double)(std::exp(-DL * DL) * std::exp((long double)lc.tau_c * (long double)lc.e[j]));
         emax = std::max(emax, std::fabs(lc.e[j]));
