@@ -431,6 +431,18 @@ def surrogate_bench(dev, with_cpu: bool, only: str | None = None, reps: int = 3)
             tc = O.bench_chain(specs, p_np, u0, 20, 1) / 20
             o.update({"cpu_rhs_us": tc * 1e6, "cpu_cores": 1, "cpu_kind": "port (oracle chain, C)",
                       "gpu_vs_cpu_rhs": tc * 1e6 / t_rhs})
+            # one training iteration on the CPU: the C epoch port (oracle/cpu_epoch.c; Tsit5 + InterpolatingAdjoint
+            # + Adam over the oracle chain, pinned to the Python driver by tests/test_cpu_epoch.py), one core, the
+            # same problem; a bounded sample (about a second per repetition): median of 3
+            tg = np.ascontiguousarray(np.broadcast_to(0.9 * u0, (len(saveat), B, N)))
+            cs = []
+            for _ in range(3):
+                *_, cst, csec = O.chain_epoch(specs, p_np, u0, tspan[1], saveat, tg, eta=eta)
+                cs.append(csec)
+            o.update({"cpu_train_iteration_ms": float(np.median(cs)) * 1e3,
+                      "cpu_train_steps": [cst["naccept"], cst["adjoint_naccept"]],
+                      "cpu_train_sample": "median of 3 repetitions, one core",
+                      "gpu_vs_cpu_train": float(np.median(cs)) * 1e3 / it_ms})
         out[name] = o
     return out
 

@@ -260,7 +260,7 @@ static int run_epoch(epoch_ctx* cp, double* p, const double* u0, double T, const
     epoch_ctx c = *cp;
     const int64_t n = c.n, P = c.P;
     const double beta1 = 7.0 / 50.0, beta2 = 2.0 / 25.0, gamma = 0.9, qmin = 0.2, qmax = 10.0, qoldinit = 1e-4;
-    if (n_save > 64) return -2;
+    if (n_save < 1) return -2;
     double* buf = malloc(sizeof(double) * n * 24);
     double* pred = malloc(sizeof(double) * n * n_save);
     dense_rec rec = {0, 0, NULL, NULL, NULL, NULL};
@@ -289,14 +289,14 @@ static int run_epoch(epoch_ctx* cp, double* p, const double* u0, double T, const
     double* emu = malloc(sizeof(double) * P);
     double* skm = malloc(sizeof(double) * P);
     memset(lam, 0, sizeof(double) * n);
-    int32_t used[64] = {0};
+    int32_t* used = calloc((size_t)n_save, sizeof(int32_t));   /* (the surrogates have 201 saveat stops) */
+    double* stops = malloc(sizeof(double) * ((size_t)n_save + 1));
     const double eps = 1e-12 * fmax(1.0, fabs(T));
     for (int32_t j = 0; j < n_save; ++j)
         if (fabs(saveat[j] - T) <= 0.0 && !used[j]) {   /* the jump at tf sets the initial λ */
             for (int64_t i = 0; i < n; ++i) lam[i] += g[j * n + i];
             used[j] = 1;
         }
-    double stops[65];
     int nst = 0;
     for (int32_t j = n_save - 1; j >= 0; --j)     /* interior saveat times in τ = T - t, ascending */
         if (!used[j] && saveat[j] > eps && saveat[j] < T - eps) {
@@ -401,6 +401,7 @@ static int run_epoch(epoch_ctx* cp, double* p, const double* u0, double T, const
     *loss_out = loss;
     stats[0] = nacc; stats[1] = nrej; stats[2] = aacc; stats[3] = arej;
     free(buf); free(pred); free(g); free(km); free(mu); free(munew); free(emu); free(skm);
+    free(used); free(stops);
     free(rec.t); free(rec.dt); free(rec.u); free(rec.k);
     return 0;
 }

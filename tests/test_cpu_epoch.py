@@ -78,3 +78,30 @@ def test_c_chain_epoch_matches_python_driver(adaptive):
                        kanode.Tsit5Options(abstol=1e-8, reltol=1e-8))
     assert st2["naccept"] == ref.stats["naccept"]
     assert np.max(np.abs(pred - ref.u.numpy())) <= 1e-12
+
+
+def test_c_chain_epoch_wide_surrogate_shape():
+    """The surrogate comparator (bench.py surrogates' CPU training iteration): a full-field chain
+    KAN [N, H, N] (the Burgers/Schrödinger surrogate form, Burgers_Surrogate.jl:85-97) at a small N,
+    several ICs and saveat stops: the C epoch against Trainer + InterpolatingAdjoint over OracleChainRHS."""
+    from oracle.oracle_rhs import OracleChainRHS
+    N, H, G, B = 24, 4, 5, 3
+    specs = [O.LayerSpec(N, H, G, "softsign"), O.LayerSpec(H, N, G, "softsign")]
+    chain = kanode.Chain(kanode.KDense(N, H, G, normalizer="softsign"), kanode.KDense(H, N, G, normalizer="softsign"))
+    p0 = chain.setup(np.random.default_rng(6))[0].astype(np.float64)
+    x = np.linspace(-1.0, 1.0, N)
+    u0 = np.stack([-np.sin(np.pi * x) + 0.1 * k * np.sin(2 * np.pi * x) for k in range(B)])
+    saveat = [0.05 * i for i in range(7)]
+    T = 0.3
+    target = np.ascontiguousarray(np.broadcast_to(0.9 * u0, (len(saveat), B, N)))
+    loss, grad, p_new, st, secs = O.chain_epoch(specs, p0, u0, T, saveat, target, abstol=1e-8, reltol=1e-8,
+                                                adaptive=True, eta=1e-2)
+    tr = kanode.Trainer(OracleChainRHS(specs), torch.as_tensor(u0), (0.0, T), saveat, torch.as_tensor(target),
+                        torch.as_tensor(p0), eta=1e-2, solver=kanode.Tsit5Options(abstol=1e-8, reltol=1e-8),
+                        sensealg="interpolating_adjoint")
+    lt, gt, sol = tr.loss_and_grad()
+    assert st["naccept"] == sol.stats["naccept"] and st["adjoint_naccept"] == sol.stats["adjoint"]["naccept"]
+    assert abs(loss - lt.item()) <= 1e-12 * abs(loss)
+    assert np.max(np.abs(grad - gt.numpy())) <= 1e-10 * np.max(np.abs(gt.numpy()))
+    tr.step()
+    assert np.max(np.abs(p_new - tr.p.numpy())) <= 1e-12 * np.max(np.abs(p0))
