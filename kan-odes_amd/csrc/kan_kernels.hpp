@@ -55,6 +55,22 @@ __device__ __forceinline__ void stage_ld(const StageArgs<T>& sa, const T* safe, 
 }
 template <typename T>
 hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_t n, hipStream_t st);
+// The saveat values that fall in one accepted Tsit5 step in one launch (round 4; kanode_solve.cpp solve_t):
+// saveat j (< nsv) is y_j = u + Σ_m w[j][m] k_m in stage_lincomb_kernel's fma order, or u_new itself when bit j
+// of `exact` is set (a saveat on the step's end), written to dst + j·n.  A surrogate forward step holds up to
+// ~40 saveat points (Burgers: 200 stops over 5 steps), each of which was one launch.
+constexpr int kSaveatPerLaunch = 48;
+template <typename T> struct SaveatStep {
+    const T* u;
+    const T* u_new;
+    const T* k[7];
+    T* dst;
+    uint64_t exact;
+    int32_t nk, nsv;
+    double w[kSaveatPerLaunch][7];
+};
+template <typename T>
+hipError_t launch_saveat_step(const SaveatStep<T>& a, int64_t n, hipStream_t st);
 // per-block partials into `slab` (<= slab_blocks rows), then out[0] = ordered total
 template <typename T>
 hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageArgs<T>& sa, double* slab,

@@ -121,6 +121,37 @@ hipError_t launch_stage_lincomb(const T* u, const StageArgs<T>& sa, T* y, int64_
 }
 
 template <typename T>
+__global__ void __launch_bounds__(kBlock) saveat_step_kernel(SaveatStep<T> a, int64_t n) {
+    const int j = blockIdx.y;
+    T* __restrict__ y = a.dst + (int64_t)j * n;
+    const bool copy = (a.exact >> j) & 1ull;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        if (copy) {
+            y[i] = a.u_new[i];
+            continue;
+        }
+        T kv[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) kv[m] = (m < a.nk ? a.k[m] : a.u)[i];   // (all loads first)
+        T v = a.u[i];
+#pragma unroll
+        for (int m = 0; m < 7; ++m)
+            if (m < a.nk) v = kfma<T>((T)a.w[j][m], kv[m], v);
+        y[i] = v;
+    }
+}
+
+template <typename T>
+hipError_t launch_saveat_step(const SaveatStep<T>& a, int64_t n, hipStream_t st) {
+    if (a.nsv < 1 || a.nsv > kSaveatPerLaunch || a.nk < 0 || a.nk > 7) return hipErrorInvalidValue;
+    const int grid = grid_for(n, kBlock, kGridCap);
+    hipLaunchKernelGGL((saveat_step_kernel<T>), dim3(grid, a.nsv), dim3(kBlock), 0, st, a, n);
+    return hipGetLastError();
+}
+template hipError_t launch_saveat_step<double>(const SaveatStep<double>&, int64_t, hipStream_t);
+template hipError_t launch_saveat_step<float>(const SaveatStep<float>&, int64_t, hipStream_t);
+
+template <typename T>
 hipError_t launch_stage_error(const T* u, const T* y, const T* du, const StageArgs<T>& sa, double* slab,
                               int slab_blocks, double* out, int64_t n, hipStream_t st) {
     const int grid = grid_for(n, kBlock, slab_blocks);

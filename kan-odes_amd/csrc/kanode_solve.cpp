@@ -488,24 +488,42 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             qold = std::max(EEst, o.qoldinit);
         }
         const double tn = t + dt;
+        // the saveat values in this step: one launch for all of them (the same arithmetic as one
+        // stage_lincomb / copy each; kan::SaveatStep)
+        kan::SaveatStep<T> sv{};
+        sv.u = (const T*)s->u(step);
+        sv.u_new = (const T*)s->u(step + 1);
+        sv.nk = s->qform ? 4 : 7;
+        for (int j = 0; j < sv.nk; ++j) sv.k[j] = (const T*)(s->qform ? s->q(step, j + 1) : ks[j]);
+        auto flush_sv = [&]() -> kanode_status {
+            if (sv.nsv == 0) return KANODE_OK;
+            SOLVE_HIP(h, kan::launch_saveat_step<T>(sv, s->n, st));
+            sv.nsv = 0;
+            sv.exact = 0;
+            return KANODE_OK;
+        };
         while (si < n_save && saveat[si] <= tn + 1e-12 * std::max(1.0, std::fabs(tn))) {
             const double tsv = saveat[si];
-            void* dst = (char*)u_save + si * sb;
+            if (sv.nsv == 0) sv.dst = (T*)((char*)u_save + si * sb);
+            const int jv = sv.nsv;
             if (std::fabs(tsv - tn) <= 1e-12 * std::max(1.0, std::fabs(tn))) {
-                SOLVE_HIP(h, hipMemcpyAsync(dst, s->u(step + 1), sb, hipMemcpyDeviceToDevice, st));
+                sv.exact |= 1ull << jv;
             } else if (s->qform) {
                 const double th = (tsv - t) / dt;
-                const double w[4] = {th, th * th, th * th * th, th * th * th * th};
-                const void* qs[4] = {s->q(step, 1), s->q(step, 2), s->q(step, 3), s->q(step, 4)};
-                SOLVE_TRY(lincomb<T>(h, s->u(step), 4, qs, w, dst, s->n, st));
+                sv.w[jv][0] = th;
+                sv.w[jv][1] = th * th;
+                sv.w[jv][2] = th * th * th;
+                sv.w[jv][3] = th * th * th * th;
             } else {
                 double w[7];
                 interp_weights((tsv - t) / dt, w);
-                for (int j = 0; j < 7; ++j) w[j] *= dt;
-                SOLVE_TRY(lincomb<T>(h, s->u(step), 7, ks, w, dst, s->n, st));
+                for (int j = 0; j < 7; ++j) sv.w[jv][j] = w[j] * dt;
             }
+            ++sv.nsv;
             ++si;
+            if (sv.nsv == kan::kSaveatPerLaunch) SOLVE_TRY(flush_sv());
         }
+        SOLVE_TRY(flush_sv());
         s->ts.push_back(t);
         s->dts.push_back(dt);
         t = tn;

@@ -763,3 +763,30 @@ def test_persistent_pair_adjoint_matches_launch_path(N, G, B, S, adaptive):
     bar = 1e-9 if adaptive else 1e-11
     assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
     assert (gu1 - gu0).abs().max().item() <= bar * gu0.abs().max().item()
+
+
+
+@pytest.mark.parametrize("name", ["fk256", "lv64", "lv32"])
+def test_dense_saveat_batches_per_step(name):
+    """Many saveat stops per accepted step (round 4: a step's saveat values are one launch,
+    kan::SaveatStep, at most 48 stops per launch): 4001 stops for LV (2000 per unit time, steps of
+    ~0.05-0.2 hold 100+, so the batch flushes) and 601 over a short FK256 span, plus stops that land on step ends (copies of u_new).  Against
+    the Python driver (one lincomb per stop): same steps, values to rounding.  lv64 / lv32 with the
+    one-workgroup solve off (the host loop, K-form interpolation); fk256 on its fused step (Q form)."""
+    rhs, u0, p, tspan, _ = _setup(name)
+    tspan, n = ((0.0, 2.0), 4000) if name.startswith("lv") else ((0.0, 0.05), 600)
+    ts = [tspan[0] + (tspan[1] - tspan[0]) * i / n for i in range(n + 1)]
+    f64 = u0.dtype == torch.float64
+    opt = kanode.Tsit5Options(abstol=1e-8 if f64 else 1e-6, reltol=1e-7 if f64 else 1e-4)
+    with rhs.hd.options(fused_solve=0):
+        nat = kanode.solve(rhs, u0, tspan, p, ts, opt)
+        py = kanode.solve(rhs, u0, tspan, p, ts, dataclasses.replace(opt, native=False))
+    assert nat.u.shape == py.u.shape == (n + 1,) + tuple(u0.shape)
+    assert n > 4 * nat.stats["naccept"]                      # several stops per step
+    scale = max(1.0, py.u.abs().max().item())
+    if f64:
+        assert nat.stats["naccept"] == py.stats["naccept"]
+        assert (nat.u - py.u).abs().max().item() <= max(1e-11, 1e-3 * opt.reltol) * scale
+    else:
+        assert abs(nat.stats["naccept"] - py.stats["naccept"]) <= 2
+        assert (nat.u - py.u).abs().max().item() <= 20 * opt.reltol * scale
