@@ -174,6 +174,12 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     hidden pre-activations per step and one of the hidden cotangents per adjoint stage between
  *     workgroups, μ and its stage vectors resident in LDS, the step control on the device; other
  *     shapes take the launch-per-stage path.  Same algorithm; sums in another fixed order.
+ *   KANODE_OPT_ADJ_FUSED_FINISH (default 0): 1 = an adaptive Fisher-KPP adjoint step on the rows
+ *     kernel (ADJ_STEP_ROWS, >= 1 + P workgroups) finishes inside that launch: the last 1 + P
+ *     workgroups to arrive each sum one parameter's stage rows (or the λ error partials) and write
+ *     μ_new, kμ_7 and the error terms in the finish kernel's order (bitwise equal); 0 = the separate
+ *     finish launch per step.  Measured equal on the adaptive epoch (the finish's cost is its memory
+ *     round trips, not its launch), so the simpler path is the default.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -188,7 +194,8 @@ typedef enum {
     KANODE_OPT_PAIR_VJP = 9,
     KANODE_OPT_PAIR_FUSE = 10,
     KANODE_OPT_PAIR_PERSIST = 11,
-    KANODE_OPT_PAIR_PERSIST_S = 12
+    KANODE_OPT_PAIR_PERSIST_S = 12,
+    KANODE_OPT_ADJ_FUSED_FINISH = 13
 } kanode_option;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);

@@ -137,7 +137,19 @@ __device__ __forceinline__ void rs_step(T (&w)[16], int lane, int& base, int& cn
 // Sum `n` (<= N) per-thread values across the block into out[0..n): a wave reduce-scatter
 // (3 <= N <= 16; wave_sum per value otherwise), then the wave partials summed in wave order (fixed
 // order, so the result is bitwise reproducible).  `red` is LDS of >= (blockDim/64)*N elements.
-template <typename T, int N>
+// Agent-scope relaxed 64-bit store / load (sc1: visible across the XCDs' L2s without a cache flush), for
+// hand-offs between workgroups of one launch (cdna_hip_programming.md Guideline 16)
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// AGENT: the sums are stored with st_agent (another workgroup of the same launch reads them)
+template <typename T, int N, bool AGENT = false>
 __device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* out) {
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
@@ -162,7 +174,8 @@ __device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* 
     for (int q = threadIdx.x; q < n; q += blockDim.x) {
         T s = red[q];
         for (int w = 1; w < nw; ++w) s += red[w * n + q];
-        out[q] = s;
+        if constexpr (AGENT) st_agent(out + q, s);
+        else out[q] = s;
     }
     __syncthreads();
 }

@@ -152,49 +152,6 @@ hipError_t launch_fk_vjp_stage_pp(const PPConst& hpc, const LayerConst& hlc, con
 // One InterpolatingAdjoint step (six stages) of the Fisher-KPP table path in one launch
 // (fk_vjp_step_pp_wave_kernel); the dense output must be in Q form.  slab_base receives the six
 // stages' [grid][P] moment rows and then the [grid] error partials; grid_out the grid.
-struct AdjStepArgs {
-    double* kl[7];             // kλ_1 (FSAL, read) .. kλ_7 (written by stage s into kl[s + 1])
-    double a[6][6];            // h·a_sj
-    const double* su_u[6];     // u_i of the forward step holding stage s
-    const double* su_q[6][4];  // its Q_1..Q_4
-    double su_c[6][4];         // θ_s^m
-    double ec[7];              // h·btilde (stage 6 error)
-    double abstol, reltol;
-    const double* lam;
-    double* lam_out;
-    double* slab[6];           // per stage: [grid][P] moment rows
-    double* err_slab;          // [grid] (null: no error)
-    int32_t reload[6];         // (set by the launcher) stage s reads u_i, Q_m other than stage s-1's
-    // combine (fixed step): stages 0..4 are not reduced one by one; each thread accumulates
-    // A = Σ_{s<5} a[5][s+1]·moments_s and the block rows of A go to slab[0], stage 5's (kμ_7, the
-    // next step's FSAL kμ_1) to slab[5]: 2 block reductions per step instead of 6.  Only the rows
-    // kernel combines; the launcher clears it otherwise.
-    int32_t combine;
-};
-hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
-                                 const double* p, double* tables, double cd, double co, int Nx,
-                                 const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
-                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true,
-                                 int* combined_out = nullptr);
-constexpr int kMaxFinishJobs = 8;
-struct FinishJob {
-    const double* slab;
-    const double* err_slab;
-    double* dp;
-    double* err_out;
-    int64_t nblk;
-    int32_t assign;
-    int32_t pad;
-    // base != null: dp[q] = fma(1, Σ, fma(coef, other[q], base[q])) -- a two-term stage_lincomb of
-    // (base; other, Σ) in its own order, so the μ update of a combined adjoint step needs no launch
-    const double* base;
-    const double* other;
-    double coef;
-};
-struct FinishJobs {
-    FinishJob j[kMaxFinishJobs];
-};
-hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, hipStream_t st);
 // The finish of an ADAPTIVE Fisher-KPP adjoint step in one launch (kan_pp.hip adj_finish_kernel):
 // block q < P forms the stage sums S_i[q] = Σ_b slab_i[b·P + q] (i < nslab, one pass, fixed order),
 //     μ_new[q] = fma(1, Σ_i ca_i S_i, fma(a0, km1[q], μ[q]))       (μ + h Σ_j a6_j kμ_j)
@@ -216,6 +173,55 @@ struct AdjFinish {
     const double* err_slab;
     double* out;
 };
+struct AdjStepArgs {
+    double* kl[7];             // kλ_1 (FSAL, read) .. kλ_7 (written by stage s into kl[s + 1])
+    double a[6][6];            // h·a_sj
+    const double* su_u[6];     // u_i of the forward step holding stage s
+    const double* su_q[6][4];  // its Q_1..Q_4
+    double su_c[6][4];         // θ_s^m
+    double ec[7];              // h·btilde (stage 6 error)
+    double abstol, reltol;
+    const double* lam;
+    double* lam_out;
+    double* slab[6];           // per stage: [grid][P] moment rows
+    double* err_slab;          // [grid] (null: no error)
+    int32_t reload[6];         // (set by the launcher) stage s reads u_i, Q_m other than stage s-1's
+    // combine (fixed step): stages 0..4 are not reduced one by one; each thread accumulates
+    // A = Σ_{s<5} a[5][s+1]·moments_s and the block rows of A go to slab[0], stage 5's (kμ_7, the
+    // next step's FSAL kμ_1) to slab[5]: 2 block reductions per step instead of 6.  Only the rows
+    // kernel combines; the launcher clears it otherwise.
+    int32_t combine;
+    // fin_ctr non-null (combine = 2): the step's finish runs inside the rows kernel -- the last P + 1
+    // workgroups to arrive (fin_ctr[0] counts arrivals, fin_ctr[1] finishers; both back to 0 at the end)
+    // each do one block of adj_finish_kernel's work on `fin` in its order (bitwise the same results), so
+    // no finish launch follows the step.  The launcher fills fin.slab / err_slab / nblk / nslab / k7.
+    unsigned* fin_ctr;
+    AdjFinish fin;
+};
+hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                 const double* p, double* tables, double cd, double co, int Nx,
+                                 const AdjStepArgs& a, double* slab_base, int slab_blocks, int64_t B, int* grid_out,
+                                 hipStream_t st, bool build, int grid_ovr = 0, bool rows = true,
+                                 int* combined_out = nullptr, bool* fused_finish_out = nullptr);
+constexpr int kMaxFinishJobs = 8;
+struct FinishJob {
+    const double* slab;
+    const double* err_slab;
+    double* dp;
+    double* err_out;
+    int64_t nblk;
+    int32_t assign;
+    int32_t pad;
+    // base != null: dp[q] = fma(1, Σ, fma(coef, other[q], base[q])) -- a two-term stage_lincomb of
+    // (base; other, Σ) in its own order, so the μ update of a combined adjoint step needs no launch
+    const double* base;
+    const double* other;
+    double coef;
+};
+struct FinishJobs {
+    FinishJob j[kMaxFinishJobs];
+};
+hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, hipStream_t st);
 hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st);
 template <typename T>
 hipError_t launch_kd_fwd_col(const LayerConst& hlc, const LayerConst* lc, const T* p, const T* x, T* y, int64_t K,

@@ -42,14 +42,7 @@ constexpr int kPAMaxXW = kPairAdjXW;    // exchange width cap (6·H·B of a step
 constexpr int kPALd = 16;              // exchange loads in flight per thread
 constexpr unsigned kPASpinMax = 1u << 22;   // a few seconds: far beyond any legitimate wait
 
-__device__ __forceinline__ void st_agent(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_agent(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
+// (st_agent / ld_agent: kan_common.hpp)
 
 // All nwg workgroups publish `cnt` values (vals[0..cnt) in LDS) as exchange e, then every workgroup
 // forms out[q] = Σ_{w = 0..nwg-1} partial_w[q] in that order (the same bits everywhere).

@@ -1101,6 +1101,128 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_NI
 #define KAN_VROWS_NI 1
 #endif
+// KAN_ADJ_FIN_BLOCK threads: with 1024 the slab rows of a step kernel's grid (up to 1024 blocks) are one load
+// per slab per thread, all in flight at once
+#ifndef KAN_ADJ_FIN_BLOCK
+#define KAN_ADJ_FIN_BLOCK 256
+#endif
+constexpr int kAdjFinBlock = KAN_ADJ_FIN_BLOCK;
+// Block q of the adaptive adjoint step's finish (adj_finish_kernel; q == P: the λ error partials).  AG: the
+// rows were stored by other workgroups of the running launch (the rows kernel's fused finish) and are read
+// with agent-scope loads.  The order depends only on blockDim, so both callers give the same bits.
+template <bool AG>
+__device__ __forceinline__ double fin_ld(const double* p) {
+    if constexpr (AG) return ld_agent(p);
+    else return *p;
+}
+template <bool AG>
+__device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, int64_t q, double* red, double* sums) {
+    // four of each thread's rows per pass, all loads issued before the adds (same order of the adds)
+    const int64_t bs = blockDim.x;
+    if (q == P) {   // the λ error partials
+        double s = 0.0;
+        int64_t b = threadIdx.x;
+        for (; b + 3 * bs < f.nblk; b += 4 * bs) {
+            double v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fin_ld<AG>(f.err_slab + b + r * bs);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += v[r];
+        }
+        for (; b < f.nblk; b += bs) s += fin_ld<AG>(f.err_slab + b);
+        const double v[1] = {s};
+        block_sum_to<double, 1>(v, 1, red, sums);
+        __syncthreads();
+        if (threadIdx.x == 0) f.out[0] = sums[0];
+        return;
+    }
+    double acc[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[i] = 0.0;
+    int64_t b = threadIdx.x;
+    if (f.nslab <= 3) {
+        for (; b + 3 * bs < f.nblk; b += 4 * bs) {
+            double v[4][3];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) v[r][i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + (b + r * bs) * P + q) : 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) acc[i] += v[r][i];
+        }
+    }
+    for (; b < f.nblk; b += bs) {
+        double v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v[i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + b * P + q) : 0.0;   // all loads first
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[i] += v[i];
+    }
+    block_sum_to<double, 6>(acc, f.nslab, red, sums);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double cm = 0.0, ce = 0.0, k7 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (i < f.nslab) {
+                cm = ::fma(f.ca[i], sums[i], cm);
+                ce = ::fma(f.ce[i], sums[i], ce);
+                if (i == f.k7) k7 = sums[i];
+            }
+        }
+        const double m0 = f.mu[q], k1 = f.km1[q];
+        const double mn = ::fma(1.0, cm, ::fma(f.a0, k1, m0));
+        f.mu_new[q] = mn;
+        f.km7[q] = k7;
+        const double e = ::fma(f.e0, k1, ce);
+        const double r = e / ::fma(f.reltol, fmax(kabs(m0), kabs(mn)), f.abstol);
+        f.out[1 + q] = r * r;
+    }
+}
+
+// The rows kernel's fused finish (AdjStepArgs::fin_ctr): every workgroup has stored its rows (agent-scope
+// stores) and arrives; the last P + 1 to arrive wait for the rest (the one arriving last does not wait) and
+// each runs one block of the finish.  Every wait is bounded: on a time-out the terms are not written and the
+// host's wait on them fails when the stream drains.  The finishers count themselves out; the last one puts
+// both counters back to zero for the next launch.
+constexpr unsigned kFinSpinMax = 1u << 22;
+__device__ __forceinline__ void rows_fused_finish(const AdjFinish& f, unsigned* ctr, int64_t P) {
+    __shared__ double fred[(kVjpBlock / kWave) * 6];
+    __shared__ double fsums[6];
+    __shared__ unsigned farr;
+    __shared__ int fok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's row stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) farr = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned G = gridDim.x;
+    const unsigned back = G - 1u - farr;   // 0: the last to arrive
+    if (back > (unsigned)P) return;
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (unsigned spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G; ++spins) {
+            if (spins > kFinSpinMax) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        fok = ok;
+    }
+    __syncthreads();
+    if (fok) adj_finish_block<true>(f, P, P - (int64_t)back, fred, fsums);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned d = __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == (unsigned)P) {
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int NORM, int PATH, int GT, int NP, int CMB, int NI = 0>
 __global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
 fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
@@ -1283,24 +1405,28 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
             for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
         } else {
-            block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+            block_sum_to<double, GT + 1, CMB == 2>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
         }
 #endif
     }
     if (combine) {
         __syncthreads();   // red is reused
-        block_sum_to<double, GT + 1>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
+        block_sum_to<double, GT + 1, CMB == 2>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
     }
     if constexpr (CMB == 2) {
         double ce[GT + 1];
 #pragma unroll
         for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
         __syncthreads();
-        block_sum_to<double, GT + 1>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
+        block_sum_to<double, GT + 1, true>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
     }
     if (a.err_slab) {
         const double v[1] = {eacc};
-        block_sum_to<double, 1>(v, 1, red, a.err_slab + blockIdx.x);
+        block_sum_to<double, 1, CMB == 2>(v, 1, red, a.err_slab + blockIdx.x);
+    }
+    if constexpr (CMB == 2) {
+        static_assert(kVjpBlock == kAdjFinBlock, "the fused finish runs adj_finish_kernel's blocks in its order");
+        if (a.fin_ctr) rows_fused_finish(a.fin, a.fin_ctr, P);
     }
 }
 
@@ -1365,55 +1491,10 @@ hipError_t launch_vjp_finish_jobs(const FinishJobs& jobs, int njobs, int64_t P, 
     return hipGetLastError();
 }
 
-// KAN_ADJ_FIN_BLOCK threads: with 1024 the slab rows of a step kernel's grid (up to 1024 blocks) are one load
-// per slab per thread, all in flight at once
-#ifndef KAN_ADJ_FIN_BLOCK
-#define KAN_ADJ_FIN_BLOCK 256
-#endif
-constexpr int kAdjFinBlock = KAN_ADJ_FIN_BLOCK;
 __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_kernel(AdjFinish f, int64_t P) {
     __shared__ double red[(kAdjFinBlock / kWave) * 6];
     __shared__ double sums[6];
-    const int64_t q = blockIdx.x;
-    if (q == P) {   // the λ error partials
-        double s = 0.0;
-        for (int64_t b = threadIdx.x; b < f.nblk; b += blockDim.x) s += f.err_slab[b];
-        const double v[1] = {s};
-        block_sum_to<double, 1>(v, 1, red, sums);
-        __syncthreads();
-        if (threadIdx.x == 0) f.out[0] = sums[0];
-        return;
-    }
-    double acc[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) acc[i] = 0.0;
-    for (int64_t b = threadIdx.x; b < f.nblk; b += blockDim.x) {
-        double v[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) v[i] = i < f.nslab ? f.slab[i][b * P + q] : 0.0;   // all loads first
-#pragma unroll
-        for (int i = 0; i < 6; ++i) acc[i] += v[i];
-    }
-    block_sum_to<double, 6>(acc, f.nslab, red, sums);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double cm = 0.0, ce = 0.0, k7 = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            if (i < f.nslab) {
-                cm = ::fma(f.ca[i], sums[i], cm);
-                ce = ::fma(f.ce[i], sums[i], ce);
-                if (i == f.k7) k7 = sums[i];
-            }
-        }
-        const double m0 = f.mu[q], k1 = f.km1[q];
-        const double mn = ::fma(1.0, cm, ::fma(f.a0, k1, m0));
-        f.mu_new[q] = mn;
-        f.km7[q] = k7;
-        const double e = ::fma(f.e0, k1, ce);
-        const double r = e / ::fma(f.reltol, fmax(kabs(m0), kabs(mn)), f.abstol);
-        f.out[1 + q] = r * r;
-    }
+    adj_finish_block<false>(f, P, blockIdx.x, red, sums);
 }
 
 hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st) {
@@ -1907,7 +1988,7 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
                                  const double* p, double* tables, double cd, double co, int Nx,
                                  const AdjStepArgs& a_in, double* slab_base, int slab_blocks, int64_t B,
                                  int* grid_out, hipStream_t st, bool build, int grid_ovr, bool rows,
-                                 int* combined_out) {
+                                 int* combined_out, bool* fused_finish_out) {
     if (!fk_vjp_pp_supported(hlc, Nx)) return hipErrorInvalidValue;
     const int fns[2] = {PP_DPHI, PP_SWISH};
     hipError_t e = hipSuccess;
@@ -1922,6 +2003,9 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     // μ error combination E (the caller asks for 2 with the error slab)
     if (!use_rows || (a.err_slab && a.combine != 2) || (!a.err_slab && a.combine == 2)) a.combine = 0;
     if (combined_out) *combined_out = a.combine;
+    // the fused finish: the combined adaptive rows step with at least 1 + P workgroups
+    if (a.combine != 2 || grid_for(B, kVjpBlock / kWave, slab_blocks) < P + 1) a.fin_ctr = nullptr;
+    if (fused_finish_out) *fused_finish_out = a.fin_ctr != nullptr;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
         bool same = a.su_u[s] == a.su_u[s - 1];
@@ -1934,6 +2018,18 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
             grid = grid_for(B, kVjpBlock / kWave, slab_blocks);                                                  \
             for (int s = 0; s < 6; ++s) a.slab[s] = slab_base + (int64_t)s * grid * P;                            \
             if (a.err_slab) a.err_slab = slab_base + (int64_t)6 * grid * P;                                       \
+            if (a.fin_ctr) {                                                                                     \
+                const int which[3] = {0, 1, 5}; /* A, E, kμ_7 (as kanode_internal_fk_adjoint_step) */            \
+                for (int q = 0; q < 3; ++q) {                                                                    \
+                    a.fin.slab[q] = a.slab[which[q]];                                                            \
+                    a.fin.ca[q] = q == 0 ? 1.0 : 0.0;                                                            \
+                    a.fin.ce[q] = q == 1 ? 1.0 : 0.0;                                                            \
+                }                                                                                                \
+                a.fin.nslab = 3;                                                                                 \
+                a.fin.k7 = 2;                                                                                    \
+                a.fin.nblk = grid;                                                                               \
+                a.fin.err_slab = a.err_slab;                                                                     \
+            }                                                                                                    \
             if (KAN_VROWS_NI && NP == 2 && hpc.ni == 256) {                                                     \
                 if (a.combine == 2)                                                                              \
                     hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, 2, 2, 256>), dim3(grid),           \

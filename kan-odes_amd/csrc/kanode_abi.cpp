@@ -66,6 +66,8 @@ struct kanode_handle {
     bool pair_fuse = true;            // KANODE_OPT_PAIR_FUSE
     bool pair_persist = true;         // KANODE_OPT_PAIR_PERSIST
     int pair_persist_s = 0;           // KANODE_OPT_PAIR_PERSIST_S (0: the kernel's default)
+    bool adj_fused_finish = false;    // KANODE_OPT_ADJ_FUSED_FINISH (measured even with the finish launch)
+    unsigned* fin_ctr = nullptr;      // its two arrival counters (device, zeroed at allocation)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
     // (then both run as kd_vjp_pair_ba_kernel) or kanode_internal_vjp_flush; pair_par picks the buffers of
     // the ping-pong pairs (hidden / dot-product partials, basis store, y, λs) the next stage writes
@@ -629,7 +631,7 @@ constexpr size_t kDeferRegion = (size_t)(kSlabBlocks / 2) * (kan::kMaxGrid + 2);
 // one-launch adjoint step).  kanode_create allocates them for handles that can take that path; this
 // covers a handle whose table path was switched on later, and refuses to allocate under capture.
 kanode_status ensure_adjoint_slabs(kanode_handle* h, hipStream_t st, bool at_create = false) {
-    if (h->defer_slab && h->step_slab) return KANODE_OK;
+    if (h->defer_slab && h->step_slab && h->fin_ctr) return KANODE_OK;
     if (!at_create && is_capturing(st))
         return fail(h, KANODE_ERR_CAPTURE, "adjoint reduction slabs would be allocated during capture");
     const size_t defer = kDeferRegion * sizeof(double) * kan::kMaxFinishJobs;
@@ -638,6 +640,15 @@ kanode_status ensure_adjoint_slabs(kanode_handle* h, hipStream_t st, bool at_cre
         (!h->step_slab && hipMalloc(&h->step_slab, step) != hipSuccess)) {
         (void)hipGetLastError();
         return fail(h, KANODE_ERR_ALLOC, "adjoint reduction slabs");
+    }
+    if (!h->fin_ctr) {   // the fused finish's arrival counters: zero here, and back to zero after every step
+        if (hipMalloc(&h->fin_ctr, 2 * sizeof(unsigned)) != hipSuccess ||
+            hipMemset(h->fin_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess) {
+            (void)hipGetLastError();
+            if (h->fin_ctr) (void)hipFree(h->fin_ctr);
+            h->fin_ctr = nullptr;
+            return fail(h, KANODE_ERR_ALLOC, "adjoint finish counters");
+        }
     }
     return KANODE_OK;
 }
@@ -992,6 +1003,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->dtable) (void)hipFree(h->dtable);
     if (h->defer_slab) (void)hipFree(h->defer_slab);
     if (h->step_slab) (void)hipFree(h->step_slab);
+    if (h->fin_ctr) (void)hipFree(h->fin_ctr);
     if (h->solve_cache) kanode_solution_free(h->solve_cache);
     delete h;
 }
@@ -1072,6 +1084,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
         if (value < 0 || value > 256) return fail(h, KANODE_ERR_INVALID_ARG, "PAIR_PERSIST_S must be in [0, 256]");
         h->pair_persist_s = (int)value;
         return KANODE_OK;
+    case KANODE_OPT_ADJ_FUSED_FINISH: return flag(h->adj_fused_finish, "ADJ_FUSED_FINISH");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -1091,6 +1104,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_PAIR_FUSE: return h->pair_fuse ? 1 : 0;
     case KANODE_OPT_PAIR_PERSIST: return h->pair_persist ? 1 : 0;
     case KANODE_OPT_PAIR_PERSIST_S: return h->pair_persist_s;
+    case KANODE_OPT_ADJ_FUSED_FINISH: return h->adj_fused_finish ? 1 : 0;
     }
     return -1;
 }
@@ -1410,10 +1424,30 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
     a->err_slab = err_out ? (double*)h->step_slab : nullptr;   // relocated by the launcher
     int grid = 0, comb = 0;
     a->combine = err_out && af ? 2 : (combined != nullptr && err_out == nullptr ? 1 : 0);
+    a->fin_ctr = nullptr;
+    if (err_out && af && h->adj_fused_finish) {   // the finish inside the rows kernel (the launcher may decline)
+        a->fin_ctr = h->fin_ctr;
+        a->fin = kan::AdjFinish{};
+        a->fin.a0 = af->a6[0];
+        a->fin.e0 = af->bt[0];
+        a->fin.abstol = af->abstol;
+        a->fin.reltol = af->reltol;
+        a->fin.mu = af->mu;
+        a->fin.mu_new = af->mu_new;
+        a->fin.km1 = af->km1;
+        a->fin.km7 = af->km7;
+        a->fin.out = af->out;
+    }
+    bool fused_fin = false;
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
                                           (int)h->spec.nx, *a, (double*)h->step_slab, kSlabBlocks / 2, batch, &grid, st,
                                           table_build(h, h->built_vjp), h->grid_ovr.vstep,
-                                          h->grid_ovr.vstep_rows, &comb));
+                                          h->grid_ovr.vstep_rows, &comb, &fused_fin));
+    if (fused_fin) {   // μ_new, kμ_7 and the error terms are written by the step kernel itself
+        *af->done = true;
+        launched = true;
+        return KANODE_OK;
+    }
     kan::FinishJobs jobs{};
     double* base = (double*)h->step_slab;
     if (comb == 1) {

@@ -92,10 +92,12 @@ OPT_PAIR_VJP = 9
 OPT_PAIR_FUSE = 10
 OPT_PAIR_PERSIST = 11
 OPT_PAIR_PERSIST_S = 12
+OPT_ADJ_FUSED_FINISH = 13
 OPTIONS = {"pointwise_table": OPT_POINTWISE_TABLE, "fused_step": OPT_FUSED_STEP, "fused_solve": OPT_FUSED_SOLVE,
            "fused_solve_cap": OPT_FUSED_SOLVE_CAP, "grid_rhs": OPT_GRID_RHS, "grid_vjp": OPT_GRID_VJP,
            "grid_adj_step": OPT_GRID_ADJ_STEP, "adj_step_rows": OPT_ADJ_STEP_ROWS, "pair_vjp": OPT_PAIR_VJP,
-           "pair_fuse": OPT_PAIR_FUSE, "pair_persist": OPT_PAIR_PERSIST, "pair_persist_s": OPT_PAIR_PERSIST_S}
+           "pair_fuse": OPT_PAIR_FUSE, "pair_persist": OPT_PAIR_PERSIST, "pair_persist_s": OPT_PAIR_PERSIST_S,
+           "adj_fused_finish": OPT_ADJ_FUSED_FINISH}
 
 SIGNATURES = [
     ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),

@@ -590,6 +590,27 @@ def test_adjoint_step_rows_kernel_matches_persistent_grid(nx, B, adaptive):
         assert torch.equal(gu1, gu0)
 
 
+@pytest.mark.parametrize("nx,B", [(256, 45), (256, 512), (128, 4096)])
+def test_adjoint_fused_finish_bitwise(nx, B):
+    """KANODE_OPT_ADJ_FUSED_FINISH = 1: the adaptive rows step finishes inside its own launch (the last 1 + P
+    workgroups to arrive each run one block of adj_finish_kernel, in its order) instead of the separate finish
+    launch (the default): the same step sequence, and solution and gradients bitwise equal.  B = 45 is the
+    smallest batch with the 12 workgroups it needs (P = 11); smaller batches take the finish launch."""
+    rhs = _fk_cfg(nx, 10, "softsign")
+    u0 = t(fk_u0(nx, B, 8))
+    p0 = t(np.random.default_rng(21).uniform(-1.0, 1.0, 11))
+    opt = kanode.Tsit5Options(abstol=1e-9, reltol=1e-8)
+    tspan, ts = (0.0, 0.3), [0.0, 0.1, 0.25, 0.3]
+    assert rhs.hd.get_option("adj_fused_finish") == 0
+    s1, g1, gu1 = _solve_grad(rhs, u0, p0, tspan, ts, opt, adj_fused_finish=1)
+    s0, g0, gu0 = _solve_grad(rhs, u0, p0, tspan, ts, opt)
+    assert s1.stats["adjoint"] == s0.stats["adjoint"]
+    assert torch.equal(s1.u, s0.u) and torch.equal(g1, g0) and torch.equal(gu1, gu0)
+    # and again on the same handle (the arrival counters are back at zero after every step)
+    s2, g2, gu2 = _solve_grad(rhs, u0, p0, tspan, ts, opt, adj_fused_finish=1)
+    assert torch.equal(g2, g1) and torch.equal(gu2, gu1)
+
+
 def test_adjoint_step_rows_kernel_batch_cap():
     """Above 8192 rows (one row per wave: 4 rows x the 2048 slab blocks) the adjoint step falls back
     to the persistent-grid kernel: both settings of KANODE_OPT_ADJ_STEP_ROWS then run the same
@@ -622,7 +643,7 @@ def test_options_round_trip_and_reject_bad_values():
     hd = rhs.hd
     assert hd.get_option("fused_step") == 1 and hd.get_option("fused_solve") == 1
     assert hd.get_option("grid_rhs") == hd.get_option("grid_vjp") == hd.get_option("grid_adj_step") == 0
-    assert hd.get_option("adj_step_rows") == 1
+    assert hd.get_option("adj_step_rows") == 1 and hd.get_option("adj_fused_finish") == 0
     with hd.options(fused_step=0, grid_vjp=7):
         assert hd.get_option("fused_step") == 0 and hd.get_option("grid_vjp") == 7
     assert hd.get_option("fused_step") == 1 and hd.get_option("grid_vjp") == 0
