@@ -18,7 +18,7 @@ __global__ void __launch_bounds__(kBlock) slab_reduce_kernel(const T* __restrict
     __shared__ T red[kBlock / kWave];
     const int64_t q = blockIdx.x;
     T s = T(0);
-    for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[b * P + q];
+    s = strided_rows_sum(slab + q, nblk, P, s);
     s = wave_sum(s);
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
     __syncthreads();
@@ -776,9 +776,9 @@ chain_vjp_finish_kernel(const T* __restrict__ slab, int64_t nblk, int64_t P, T* 
     const int64_t q = blockIdx.x;
     double s = 0.0;
     if (q < P) {
-        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += (double)slab[b * P + q];
+        s = strided_rows_sum(slab + q, nblk, P, s);
     } else {
-        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += err_slab[b];
+        s = strided_rows_sum(err_slab, nblk, 1, s);
     }
     s = wave_sum(s);
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;

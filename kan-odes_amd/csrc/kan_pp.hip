@@ -1439,9 +1439,9 @@ vjp_finish_kernel(const double* __restrict__ slab, int64_t nblk, int64_t P, doub
     const int64_t q = blockIdx.x;
     double s = 0.0;
     if (q < P) {
-        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[b * P + q];
+        s = strided_rows_sum(slab + q, nblk, P, s);
     } else {
-        for (int64_t b = threadIdx.x; b < nblk; b += blockDim.x) s += err_slab[b];
+        s = strided_rows_sum(err_slab, nblk, 1, s);
     }
     s = wave_sum(s);
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
@@ -1465,9 +1465,9 @@ __global__ void __launch_bounds__(kBlock) vjp_finish_jobs_kernel(FinishJobs jobs
     if (q < P ? !jb.dp : !jb.err_out) return;
     double s = 0.0;
     if (q < P) {
-        for (int64_t b = threadIdx.x; b < jb.nblk; b += blockDim.x) s += jb.slab[b * P + q];
+        s = strided_rows_sum(jb.slab + q, jb.nblk, P, s);
     } else {
-        for (int64_t b = threadIdx.x; b < jb.nblk; b += blockDim.x) s += jb.err_slab[b];
+        s = strided_rows_sum(jb.err_slab, jb.nblk, 1, s);
     }
     s = wave_sum(s);
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
