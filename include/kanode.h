@@ -330,6 +330,24 @@ kanode_status kanode_adam_step(void* x, void* m, void* v, const void* g, int64_t
                                double eta, double beta1, double beta2, double eps, double beta1_t, double beta2_t,
                                void* stream);
 
+/* --- the data-parallel gradient all-reduce (one process per GPU) -----------------
+ * For hosts without a collective of their own (Julia, C): after kanode_adjoint_tsit5 on each rank's
+ * trajectory shard, the flat [dp; L] is SUM all-reduced in place over RCCL (xGMI inside a node), then
+ * kanode_adam_step(..., scale = 1/nranks, ...) applies the mean (the same step as kanode.Trainer with
+ * torch.distributed, LV_driver_KANODE.jl:219-291 per rank).  Rank 0 makes the unique id and the host
+ * hands its KANODE_COMM_ID_BYTES bytes to every rank (a file, MPI, an environment variable); every rank
+ * then calls kanode_comm_create with the same nranks and id and its own rank and device (collective:
+ * it returns when all ranks have joined).  The all-reduce is stream-ordered (stream = the handle's). */
+#define KANODE_COMM_ID_BYTES 128
+typedef struct kanode_comm kanode_comm;
+kanode_status kanode_comm_unique_id(uint8_t* id /* [KANODE_COMM_ID_BYTES] */);
+kanode_status kanode_comm_create(int32_t nranks, int32_t rank, const uint8_t* id, int32_t device, kanode_comm** out);
+kanode_status kanode_comm_allreduce_sum(kanode_comm* c, void* buf, int64_t count, int32_t dtype, void* stream);
+int32_t kanode_comm_size(const kanode_comm* c);
+int32_t kanode_comm_rank(const kanode_comm* c);
+const char* kanode_comm_last_error(const kanode_comm* c);   /* NULL: the last failure without a communicator */
+void kanode_comm_destroy(kanode_comm* c);
+
 /* host-pointer variants (synchronous) */
 kanode_status kanode_rhs_host(kanode_handle* h, const void* p, const void* u, void* du, int64_t batch);
 kanode_status kanode_vjp_host(kanode_handle* h, const void* p, const void* u, const void* lam, void* lam_J,

@@ -374,4 +374,39 @@ function ChainRulesCore.rrule(::typeof(solve_tsit5), h::Handle, u0::AbstractVecO
     return sol, solve_tsit5_pullback
 end
 
+# --- data-parallel training across GPUs (kanode_comm_*): one process per GPU, each with its trajectory
+# shard; after the adjoint, the flat [dp; L] (device) is SUM all-reduced over RCCL and the mean applied by
+# kanode_adam_step(scale = 1/nranks).  Rank 0 calls comm_unique_id() and the host distributes the bytes
+# (MPI.bcast, a file); every rank then calls Comm(nranks, rank, id, device) (collective).
+const COMM_ID_BYTES = 128
+function comm_unique_id()
+    id = zeros(UInt8, COMM_ID_BYTES)
+    st = ccall(sym(:kanode_comm_unique_id), Cint, (Ptr{UInt8},), id)
+    st == 0 || error("libkanode: ", unsafe_string(ccall(sym(:kanode_comm_last_error), Cstring, (Ptr{Cvoid},), C_NULL)))
+    return id
+end
+mutable struct Comm
+    ptr::Ptr{Cvoid}
+    nranks::Int
+    rank::Int
+end
+function Comm(nranks::Integer, rank::Integer, id::Vector{UInt8}, device::Integer)
+    length(id) == COMM_ID_BYTES || throw(ArgumentError("the unique id is $COMM_ID_BYTES bytes"))
+    out = Ref{Ptr{Cvoid}}(C_NULL)
+    st = ccall(sym(:kanode_comm_create), Cint, (Int32, Int32, Ptr{UInt8}, Int32, Ref{Ptr{Cvoid}}),
+               nranks, rank, id, device, out)
+    st == 0 || error("libkanode: ", unsafe_string(ccall(sym(:kanode_comm_last_error), Cstring, (Ptr{Cvoid},), C_NULL)))
+    c = Comm(out[], Int(nranks), Int(rank))
+    finalizer(x -> (x.ptr == C_NULL || ccall(sym(:kanode_comm_destroy), Cvoid, (Ptr{Cvoid},), x.ptr)), c)
+    return c
+end
+"""allreduce_sum!(c, buf, count, T; stream): buf (device, count entries of T) <- Σ over the ranks, in place."""
+function allreduce_sum!(c::Comm, buf::Ptr{Cvoid}, count::Integer, ::Type{T}; stream::Ptr{Cvoid} = C_NULL) where {T}
+    haskey(DTYPE, T) || throw(ArgumentError("the all-reduce takes Float32 or Float64, not $T"))
+    st = ccall(sym(:kanode_comm_allreduce_sum), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int32, Ptr{Cvoid}),
+               c.ptr, buf, count, DTYPE[T], stream)
+    st == 0 || error("libkanode: ", unsafe_string(ccall(sym(:kanode_comm_last_error), Cstring, (Ptr{Cvoid},), c.ptr)))
+    return buf
+end
+
 end # module

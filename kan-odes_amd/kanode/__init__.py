@@ -12,13 +12,13 @@ from .rhs import ChainRHS, FisherKPPRHS, fisher_kpp_laplacian, layer_apply, rhs_
 from .ode import Solution, Tsit5Options, solve
 from .adjoint import DenseRecord, interpolating_adjoint
 from .train import Adam, FusedAdam, Trainer, mse_loss, reg_loss
-from . import checkpoint, tp
+from . import checkpoint, comm, tp
 from .tp import GridShardedChainRHS
 
 __all__ = [
     "DenseRecord", "interpolating_adjoint",
     "KanodeError", "LIB_PATH", "lib", "KanodeHandle", "LayerCfg", "Chain", "KDense", "glorot_uniform",
     "linrange_f32", "ChainRHS", "FisherKPPRHS", "fisher_kpp_laplacian", "layer_apply", "rhs_apply",
-    "Solution", "Tsit5Options", "solve", "Adam", "FusedAdam", "Trainer", "mse_loss", "reg_loss", "checkpoint", "tp",
+    "Solution", "Tsit5Options", "solve", "Adam", "FusedAdam", "Trainer", "mse_loss", "reg_loss", "checkpoint", "comm", "tp",
     "GridShardedChainRHS",
 ]

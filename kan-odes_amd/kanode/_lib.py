@@ -131,7 +131,15 @@ SIGNATURES = [
     ("kanode_edge_activations", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),
     ("kanode_adam_step", C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_double,
                                    C.c_double, C.c_double, C.c_double, C.c_double, _P]),
+    ("kanode_comm_unique_id", C.c_int, [_P]),
+    ("kanode_comm_create", C.c_int, [C.c_int32, C.c_int32, _P, C.c_int32, C.POINTER(_P)]),
+    ("kanode_comm_allreduce_sum", C.c_int, [_P, _P, C.c_int64, C.c_int32, _P]),
+    ("kanode_comm_size", C.c_int32, [_P]),
+    ("kanode_comm_rank", C.c_int32, [_P]),
+    ("kanode_comm_last_error", C.c_char_p, [_P]),
+    ("kanode_comm_destroy", None, [_P]),
 ]
+COMM_ID_BYTES = 128
 
 _lib = None
 
