@@ -20,5 +20,5 @@ for f in kan-odes_amd/build/*.o; do
     objs="$objs $f"
   fi
 done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/bin/var/$name.so $objs
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/bin/var/$name.so $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built tools/bin/var/$name.so
