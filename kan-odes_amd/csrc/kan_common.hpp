@@ -166,9 +166,10 @@ __device__ __forceinline__ A strided_rows_sum(const T* x, int64_t n, int64_t str
     return s;
 }
 
-// AGENT: the sums are stored with st_agent (another workgroup of the same launch reads them)
+// AGENT: the sums are stored with st_agent (another workgroup of the same launch reads them); sum q goes
+// to out[q·ostride]
 template <typename T, int N, bool AGENT = false>
-__device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* out) {
+__device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* out, int64_t ostride = 1) {
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     const int nw = blockDim.x / kWave;
@@ -192,8 +193,8 @@ __device__ __forceinline__ void block_sum_to(const T (&v)[N], int n, T* red, T* 
     for (int q = threadIdx.x; q < n; q += blockDim.x) {
         T s = red[q];
         for (int w = 1; w < nw; ++w) s += red[w * n + q];
-        if constexpr (AGENT) st_agent(out + q, s);
-        else out[q] = s;
+        if constexpr (AGENT) st_agent(out + q * ostride, s);
+        else out[q * ostride] = s;
     }
     __syncthreads();
 }

@@ -164,6 +164,8 @@ struct AdjFinish {
     const double* slab[6];
     double ca[6], ce[6];
     int32_t nslab, k7;
+    int32_t tr, pad;           // tr: slab i holds its rows parameter-major, [P][nblk] (the rows kernel's
+                               // combined adaptive step), so block q reads one contiguous row of nblk
     int64_t nblk;
     double a0, e0, abstol, reltol;
     const double* mu;

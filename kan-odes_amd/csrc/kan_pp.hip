@@ -1139,6 +1139,7 @@ __device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, 
     double acc[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) acc[i] = 0.0;
+    const int64_t rs = f.tr ? 1 : P, qo = f.tr ? q * f.nblk : q;   // row b of parameter q at b·rs + qo
     int64_t b = threadIdx.x;
     if (f.nslab <= 3) {
         for (; b + 3 * bs < f.nblk; b += 4 * bs) {
@@ -1146,7 +1147,7 @@ __device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, 
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int i = 0; i < 3; ++i) v[r][i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + (b + r * bs) * P + q) : 0.0;
+                for (int i = 0; i < 3; ++i) v[r][i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + (b + r * bs) * rs + qo) : 0.0;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1156,7 +1157,7 @@ __device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, 
     for (; b < f.nblk; b += bs) {
         double v[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) v[i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + b * P + q) : 0.0;   // all loads first
+        for (int i = 0; i < 6; ++i) v[i] = i < f.nslab ? fin_ld<AG>(f.slab[i] + b * rs + qo) : 0.0;   // all loads first
 #pragma unroll
         for (int i = 0; i < 6; ++i) acc[i] += v[i];
     }
@@ -1405,20 +1406,26 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
             for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
         } else {
-            block_sum_to<double, GT + 1, CMB == 2>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
+            if constexpr (CMB == 2)   // parameter-major rows [P][grid] (AdjFinish::tr): the finish reads them coalesced
+                block_sum_to<double, GT + 1, true>(acc, P, red, a.slab[s] + blockIdx.x, gridDim.x);
+            else
+                block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
         }
 #endif
     }
     if (combine) {
         __syncthreads();   // red is reused
-        block_sum_to<double, GT + 1, CMB == 2>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
+        if constexpr (CMB == 2)
+            block_sum_to<double, GT + 1, true>(comb, P, red, a.slab[0] + blockIdx.x, gridDim.x);
+        else
+            block_sum_to<double, GT + 1>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
     }
     if constexpr (CMB == 2) {
         double ce[GT + 1];
 #pragma unroll
         for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
         __syncthreads();
-        block_sum_to<double, GT + 1, true>(ce, P, red, a.slab[1] + (int64_t)blockIdx.x * P);
+        block_sum_to<double, GT + 1, true>(ce, P, red, a.slab[1] + blockIdx.x, gridDim.x);
     }
     if (a.err_slab) {
         const double v[1] = {eacc};
@@ -2027,6 +2034,7 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
                 }                                                                                                \
                 a.fin.nslab = 3;                                                                                 \
                 a.fin.k7 = 2;                                                                                    \
+                a.fin.tr = 1;                                                                                    \
                 a.fin.nblk = grid;                                                                               \
                 a.fin.err_slab = a.err_slab;                                                                     \
             }                                                                                                    \

@@ -1486,6 +1486,7 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
             }
             f.nslab = 3;
             f.k7 = 2;
+            f.tr = 1;   // the rows kernel stores the combined rows parameter-major
         } else {
             for (int s = 0; s < 6; ++s) {
                 f.slab[s] = base + (int64_t)s * grid * P;
