@@ -213,7 +213,7 @@ struct FinishJob {
     double* err_out;
     int64_t nblk;
     int32_t assign;
-    int32_t pad;
+    int32_t tr;                // slab rows parameter-major, [P][nblk] (the rows kernel's combined steps)
     // base != null: dp[q] = fma(1, Σ, fma(coef, other[q], base[q])) -- a two-term stage_lincomb of
     // (base; other, Σ) in its own order, so the μ update of a combined adjoint step needs no launch
     const double* base;

@@ -1406,8 +1406,12 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #pragma unroll
             for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
         } else {
-            if constexpr (CMB == 2)   // parameter-major rows [P][grid] (AdjFinish::tr): the finish reads them coalesced
+            // a combined step's rows go parameter-major, [P][grid] (AdjFinish::tr, FinishJob::tr): the finish
+            // reads them coalesced
+            if constexpr (CMB == 2)
                 block_sum_to<double, GT + 1, true>(acc, P, red, a.slab[s] + blockIdx.x, gridDim.x);
+            else if (combine)
+                block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + blockIdx.x, gridDim.x);
             else
                 block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
         }
@@ -1415,10 +1419,7 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     }
     if (combine) {
         __syncthreads();   // red is reused
-        if constexpr (CMB == 2)
-            block_sum_to<double, GT + 1, true>(comb, P, red, a.slab[0] + blockIdx.x, gridDim.x);
-        else
-            block_sum_to<double, GT + 1>(comb, P, red, a.slab[0] + (int64_t)blockIdx.x * P);
+        block_sum_to<double, GT + 1, CMB == 2>(comb, P, red, a.slab[0] + blockIdx.x, gridDim.x);
     }
     if constexpr (CMB == 2) {
         double ce[GT + 1];
@@ -1472,7 +1473,7 @@ __global__ void __launch_bounds__(kBlock) vjp_finish_jobs_kernel(FinishJobs jobs
     if (q < P ? !jb.dp : !jb.err_out) return;
     double s = 0.0;
     if (q < P) {
-        s = strided_rows_sum(jb.slab + q, jb.nblk, P, s);
+        s = jb.tr ? strided_rows_sum(jb.slab + q * jb.nblk, jb.nblk, 1, s) : strided_rows_sum(jb.slab + q, jb.nblk, P, s);
     } else {
         s = strided_rows_sum(jb.err_slab, jb.nblk, 1, s);
     }

@@ -1459,6 +1459,7 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
             jb.dp = (double*)km[s];
             jb.nblk = grid;
             jb.assign = 1;
+            jb.tr = 1;   // the rows kernel stores combined rows parameter-major
             if (q == 0 && mu) {   // μ_new = μ + a61·kμ_1 + A in the same launch (A itself is not stored)
                 jb.dp = mu->mu_new;
                 jb.base = mu->mu;
