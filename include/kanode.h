@@ -180,6 +180,15 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     μ_new, kμ_7 and the error terms in the finish kernel's order (bitwise equal); 0 = the separate
  *     finish launch per step.  Measured equal on the adaptive epoch (the finish's cost is its memory
  *     round trips, not its launch), so the simpler path is the default.
+ *   KANODE_OPT_PAIR_PERSIST_MAX_WG (default 0): the persistent pair adjoint's workgroups spin on each
+ *     other, so it is launched only when all of them can be resident at once: 0 = the capacity the
+ *     device reports (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs); n > 0 = at most n (a
+ *     partitioned or shared device).  A grid above the capacity takes the launch-per-stage path.
+ *   KANODE_OPT_PAIR_PERSIST_ABORT (default 0, tests only): 1 raises the kernel's abort word at
+ *     launch, which is what an exchange time-out does (e.g. workgroups kept off the device by other
+ *     work): the adjoint then re-runs on the launch-per-stage path.
+ *   KANODE_OPT_LAST_ADJOINT (read-only): the path the handle's last kanode_adjoint_tsit5 took,
+ *     a kanode_adjoint_path value.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -195,8 +204,18 @@ typedef enum {
     KANODE_OPT_PAIR_FUSE = 10,
     KANODE_OPT_PAIR_PERSIST = 11,
     KANODE_OPT_PAIR_PERSIST_S = 12,
-    KANODE_OPT_ADJ_FUSED_FINISH = 13
+    KANODE_OPT_ADJ_FUSED_FINISH = 13,
+    KANODE_OPT_PAIR_PERSIST_MAX_WG = 14,
+    KANODE_OPT_PAIR_PERSIST_ABORT = 15,
+    KANODE_OPT_LAST_ADJOINT = 16
 } kanode_option;
+typedef enum {
+    KANODE_ADJ_NONE = 0,            /* no adjoint on this handle yet */
+    KANODE_ADJ_HOST_LOOP = 1,       /* the host-loop integrator (per-step / per-stage launches) */
+    KANODE_ADJ_CHAIN_WG = 2,        /* a small chain's whole adjoint in one workgroup (kd_chain_adjoint_kernel) */
+    KANODE_ADJ_PAIR_PERSIST = 3,    /* a surrogate pair's whole adjoint in one launch (kd_pair_adjoint_kernel) */
+    KANODE_ADJ_PAIR_FALLBACK = 4    /* that launch timed out on an exchange; re-run on the host loop */
+} kanode_adjoint_path;
 kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value);
 int64_t kanode_get_option(const kanode_handle* h, int32_t option);
 
@@ -337,7 +356,9 @@ kanode_status kanode_adam_step(void* x, void* m, void* v, const void* g, int64_t
  * torch.distributed, LV_driver_KANODE.jl:219-291 per rank).  Rank 0 makes the unique id and the host
  * hands its KANODE_COMM_ID_BYTES bytes to every rank (a file, MPI, an environment variable); every rank
  * then calls kanode_comm_create with the same nranks and id and its own rank and device (collective:
- * it returns when all ranks have joined).  The all-reduce is stream-ordered (stream = the handle's). */
+ * it returns when all ranks have joined).  Each rank needs its own GPU (RCCL refuses a second rank on a
+ * device: kanode_comm_create then fails on both ranks instead of hanging); the calling thread's current
+ * device is left as it was.  The all-reduce is stream-ordered (stream = the handle's). */
 #define KANODE_COMM_ID_BYTES 128
 typedef struct kanode_comm kanode_comm;
 kanode_status kanode_comm_unique_id(uint8_t* id /* [KANODE_COMM_ID_BYTES] */);

@@ -267,7 +267,7 @@ template <typename T> __device__ __forceinline__ void rec_anchor(const Math<T>& 
     const T E = M.exp(-p2);
     E0 = kfma<T>(-E, perr, E);                    // exp(-p2 - perr), |perr| <= ulp(p2)/2
     const T tw = z0 + z0;                         // the correction exp(2 z0 e_j) is in 2·z0
-    R = M.exp(rc.unit_delta ? tw : tw * rc.delta);
+    R = M.exp(tw * rc.delta);                     // (δ = 1 exactly on the default grids: the same bits as exp(tw))
     taup = tw - rc.tau_c;
 }
 template <typename T> __device__ __forceinline__ void rec_anchor(const Math<T>& M, const LayerConst& lc, T n, T& z0,

@@ -346,6 +346,8 @@ struct PairAdjArgs {
     unsigned* abrt;
     int64_t P;        // parameters of the chain (the error norm's count)
     int S;            // grid points per workgroup (0: 8)
+    int max_wg;       // co-resident workgroups assumed at most (0: the occupancy query's capacity)
+    int force_abort;  // tests: the abort word raised at launch (as an exchange time-out raises it)
 };
 int pair_adjoint_workgroups(const LayerConst* hl, int64_t B, int S);
 hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, const double* p, int64_t B,

@@ -6,7 +6,9 @@
 //     vt = β2·vt + (1 - β2)·Δ²
 //     Δ  = mt / (1 - βp1) / (√(vt / (1 - βp2)) + ϵ) · η ;   x .-= Δ ;   βp .*= β
 // Flux evaluates these broadcasts with its Float64 hyper-parameters, so a Float32 x, mt, vt is
-// promoted, computed in Float64 and rounded on store: the same here.  Δ arrives as the SUM
+// promoted, computed in Float64 and rounded on store: the same here.  apply! stores the step into the
+// gradient array Δ (`@. Δ = … * η`, Float32 with Float32 parameters) and update! subtracts that array
+// (`x .-= Δ`, a Float32 broadcast), so the step is rounded to T before a subtraction in T.  Δ arrives as the SUM
 // all-reduce of the ranks' gradients; `scale` (1/world_size) forms their mean in the same pass,
 // so the whole post-collective update is ONE launch instead of the ~8 elementwise torch kernels of
 // kanode.Adam (kanode/train.py).  The operation order is kanode.Adam's (torch's add_(alpha) and
@@ -29,7 +31,8 @@ adam_step_kernel(T* __restrict__ x, T* __restrict__ m, T* __restrict__ v, const 
         v[i] = vs;
         const double den = __dadd_rn(::sqrt(__ddiv_rn((double)vs, a.c2)), a.eps);
         const double step = __dmul_rn(__ddiv_rn(__ddiv_rn((double)ms, a.c1), den), a.eta);
-        x[i] = (T)__dsub_rn((double)x[i], step);
+        if constexpr (std::is_same<T, double>::value) x[i] = __dsub_rn(x[i], step);
+        else x[i] = __fsub_rn(x[i], (float)step);
     }
 }
 

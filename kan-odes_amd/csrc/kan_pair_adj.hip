@@ -805,8 +805,21 @@ hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, c
                                  : reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<16>);
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    // every workgroup spins on the others at each exchange, so all nwg must be resident at once: launch only
+    // when the device's capacity for this kernel (workgroups per CU at this LDS carve x CUs) covers the grid
+    // (a caller-set cap stands for a partitioned or shared device).  Otherwise the caller takes the
+    // launch-per-stage path.  Work already running on the device can still hold CUs: the exchanges then
+    // time out, the kernel reports it and the caller re-runs on that path too.
+    int dev = 0, ncu = 0, per_cu = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kPA, lds)) != hipSuccess) return e;
+    int64_t cap = (int64_t)per_cu * ncu;
+    if (pa.max_wg > 0 && pa.max_wg < cap) cap = pa.max_wg;
+    if (nwg > cap) return hipErrorNotSupported;
     e = hipMemsetAsync(pa.ctr, 0, 16, st);   // the arrival counter and the abort word
     if (e != hipSuccess) return e;
+    if (pa.force_abort && (e = hipMemsetAsync(pa.abrt, 1, 1, st)) != hipSuccess) return e;
     if (pa.S == 4) hipLaunchKernelGGL(kd_pair_adjoint_kernel<4>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
     else if (pa.S == 8) hipLaunchKernelGGL(kd_pair_adjoint_kernel<8>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);
     else hipLaunchKernelGGL(kd_pair_adjoint_kernel<16>, dim3(nwg), dim3(kPA), lds, st, dlc, p, B, pa);

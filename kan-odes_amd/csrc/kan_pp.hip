@@ -360,6 +360,32 @@ __device__ __forceinline__ double wave_rol1(double v) {
 
 typedef double kd2 __attribute__((ext_vector_type(2)));
 
+// (D*lap)*λ at the 2·NP consecutive points a lane holds (pair k = v[k].x, v[k].y; the wave's lanes hold
+// the row in order): lap3's ascending-column orders, no FMA contraction.  co·v is formed once per point and
+// shared by both neighbours' rows (the same product bits as lap_pair's), the two cross-lane neighbours
+// arrive by one wave rotation each (lane 0's left neighbour is lane 63's last point: the periodic wrap),
+// and only the row's first (lane 0) and last (lane 63) points take their boundary orders.
+template <int NP>
+__device__ __forceinline__ void lap_lane(const kd2 (&v)[NP], int lane, double cd, double co, double (&r)[2 * NP]) {
+#pragma clang fp contract(off)
+    constexpr int L = 2 * NP;
+    double cu[L], du[L];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        cu[2 * k] = co * v[k].x;
+        cu[2 * k + 1] = co * v[k].y;
+        du[2 * k] = cd * v[k].x;
+        du[2 * k + 1] = cd * v[k].y;
+    }
+    const double cl = wave_ror1(cu[L - 1]), cr = wave_rol1(cu[0]);
+#pragma unroll
+    for (int m = 0; m < L; ++m) r[m] = ((m == 0 ? cl : cu[m - 1]) + du[m]) + (m == L - 1 ? cr : cu[m + 1]);
+    const double first = (du[0] + cu[1]) + cl;            // row 0: (cd·u0 + co·up) + co·um
+    const double last = (cr + cu[L - 2]) + du[L - 1];     // row Nx-1: (co·up + co·um) + cd·u0
+    r[0] = lane == 0 ? first : r[0];
+    r[L - 1] = lane == kWave - 1 ? last : r[L - 1];
+}
+
 #ifndef KAN_PP_NT
 #define KAN_PP_NT 1
 #endif
@@ -614,12 +640,17 @@ __device__ __forceinline__ void pp_direct_dphi_sw(const Math<double>& M, const L
 template <bool SPLITH = (KAN_VJP_SPLIT_HORNER != 0)>
 __device__ __forceinline__ bool pp_eval2(const double2* __restrict__ td, const double2* __restrict__ ts, int ni,
                                          double inv_w, double x0, double u, double& d, double& s) {
+    // interval index without selects: v_cvt_i32_f64 saturates out-of-range values (and gives 0 for NaN,
+    // whose t and so y are NaN: rejected below), so one unsigned compare is the range check, and the masked
+    // index keeps the LDS reads in the table for the points the direct formula takes (ni: a power of two).
+    // In range, k and t are those of the clamped form (the same bits).
     const double x = ::fma(u, inv_w, x0);
-    const bool in = (x >= 0.0) && (x < (double)ni);
-    const double xc = in ? x : 0.0;
-    const double fl = __builtin_floor(xc);
-    const int k = (int)fl;
-    const double t = ::fma(2.0, xc - fl, -1.0);
+    const double fl = __builtin_floor(x);
+    int ki;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(fl));
+    const bool in = (unsigned)ki < (unsigned)ni;
+    const int k = ki & (ni - 1);
+    const double t = ::fma(2.0, x - fl, -1.0);
     const double2* __restrict__ a = td + k;
     const double2* __restrict__ b = ts + k;
     double y, z;
@@ -1095,6 +1126,15 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_NORED
 #define KAN_VROWS_NORED 0
 #endif
+#ifndef KAN_VROWS_SKEL
+#define KAN_VROWS_SKEL 0
+#endif
+#ifndef KAN_VROWS_CONTIG
+#define KAN_VROWS_CONTIG 1
+#endif
+#ifndef KAN_VROWS_L2LOAD
+#define KAN_VROWS_L2LOAD 0
+#endif
 // NI > 0: the table's interval count compiled in, so the Horner coefficients' LDS offsets are instruction
 // immediates (as fk_vjp_pp_wave_kernel; round 4: the per-point address arithmetic of the runtime count
 // was ~8 VALU per point and stage)
@@ -1236,7 +1276,15 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6);
     const bool live = b < B;
-    const int64_t rb = (live ? b : 0) * Nx + 2 * lane;
+    // KAN_VROWS_CONTIG: lane l holds the row's points [2·NP·l, 2·NP·(l + 1)) (pair k at 2·NP·l + 2k), so
+    // the stencil's only cross-lane values are the two ends of each lane's run; otherwise pair k at 128k + 2l
+    constexpr int kOff = KAN_VROWS_CONTIG ? 2 : 128;
+    const int64_t rb = (live ? b : 0) * Nx + (KAN_VROWS_CONTIG ? 2 * NP : 2) * lane;
+#if KAN_VROWS_L2LOAD   // timing experiment only: every wave loads one of 64 rows (L2-resident), stores its own
+    const int64_t rbl = ((live ? b : 0) & 63) * Nx + (KAN_VROWS_CONTIG ? 2 * NP : 2) * lane;
+#else
+    const int64_t rbl = rb;
+#endif
     // the row's loads are in flight while the block stages its tables
     kd2 lam0[NP], kl[6][NP], ui[NP], qi[4][NP];
 #pragma unroll
@@ -1250,11 +1298,11 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     if (live) {
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-            lam0[k] = ld_vstep(a.lam + rb + 128 * k);
-            kl[0][k] = ld_vstep(a.kl[0] + rb + 128 * k);
-            ui[k] = ld_vstep(a.su_u[0] + rb + 128 * k);
+            lam0[k] = ld_vstep(a.lam + rbl + kOff * k);
+            kl[0][k] = ld_vstep(a.kl[0] + rbl + kOff * k);
+            ui[k] = ld_vstep(a.su_u[0] + rbl + kOff * k);
 #pragma unroll
-            for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[0][m] + rb + 128 * k);
+            for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[0][m] + rbl + kOff * k);
         }
     }
     const int tsz = (kPPCoef / 2) * ni;
@@ -1270,8 +1318,9 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     const RecScalars<double> rc(lc);
     const int P = GT + (lc.use_base ? 1 : 0);
     double eacc = 0.0;
-    const bool combine = a.combine != 0;   // (a runtime flag: a compile-time one made the fixed-step
-                                           // instantiation spill 1.2 KB/lane)
+    // (a runtime flag: a compile-time one made the fixed-step instantiation spill 1.2 KB/lane, and the
+    // adaptive one, which is launched only to combine, 168 B/lane: round 5, 57 -> 69 us per step)
+    const bool combine = a.combine != 0;
     double comb[GT + 1];
 #pragma unroll
     for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
@@ -1293,9 +1342,9 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             if (s > 0 && a.reload[s]) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) {
-                    ui[k] = ld_vstep(a.su_u[s] + rb + 128 * k);
+                    ui[k] = ld_vstep(a.su_u[s] + rbl + kOff * k);
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[s][m] + rb + 128 * k);
+                    for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[s][m] + rbl + kOff * k);
                 }
             }
             kd2 uv[NP], lv[NP], ev[NP];
@@ -1330,8 +1379,15 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
             }
             if (last && a.lam_out) {
 #pragma unroll
-                for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + 128 * k, lv[k]);
+                for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + kOff * k, lv[k]);
             }
+#if KAN_VROWS_CONTIG
+            double la[2 * NP];
+            lap_lane<NP>(lv, lane, cd, co, la);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const double a0 = la[2 * k], a1 = la[2 * k + 1];
+#else
             double rr[NP], rl[NP];
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
@@ -1344,6 +1400,16 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                 const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
                 double a0, a1;
                 lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, a0, a1);
+#endif
+#if KAN_VROWS_SKEL   // timing experiment only: the memory and reduction skeleton without the pullback
+                const double x0b = uv[k].x * lv[k].x, x1b = uv[k].y * lv[k].y;
+#pragma unroll
+                for (int j = 0; j < GT; ++j) {
+                    S0[j] = k == 0 ? x0b : S0[j] + x0b;
+                    S1[j] = S2[j] = (float)x1b;
+                }
+                dW = x1b;
+#else
 #if KAN_VROWS_SB
                 __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -1354,13 +1420,14 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 #endif
                 const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].y, lv[k].y,
                                                                S0, S1, S2, dW);
+#endif
                 kd2 o;
                 o.x = a0 + x0b;
                 o.y = a1 + x1b;
                 if (!last) {
                     kl[s + 1 < 6 ? s + 1 : 5][k] = o;
                 } else {
-                    st_vstep(a.kl[6] + rb + 128 * k, o);
+                    st_vstep(a.kl[6] + rb + kOff * k, o);
                     if (want_err) {
                         const double en = a.ec[6];
                         const double ex = ::fma(en, o.x, ev[k].x), ey = ::fma(en, o.y, ev[k].y);
@@ -2014,6 +2081,9 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
     // the fused finish: the combined adaptive rows step with at least 1 + P workgroups
     if (a.combine != 2 || grid_for(B, kVjpBlock / kWave, slab_blocks) < P + 1) a.fin_ctr = nullptr;
     if (fused_finish_out) *fused_finish_out = a.fin_ctr != nullptr;
+    // the arrival counters start every fused launch at zero (a timed-out wait in an earlier launch
+    // may leave a late arrival behind in them, which would let the next launch's finishers start early)
+    if (a.fin_ctr && (e = hipMemsetAsync(a.fin_ctr, 0, 2 * sizeof(unsigned), st)) != hipSuccess) return e;
     a.reload[0] = 1;
     for (int s = 1; s < 6; ++s) {
         bool same = a.su_u[s] == a.su_u[s - 1];

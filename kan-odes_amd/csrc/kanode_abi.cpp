@@ -66,6 +66,9 @@ struct kanode_handle {
     bool pair_fuse = true;            // KANODE_OPT_PAIR_FUSE
     bool pair_persist = true;         // KANODE_OPT_PAIR_PERSIST
     int pair_persist_s = 0;           // KANODE_OPT_PAIR_PERSIST_S (0: the kernel's default)
+    int pair_persist_max_wg = 0;      // KANODE_OPT_PAIR_PERSIST_MAX_WG (0: the device's co-resident capacity)
+    bool pair_persist_abort = false;  // KANODE_OPT_PAIR_PERSIST_ABORT (tests: raise the abort word at launch)
+    int last_adjoint = KANODE_ADJ_NONE;   // KANODE_OPT_LAST_ADJOINT (read-only)
     bool adj_fused_finish = false;    // KANODE_OPT_ADJ_FUSED_FINISH (measured even with the finish launch)
     unsigned* fin_ctr = nullptr;      // its two arrival counters (device, zeroed at allocation)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
@@ -1081,10 +1084,15 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_PAIR_FUSE: return flag(h->pair_fuse, "PAIR_FUSE");
     case KANODE_OPT_PAIR_PERSIST: return flag(h->pair_persist, "PAIR_PERSIST");
     case KANODE_OPT_PAIR_PERSIST_S:
-        if (value < 0 || value > 256) return fail(h, KANODE_ERR_INVALID_ARG, "PAIR_PERSIST_S must be in [0, 256]");
+        // the kernel is instantiated for 4, 8 and 16 points per workgroup
+        if (value != 0 && value != 4 && value != 8 && value != 16)
+            return fail(h, KANODE_ERR_INVALID_ARG, "PAIR_PERSIST_S takes 0 (default), 4, 8 or 16");
         h->pair_persist_s = (int)value;
         return KANODE_OK;
     case KANODE_OPT_ADJ_FUSED_FINISH: return flag(h->adj_fused_finish, "ADJ_FUSED_FINISH");
+    case KANODE_OPT_PAIR_PERSIST_MAX_WG: return count(h->pair_persist_max_wg, "PAIR_PERSIST_MAX_WG", 1 << 20);
+    case KANODE_OPT_PAIR_PERSIST_ABORT: return flag(h->pair_persist_abort, "PAIR_PERSIST_ABORT");
+    case KANODE_OPT_LAST_ADJOINT: return fail(h, KANODE_ERR_INVALID_ARG, "LAST_ADJOINT is read-only");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -1105,6 +1113,9 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_PAIR_PERSIST: return h->pair_persist ? 1 : 0;
     case KANODE_OPT_PAIR_PERSIST_S: return h->pair_persist_s;
     case KANODE_OPT_ADJ_FUSED_FINISH: return h->adj_fused_finish ? 1 : 0;
+    case KANODE_OPT_PAIR_PERSIST_MAX_WG: return h->pair_persist_max_wg;
+    case KANODE_OPT_PAIR_PERSIST_ABORT: return h->pair_persist_abort ? 1 : 0;
+    case KANODE_OPT_LAST_ADJOINT: return h->last_adjoint;
     }
     return -1;
 }
@@ -1551,12 +1562,15 @@ kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int6
     if (!kanode_internal_pair_persist_ok(h)) return KANODE_OK;
     a->S = h->pair_persist_s;
     a->P = h->P;
+    a->max_wg = h->pair_persist_max_wg;
+    a->force_abort = h->pair_persist_abort ? 1 : 0;
     const hipError_t e = kan::launch_kd_pair_adjoint(h->hlc, h->dlc, (const double*)p, batch, *a, (hipStream_t)stream);
     if (e == hipErrorNotSupported) return KANODE_OK;
     if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_pair_adjoint: ") + hipGetErrorString(e));
     launched = true;
     return KANODE_OK;
 }
+void kanode_internal_set_last_adjoint(kanode_handle* h, int path) { h->last_adjoint = path; }
 int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch) {
     return kan::pair_adjoint_workgroups(h->hlc, batch, h->pair_persist_s);
 }

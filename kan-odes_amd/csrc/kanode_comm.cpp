@@ -62,14 +62,18 @@ kanode_status kanode_comm_create(int32_t nranks, int32_t rank, const uint8_t* id
                          "kanode_comm_create: device " + std::to_string(device) + " not present (" +
                              std::to_string(ndev) + " visible)");
     }
-    if (hipSetDevice(device) != hipSuccess) {
+    // RCCL binds the communicator to the calling thread's current device; the caller's (Julia's, torch's)
+    // current device is put back afterwards.  One rank per GPU: RCCL refuses two on one device.
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
         (void)hipGetLastError();
-        return comm_fail(nullptr, KANODE_ERR_HIP, "kanode_comm_create: hipSetDevice failed");
+        return comm_fail(nullptr, KANODE_ERR_HIP, "kanode_comm_create: hipGetDevice / hipSetDevice failed");
     }
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     auto* c = new kanode_comm();
     const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+    (void)hipSetDevice(prev);
     if (r != ncclSuccess) {
         delete c;
         return comm_fail(nullptr, KANODE_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));

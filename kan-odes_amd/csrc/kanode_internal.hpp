@@ -102,6 +102,8 @@ kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int
 bool kanode_internal_pair_persist_ok(const kanode_handle* h);
 int64_t kanode_internal_param_length(const kanode_handle* h);
 int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch);
+// KANODE_OPT_LAST_ADJOINT: record the path kanode_adjoint_tsit5 took (a kanode_adjoint_path value)
+void kanode_internal_set_last_adjoint(kanode_handle* h, int path);
 kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int64_t batch, kan::PairAdjArgs* a,
                                            void* stream, bool& launched);
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

@@ -1373,12 +1373,18 @@ kanode_status adjoint_pair_t(kanode_handle* h, const void* p, kanode_solution* s
     if (!launched) return KANODE_OK;
     auto& f = s->fused;
     SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    unsigned abort_word = 0;
+    SOLVE_HIP(h, hipMemcpyAsync(&abort_word, pa.abrt, sizeof(abort_word), hipMemcpyDeviceToHost, st));
     SOLVE_HIP(h, hipStreamSynchronize(st));
     int64_t res[4];
     std::memcpy(res, s->hscal, sizeof(res));
+    if (res[3] == 3 || abort_word != 0) {
+        // an exchange timed out (workgroups not co-resident: other work held CUs) and the grid drained:
+        // the launch-per-stage path (adjoint_t) re-runs the adjoint and writes every output again
+        kanode_internal_set_last_adjoint(h, KANODE_ADJ_PAIR_FALLBACK);
+        return KANODE_OK;
+    }
     if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
-    if (res[3] == 3)
-        return kanode_internal_fail(h, KANODE_ERR_HIP, "persistent pair adjoint: an exchange between workgroups timed out");
     if (stats) {
         stats->naccept = res[0];
         stats->nreject = res[1];
@@ -1514,12 +1520,20 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
     SOLVE_TRY(ctl_begin(h, s, st));
     TableHold hold(h);
     bool done = false;
+    kanode_internal_set_last_adjoint(h, KANODE_ADJ_NONE);
     kanode_status r = s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
                                              : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done);
-    if (r == KANODE_OK && !done) r = adjoint_pair_t(h, p, s, dl_du, du0, dp, o, stats, st, done);
-    if (r == KANODE_OK && !done)
+    if (r == KANODE_OK && done) kanode_internal_set_last_adjoint(h, KANODE_ADJ_CHAIN_WG);
+    if (r == KANODE_OK && !done) {
+        r = adjoint_pair_t(h, p, s, dl_du, du0, dp, o, stats, st, done);
+        if (r == KANODE_OK && done) kanode_internal_set_last_adjoint(h, KANODE_ADJ_PAIR_PERSIST);
+    }
+    if (r == KANODE_OK && !done) {
+        const bool fell_back = kanode_get_option(h, KANODE_OPT_LAST_ADJOINT) == KANODE_ADJ_PAIR_FALLBACK;
         r = s->dtype == KANODE_F64 ? adjoint_t<double>(h, p, s, dl_du, du0, dp, o, stats, st)
                                    : adjoint_t<float>(h, p, s, dl_du, du0, dp, o, stats, st);
+        if (!fell_back) kanode_internal_set_last_adjoint(h, KANODE_ADJ_HOST_LOOP);
+    }
     if (r != KANODE_OK) {
         // a failed adjoint may leave a deferred surrogate-pair stage (raw pointers into this solution and the
         // handle's workspace) and finish jobs pending on the handle: drop them, so no later call launches them

@@ -155,8 +155,10 @@ class KanodeHandle:
                 "kanode_set_option")
 
     def set_option(self, name: str, value: int) -> None:
-        """kanode_set_option by name (see include/kanode.h: pointwise_table, fused_step, fused_solve,
-        fused_solve_cap, grid_rhs, grid_vjp, grid_adj_step, adj_step_rows)."""
+        """kanode_set_option by name (include/kanode.h; the names are _lib.OPTIONS: pointwise_table,
+        fused_step, fused_solve, fused_solve_cap, grid_rhs, grid_vjp, grid_adj_step, adj_step_rows, pair_vjp,
+        pair_fuse, pair_persist, pair_persist_s, adj_fused_finish, pair_persist_max_wg, pair_persist_abort;
+        last_adjoint is read-only)."""
         if name not in L.OPTIONS:
             raise KeyError(f"unknown option {name!r}; known: {sorted(L.OPTIONS)}")
         L.check(L.lib().kanode_set_option(self._h, L.OPTIONS[name], int(value)), self._h, "kanode_set_option")

@@ -26,7 +26,8 @@ class Adam:
     Δ = mt / (1-β1^t) / (√(vt / (1-β2^t)) + ϵ) · η;  x .-= Δ.
 
     Flux evaluates these broadcasts with its Float64 hyper-parameters, so Float32 x, mt, vt are
-    promoted, computed in Float64 and rounded on store.  This torch statement does the same, in the
+    promoted, computed in Float64 and rounded on store; apply! stores the step into the gradient array
+    (Float32 with Float32 parameters) and update! subtracts it in Float32.  This torch statement does the same, in the
     operation order of the fused kernel (kan_optim.hip: every product and sum rounded separately), so
     the CPU and GPU trainers take the same optimiser trajectory for either dtype."""
 
@@ -54,9 +55,10 @@ class Adam:
         return step
 
     def update(self, x: torch.Tensor, d: torch.Tensor) -> None:
-        """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ) (the subtraction in Float64, rounded on store)."""
+        """Flux.update!(opt, x, Δ): x .-= apply!(opt, x, Δ), the step rounded to x's dtype (apply! stores it
+        into the gradient array) and subtracted in that dtype."""
         with torch.no_grad():
-            x.copy_(x.double() - self.apply(x, d))
+            x.sub_(self.apply(x, d).to(x.dtype))
 
 
 class FusedAdam(Adam):

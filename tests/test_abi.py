@@ -46,6 +46,9 @@ def test_option_ids_match_the_header():
     body = re.search(r"typedef enum \{([^}]*)\} kanode_option;", src, flags=re.S).group(1)
     ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"KANODE_OPT_(\w+)\s*=\s*(\d+)", body)}
     assert ids == L.OPTIONS
+    body = re.search(r"typedef enum \{([^}]*)\} kanode_adjoint_path;", src, flags=re.S).group(1)
+    paths = {m.group(1): int(m.group(2)) for m in re.finditer(r"KANODE_ADJ_(\w+)\s*=\s*(\d+)", body)}
+    assert paths == {n: getattr(L, "ADJ_" + n) for n in paths} and len(paths) == 5
 
 
 def test_library_has_no_environment_knobs():

@@ -752,7 +752,7 @@ def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, persist, 
     assert eg <= bar_g and egu <= bar_g
 
 
-@pytest.mark.parametrize("N,G,B,S", [(512, 5, 4, 0), (512, 5, 1, 0), (41, 5, 2, 0), (512, 5, 4, 4), (41, 5, 3, 7)])
+@pytest.mark.parametrize("N,G,B,S", [(512, 5, 4, 0), (512, 5, 1, 0), (41, 5, 2, 0), (512, 5, 4, 4), (41, 5, 3, 4)])
 @pytest.mark.parametrize("adaptive", [True, False])
 def test_persistent_pair_adjoint_matches_launch_path(N, G, B, S, adaptive):
     """KANODE_OPT_PAIR_PERSIST: the whole surrogate adjoint as one launch (kd_pair_adjoint_kernel: the grid
@@ -760,7 +760,8 @@ def test_persistent_pair_adjoint_matches_launch_path(N, G, B, S, adaptive):
     control on the device) against the launch-per-stage native adjoint, which the full-size oracle test
     above pins.  Same algorithm, sums in another fixed order: equal step counts, gradients to 1e-11 of
     their scale (fixed steps) / 1e-9 (adaptive: the step sizes move with the rounding of the error norm);
-    bitwise reproducible between two runs."""
+    bitwise reproducible between two runs.  KANODE_OPT_LAST_ADJOINT shows which path ran (a
+    shape the kernel rejects would otherwise compare the launch path with itself)."""
     chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
     rhs = kanode.ChainRHS(chain, device=device())
     x = np.linspace(-1.0, 1.0, N)
@@ -778,12 +779,55 @@ def test_persistent_pair_adjoint_matches_launch_path(N, G, B, S, adaptive):
             sol = kanode.solve(rhs, x0, (0.0, 0.05), p, ts, opt, sensealg="interpolating_adjoint")
             g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
             out.append((g, gu, sol.stats))
+            assert rhs.hd.get_option("last_adjoint") == (L.ADJ_PAIR_PERSIST if persist else L.ADJ_HOST_LOOP)
     (g1, gu1, s1), (g1b, gu1b, _), (g0, gu0, s0) = out
     assert torch.equal(g1, g1b) and torch.equal(gu1, gu1b)
     assert s1["adjoint"]["naccept"] == s0["adjoint"]["naccept"] and s1["adjoint"]["nreject"] == s0["adjoint"]["nreject"]
     bar = 1e-9 if adaptive else 1e-11
     assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
     assert (gu1 - gu0).abs().max().item() <= bar * gu0.abs().max().item()
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_persistent_pair_adjoint_falls_back(adaptive):
+    """VERDICT r4 #3 / ADVICE r4: the one-launch surrogate adjoint's workgroups spin on each other, so it runs
+    only when all of them can be resident, and an exchange time-out re-runs the adjoint on the launch-per-stage
+    path instead of failing the call.  Forced both ways on the Burgers [512, 10, 512] shape (64 workgroups):
+    PAIR_PERSIST_MAX_WG = 8 (a device with room for 8 resident workgroups: the launch is refused up front) and
+    PAIR_PERSIST_ABORT = 1 (the abort word raised at launch, as a time-out raises it: the kernel drains and
+    the host re-runs).  Both give the launch path's gradient bitwise, and the handle then still takes the
+    one-launch path when allowed."""
+    N, G, B = 512, 5, 4
+    chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
+    rhs = kanode.ChainRHS(chain, device=device())
+    x = np.linspace(-1.0, 1.0, N)
+    a = np.random.default_rng(7).normal(0.0, 0.1, (B, 3))
+    u0 = t(-np.sin(np.pi * x)[None, :] + sum(a[:, k:k + 1] * np.sin((k + 1) * np.pi * x)[None, :] for k in range(3)))
+    p0 = t(chain.setup(np.random.default_rng(3))[0].astype(np.float64))
+    ts = [0.0, 0.01, 0.02, 0.035, 0.05]
+    w = torch.as_tensor(np.random.default_rng(4).normal(size=(len(ts),) + tuple(u0.shape)), device=device())
+    opt = kanode.Tsit5Options() if adaptive else kanode.Tsit5Options(adaptive=False, dt=0.004)
+
+    def grad(**o):
+        with rhs.hd.options(**o):
+            p = p0.detach().clone().requires_grad_(True)
+            x0 = u0.detach().clone().requires_grad_(True)
+            sol = kanode.solve(rhs, x0, (0.0, 0.05), p, ts, opt, sensealg="interpolating_adjoint")
+            g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+            return g, gu, rhs.hd.get_option("last_adjoint")
+
+    g0, gu0, path0 = grad(pair_persist=0)
+    assert path0 == L.ADJ_HOST_LOOP
+    gc, guc, pathc = grad(pair_persist_max_wg=8)
+    assert pathc == L.ADJ_HOST_LOOP
+    ga, gua, patha = grad(pair_persist_abort=1)
+    assert patha == L.ADJ_PAIR_FALLBACK
+    for g, gu in ((gc, guc), (ga, gua)):
+        assert torch.equal(g, g0) and torch.equal(gu, gu0)
+    g1, gu1, path1 = grad()
+    assert path1 == L.ADJ_PAIR_PERSIST
+    bar = 1e-9 if adaptive else 1e-11
+    assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
 
 
 

@@ -25,7 +25,7 @@ def flux_adam(x, grads, eta, scale, dtype=np.float64, b1=0.9, b2=0.999, eps=1e-8
         m = (b1 * m.astype(np.float64) + (1 - b1) * d).astype(dtype)
         v = (b2 * v.astype(np.float64) + ((1 - b2) * d) * d).astype(dtype)
         step = m.astype(np.float64) / (1 - bp1) / (np.sqrt(v.astype(np.float64) / (1 - bp2)) + eps) * eta
-        x = (x.astype(np.float64) - step).astype(dtype)
+        x = x - step.astype(dtype)      # apply! stores Δ in the gradient's eltype; x .-= Δ in that type
         flux_adam.abs_sum = flux_adam.abs_sum + np.abs(step)
         bp1 *= b1
         bp2 *= b2

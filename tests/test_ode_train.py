@@ -94,7 +94,7 @@ def test_adam_float32_promotes_like_flux():
         m = (b1 * m.astype(np.float64) + (1 - b1) * d).astype(np.float32)
         v = (b2 * v.astype(np.float64) + ((1 - b2) * d) * d).astype(np.float32)
         step = m.astype(np.float64) / (1 - bp1) / (np.sqrt(v.astype(np.float64) / (1 - bp2)) + 1e-8) * 1e-3
-        xr = (xr.astype(np.float64) - step).astype(np.float32)
+        xr = xr - step.astype(np.float32)   # Δ stored in the Float32 gradient array, x .-= Δ in Float32
         bp1 *= b1
         bp2 *= b2
     assert x.dtype == torch.float32
