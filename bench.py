@@ -351,6 +351,90 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     return out
 
 
+def fk26_train_bench(dev, with_cpu: bool, reps: int = 20):
+    """The reference's own Fisher-KPP training iteration (PDE examples/Fisher-KPP_Source.jl:34-49,95-109,194-213):
+    26 points (dx = 0.04 on [0, 1], periodic Laplacian, D = 0.01), the one initial condition (Amp = 1, Delta = 0.2),
+    T = 5, saveat every 0.5 (11 stops), adaptive Tsit5 at the default tolerances, the InterpolatingAdjoint gradient
+    and one Adam(1e-2) step; the training data from the true reaction u(1 - u) (:52,60-66) and a trained-like
+    KDense(1,1,10) (fk_trained_like_params: the state stays in the table's range as the reference's training does).
+    GPU: the whole forward solve and the whole adjoint are one workgroup each (kan_small.hip).  CPU: the same
+    iteration in C on one core (oracle/cpu_epoch.c over the dense-Laplacian oracle RHS, kind "port"; median of 20
+    after 3 warm-ups).  The reference selects ForwardDiffSensitivity at this size; both sides here
+    run the InterpolatingAdjoint (tests/test_gpu_anchors.py bounds the difference)."""
+    from scipy.integrate import solve_ivp
+    nx, dx, D, T = 26, 0.04, 0.01, 5.0
+    x = np.arange(nx) * dx
+    rho0 = (np.tanh((x - 0.4) / 0.02) - np.tanh((x - 0.6) / 0.02)) / 2
+    lap = (np.diag(-2.0 * np.ones(nx)) + np.diag(np.ones(nx - 1), 1) + np.diag(np.ones(nx - 1), -1)) / dx ** 2
+    lap[0, -1] = lap[-1, 0] = 1.0 / dx ** 2
+    saveat = [0.5 * i for i in range(11)]
+    truth = solve_ivp(lambda t, u: D * lap @ u + u * (1 - u), (0.0, T), rho0, t_eval=saveat, method="DOP853",
+                      rtol=1e-10, atol=1e-12).y.T[:, None, :]
+    p0 = fk_trained_like_params()
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=D, dtype=torch.float64, device=dev)
+    u0 = torch.as_tensor(rho0[None, :], device=dev)
+    tr = kanode.Trainer(rhs, u0, (0.0, T), saveat, torch.as_tensor(truth, device=dev), torch.as_tensor(p0, device=dev),
+                        eta=1e-2, solver=kanode.Tsit5Options())
+    tr.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    gpu = (time.perf_counter() - t0) / reps * 1e3
+    _, _, sol = tr.loss_and_grad()
+    out = {"unit": "ms/iteration", "batch": 1, "nx": nx, "dtype": "f64", "gpu": gpu,
+           "forward_steps": sol.stats["naccept"], "adjoint_steps": sol.stats["adjoint"]["naccept"],
+           "gpu_path": "one-workgroup solve + one-workgroup adjoint" if rhs.hd.get_option("last_adjoint") == 2
+           else "host loop",
+           "what": "one Fisher-KPP_Source.jl training iteration: adaptive Tsit5 (T = 5, saveat 0.5, default "
+                   "tolerances) + InterpolatingAdjoint + Adam(1e-2), 26 points, one IC"}
+    if with_cpu:
+        from oracle import oracle as O
+        spec = O.LayerSpec(1, 1, 10, "softsign")
+        pc = p0.copy()
+        times = []
+        for r in range(23):
+            t0 = time.perf_counter()
+            _, _, pc, st, _ = O.fk_epoch(spec, pc, D, dx, rho0[None, :], T, saveat, truth, eta=1e-2)
+            if r >= 3:
+                times.append(time.perf_counter() - t0)
+        out.update({"cpu": float(np.median(times)) * 1e3, "cpu_cores": 1,
+                    "cpu_steps": [st.get("naccept"), st.get("adjoint_naccept")],
+                    "cpu_kind": "port (oracle/cpu_epoch.c: C Tsit5 + InterpolatingAdjoint + Adam over the dense-"
+                                "Laplacian oracle RHS, one core; median of 20 after 3 warm-ups)",
+                    "speedup": float(np.median(times)) * 1e3 / gpu})
+    return out
+
+
+def shard_ceiling(rhs, u, du, ps, stream, steps: int, full_rate: float):
+    """The compute side of strong scaling, measured on this one GPU: the same timed step (table build + RHS over
+    one rank's shard, parameters alternating so every step rebuilds) at the per-rank batches of N = 2, 4, 8
+    ranks (the first B/N trajectories).  projected_ratio = N x rate(B/N) / rate(B) is the speed-up N GPUs would
+    reach with no cost of their own (the bench's ranks share nothing on the data path); a SCALE line can be
+    checked against it."""
+    B = u.shape[0]
+    out = {}
+    for n in (2, 4, 8):
+        b = B // n
+        us, dus = u[:b], du[:b]
+        for i in range(5):
+            rhs.rhs(us, ps[i & 1], dus)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(steps):
+            rhs.rhs(us, ps[(5 + i) & 1], dus)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / steps
+        rate = b / (ms * 1e-3)
+        out[f"n{n}"] = {"batch_per_gpu": b, "ms_per_step": ms, "rate_per_gpu": rate,
+                        "projected_ratio": n * rate / full_rate}
+    return out
+
+
 def _graph_us(fn, reps: int = 50) -> float:
     """Device time per call from a hipGraph of `reps` back-to-back calls (launch-bound sizes)."""
     st = torch.cuda.Stream()
@@ -754,6 +838,9 @@ def main() -> None:
 
     total_evals = B * args.steps * world
     value = total_evals / elapsed
+    ceiling = None
+    if world == 1 and not weak:
+        ceiling = shard_ceiling(rhs, u, du, ps, stream, args.steps, B / (kern_ms * 1e-3))
     alg_bytes = 8.0 * (rhs.P + B * (nx + nx))       # p + u in + du out, per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(f"{args.workload}:{'table' if table else 'recurrence'}", alg_bytes)
@@ -780,6 +867,7 @@ def main() -> None:
         "launch": ("self-spawned ranks (bench.py --gpus)" if os.environ.get(LAUNCH_ENV) == "self"
                    else "external launcher (WORLD_SIZE)") if dist else "single process",
         "rank_timed_s": rank_elapsed,
+        "shard_ceiling": ceiling,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("fk_pp_build_kernel + fk_rhs_pp_wave_kernel<SOFTSIGN,RBF,2>" if table
@@ -818,6 +906,7 @@ def main() -> None:
     if rank == 0 and not args.no_vjp:
         out["lv4096"] = lv4096_bench(dev)
         out["lv1_train"] = lv1_train_bench(dev, world == 1 and not args.no_cpu_baseline)
+        out["fk26_train"] = fk26_train_bench(dev, world == 1 and not args.no_cpu_baseline)
         out["surrogates"] = surrogate_bench(dev, world == 1 and not args.no_cpu_baseline)
 
     if not args.no_epoch:

@@ -189,6 +189,10 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     work): the adjoint then re-runs on the launch-per-stage path.
  *   KANODE_OPT_LAST_ADJOINT (read-only): the path the handle's last kanode_adjoint_tsit5 took,
  *     a kanode_adjoint_path value.
+ *   KANODE_OPT_CHAIN_WIDE (default 1): the one-workgroup adjoint of ONE trajectory of a two-layer chain
+ *     with base activations (the Lotka-Volterra driver's shape) spreads the pullback over the whole
+ *     workgroup, one basis function per lane (kd_chain_adjoint_wide_kernel); 0 = the 16-lane group of
+ *     the batched kernel.  Same formulas; sums in another order.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -207,7 +211,8 @@ typedef enum {
     KANODE_OPT_ADJ_FUSED_FINISH = 13,
     KANODE_OPT_PAIR_PERSIST_MAX_WG = 14,
     KANODE_OPT_PAIR_PERSIST_ABORT = 15,
-    KANODE_OPT_LAST_ADJOINT = 16
+    KANODE_OPT_LAST_ADJOINT = 16,
+    KANODE_OPT_CHAIN_WIDE = 17
 } kanode_option;
 typedef enum {
     KANODE_ADJ_NONE = 0,            /* no adjoint on this handle yet */

@@ -9,6 +9,7 @@
 // ordered slab reduction (bitwise reproducible; no float atomics).
 #include "kan_common.hpp"
 #include "kan_kernels.hpp"
+#include "kan_onewg.hpp"
 
 namespace kan {
 
@@ -403,20 +404,53 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
 // initial step, PI controller, saveat from the dense output, FSAL).  No launch or host
 // round trip per stage or step: the host loop pays ~6 launches + one 8-byte read per step.
 template <typename T, int NORM, int PATH, class S>
+__device__ __forceinline__ T chain_pullback(const Math<T>& M, const LayerConst* lcl, int nl, const T* ps,
+                                            T* __restrict__ row, int j, T yj, T lj);
+
+// The small-chain right-hand side for the one-workgroup drivers (kan_onewg.hpp): column group g of 16
+// lanes holds trajectory g, lane j entry j; f is chain_forward, the VJP chain_pullback with the group
+// gradient rows summed into kμ in the order of kd_chain_vjp_stage_kernel + chain_vjp_finish_kernel (4
+// groups per block, then the blocks).
+template <typename T, int NORM, int PATH, class S>
+struct ChainModel {
+    const Math<T>& M;
+    const LayerConst* lcl;
+    int nl;
+    const T* ps;
+    T* rows;     // [NG][P] group gradient rows (LDS, zero between calls)
+    int P, j, NGa;
+    bool act;
+    int64_t idx, n;
+    __device__ T rhs(T y) { return chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, y); }
+    __device__ T vjp(T y, T ls, T* __restrict__ km) {
+        const T lj = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, rows + (size_t)(threadIdx.x / kChainDim) * P, j,
+                                                       y, ls);
+        __syncthreads();
+        // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order.  The rows of
+        // groups without a trajectory (g >= B) stay zero, so they are left out of the sum
+        for (int q = threadIdx.x; q < P; q += blockDim.x) {
+            T tot = T(0);
+            for (int g0 = 0; g0 < NGa; g0 += 4) {
+                T sblk = rows[(size_t)g0 * P + q];
+                for (int g = g0 + 1; g < g0 + 4 && g < NGa; ++g) sblk = sblk + rows[(size_t)g * P + q];
+                tot = g0 == 0 ? sblk : tot + sblk;
+            }
+            km[q] = tot;
+            for (int g = 0; g < NGa; ++g) rows[(size_t)g * P + q] = T(0);
+        }
+        __syncthreads();
+        return act ? lj : T(0);
+    }
+};
+
+// A whole Tsit5 solve of a small chain in one workgroup: column group g owns trajectory g, lane j holds
+// u_j and its seven stage values in registers, every stage is chain_forward, and the embedded-error norm
+// over the whole state is a block sum that every lane receives (onewg_tsit5).  No launch or host round
+// trip per stage or step: the host loop pays ~6 launches + one 8-byte read per step.
+template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
                       const T* __restrict__ u0, int64_t B, ChainSolveArgs a) {
-    constexpr double TA[6][6] = {
-        {0.161, 0, 0, 0, 0, 0},
-        {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
-        {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
-        {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
-        {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
-        {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
-    };
-    constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
-                              -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
-                              0.015151515151515152};
     extern __shared__ __attribute__((aligned(16))) unsigned char cs_raw[];
     LayerConst* lcl = reinterpret_cast<LayerConst*>(cs_raw);
     T* ps = reinterpret_cast<T*>(cs_raw + nl * sizeof(LayerConst));
@@ -433,123 +467,9 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
     const int N = lcl[0].I;
     const int j = threadIdx.x & (kChainDim - 1);
     const int64_t col = threadIdx.x / kChainDim;
-    const bool act = col < B && j < N;
-    const int64_t idx = (int64_t)N * col + j;
-    const int64_t n = (int64_t)N * B;
-    T* __restrict__ usave = reinterpret_cast<T*>(a.u_save);
-    T* __restrict__ rec = reinterpret_cast<T*>(a.rec);
-    // Σ over the state of v (inactive lanes give 0), the same ordered total in every lane
-    auto bsum = [&](double v) -> double {
-        v = wave_sum(act ? v : 0.0);
-        __syncthreads();
-        if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
-        __syncthreads();
-        double t = red[0];
-        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
-        return t;
-    };
-    T u = act ? u0[idx] : T(0);
-    T k[7];
-    k[0] = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, u);
-    if (rec && act) reinterpret_cast<T*>(a.k1_0)[idx] = k[0];
-    const double t0 = a.t0, tf = a.tf;
-    int64_t si = 0;
-    while (si < a.n_save && a.saveat[si] <= t0 + 1e-14 * ::fmax(1.0, ::fabs(t0))) {
-        if (act && usave) usave[si * n + idx] = u;
-        ++si;
-    }
-    double dt = a.dt;
-    if (a.adaptive && !(a.dt > 0)) {   // Hairer & Wanner (solve_t initdt)
-        const double sk = ::fma(a.reltol, kabs((double)u), a.abstol);
-        const double d0 = ::sqrt(bsum(((double)u / sk) * ((double)u / sk)) / (double)n);
-        const double d1 = ::sqrt(bsum(((double)k[0] / sk) * ((double)k[0] / sk)) / (double)n);
-        double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
-        dt0 = ::fmin(dt0, tf - t0);
-        const T f1 = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, kfma<T>((T)dt0, k[0], u));
-        const double e = ::fma(-1.0, (double)k[0], (double)f1) / sk;
-        const double d2 = ::sqrt(bsum(e * e) / (double)n) / dt0;
-        const double mx = ::fmax(d1, d2);
-        const double dt1 = mx <= 1e-15 ? ::fmax(1e-6, dt0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
-        dt = ::fmin(::fmin(100 * dt0, dt1), tf - t0);
-    }
-    double qold = a.qoldinit, t = t0;
-    int64_t naccept = 0, nreject = 0, nf = 0, it = 0, status = 0;
-    for (; it < a.maxiters; ++it) {
-        if (t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf))) break;
-        dt = ::fmin(dt, tf - t);
-        T y = u;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            y = u;
-#pragma unroll
-            for (int m = 0; m <= i; ++m) y = kfma<T>((T)(dt * TA[i][m]), k[m], y);
-            k[i + 1] = chain_forward<T, NORM, PATH, S>(M, lcl, nl, ps, j, y);
-        }
-        nf += 6;
-        double dtnew = dt;
-        if (a.adaptive) {
-            double ev = 0.0;
-#pragma unroll
-            for (int m = 0; m < 6; ++m) ev = ::fma(dt * BT[m], (double)k[m], ev);
-            const double e = ::fma(dt * BT[6], (double)k[6], ev);
-            const double sk = ::fma(a.reltol, ::fmax(kabs((double)u), kabs((double)y)), a.abstol);
-            const double r = e / sk;
-            const double eest = ::sqrt(bsum(r * r) / (double)n);
-            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
-            if (eest > 1.0 && dt > a.dtmin) {
-                ++nreject;
-                dt = dt / ::fmin(1.0 / a.qmin, q11 / a.gamma);
-                continue;
-            }
-            double q = q11 / ::pow(qold, a.beta2);
-            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
-            if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
-            dtnew = q > 0 ? dt / q : dt * a.qmax;
-            qold = ::fmax(eest, a.qoldinit);
-        }
-        if (rec && naccept >= a.cap) {   // dense-output storage exhausted
-            status = 2;
-            break;
-        }
-        const double tn = t + dt;
-        while (si < a.n_save && a.saveat[si] <= tn + 1e-12 * ::fmax(1.0, ::fabs(tn))) {
-            const double tsv = a.saveat[si];
-            T v = y;
-            if (!(::fabs(tsv - tn) <= 1e-12 * ::fmax(1.0, ::fabs(tn)))) {
-                double w[7];
-                tsit5_interp_weights((tsv - t) / dt, w);
-                v = u;
-#pragma unroll
-                for (int m = 0; m < 7; ++m) v = kfma<T>((T)(w[m] * dt), k[m], v);
-            }
-            if (act && usave) usave[si * n + idx] = v;
-            ++si;
-        }
-        if (rec) {
-            T* __restrict__ r = rec + naccept * 7 * n;
-            if (act) {
-                r[idx] = u;
-#pragma unroll
-                for (int m = 1; m < 7; ++m) r[(int64_t)m * n + idx] = k[m];
-            }
-            if (threadIdx.x == 0) {
-                a.ts[naccept] = t;
-                a.dts[naccept] = dt;
-            }
-        }
-        u = y;   // commit u <- u_new, k_1 <- k_7 (FSAL)
-        k[0] = k[6];
-        t = tn;
-        ++naccept;
-        dt = dtnew;
-    }
-    if (status == 0 && it == a.maxiters && !(t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf)))) status = 1;
-    if (threadIdx.x == 0) {
-        a.out[0] = naccept;
-        a.out[1] = nreject;
-        a.out[2] = nf + 1;
-        a.out[3] = status;
-    }
+    ChainModel<T, NORM, PATH, S> m{M, lcl, nl, ps, nullptr, P, j, 0, col < B && j < N, (int64_t)N * col + j,
+                                   (int64_t)N * B};
+    onewg_tsit5<T>(m, u0, a, red);
 }
 
 // The adjoint stage of a small chain in one launch (kanode_vjp_stage for the LV [2,10,2]
@@ -1130,31 +1050,13 @@ kd_chain_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __rest
 // stage values then live in scratch, which only the non-LV small chains pay for)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wpass-failed"
+// The whole InterpolatingAdjoint of a small chain in one workgroup (onewg_adjoint), after a
+// kd_chain_tsit5_kernel forward: column group g holds λ of trajectory g and its seven stage values in
+// registers; μ, its seven stage vectors and the group gradient rows in LDS.
 template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t B,
                         ChainAdjointArgs a) {
-    constexpr double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
-    constexpr double TA[6][6] = {
-        {0.161, 0, 0, 0, 0, 0},
-        {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
-        {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
-        {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
-        {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
-        {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
-    };
-    constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
-                              -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
-                              0.015151515151515152};
-    constexpr double RI[7][4] = {
-        {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
-        {0.0, 0.13169999999999998, -0.2234, 0.1017},
-        {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
-        {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
-        {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
-        {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
-        {0.0, 1.5, -4.0, 2.5},
-    };
     extern __shared__ __attribute__((aligned(16))) unsigned char ca_raw[];
     const int NG = blockDim.x / kChainDim;
     const int NGa = B < NG ? (int)B : NG;   // groups holding a trajectory
@@ -1182,217 +1084,241 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
     const Math<T> M{tab};
     const int N = lcl[0].I;
     const int j = threadIdx.x & (kChainDim - 1);
-    const int grp = threadIdx.x / kChainDim;
-    const int64_t col = grp;
-    const bool act = col < B && j < N;
-    const int64_t idx = (int64_t)N * col + j;
-    const int64_t n = (int64_t)N * B;
-    const T* __restrict__ rec = reinterpret_cast<const T*>(a.rec);
-    const T* __restrict__ dl = reinterpret_cast<const T*>(a.dl_du);
-    T* __restrict__ row = rows + (size_t)grp * P;
-    const double t0 = a.t0, tf = a.tf, TT = tf - t0;
-    const int64_t ntot = n + P;
-    auto bsum = [&](double v) -> double {   // Σ over the block, every thread gets the ordered total
-        v = wave_sum(v);
-        __syncthreads();
-        if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
-        __syncthreads();
-        double t = red[0];
-        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
-        return t;
-    };
-    auto add_rows = [&](int gidx, T l) -> T {   // λ += Σ dl_du[r] (rows in order)
-        for (int32_t q = a.joff[gidx]; q < a.joff[gidx + 1]; ++q)
-            if (act) l = l + dl[(int64_t)a.jrows[q] * n + idx];
-        return l;
-    };
-    int64_t cur = a.nsteps - 1;   // forward step holding t (moves back as τ grows)
-    // adjoint RHS at τ with adjoint stage input ls: returns λsᵀ∂f/∂u, kμ -> km[slot]
-    auto adj = [&](double tau, T ls, int slot) -> T {
-        const double t = tf - tau;
-        while (cur > 0 && tsl[cur] > t) --cur;
-        while (cur + 1 < a.nsteps && tsl[cur + 1] <= t) ++cur;
-        const double dti = dtsl[cur];
-        const double th = ::fmin(1.0, ::fmax(0.0, (t - tsl[cur]) / dti));
-        T y = T(0);
-        if (act) {
-            const T* __restrict__ r = rec + cur * 7 * n;
-            const T* __restrict__ k1 = cur == 0 ? reinterpret_cast<const T*>(a.k1_0) : rec + (cur - 1) * 7 * n + 6 * n;
-            T kv[7];
-            kv[0] = k1[idx];
-#pragma unroll
-            for (int m = 1; m < 7; ++m) kv[m] = r[(int64_t)m * n + idx];
-            y = r[idx];
-#pragma unroll
-            for (int m = 0; m < 7; ++m) {
-                const double b = th * (RI[m][0] + th * (RI[m][1] + th * (RI[m][2] + th * RI[m][3])));
-                y = kfma<T>((T)(b * dti), kv[m], y);
-            }
-        }
-        const T lj = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, row, j, y, act ? ls : T(0));
-        __syncthreads();
-        // kμ = Σ of the group rows: 4 groups per block-equivalent, then across them, in order.  The
-        // rows of groups without a trajectory (g >= B) stay zero, so they are left out of the sum
-        for (int q = threadIdx.x; q < P; q += blockDim.x) {
-            T tot = T(0);
-            for (int g0 = 0; g0 < NGa; g0 += 4) {
-                T sblk = rows[(size_t)g0 * P + q];
-                for (int g = g0 + 1; g < g0 + 4 && g < NGa; ++g) sblk = sblk + rows[(size_t)g * P + q];
-                tot = g0 == 0 ? sblk : tot + sblk;
-            }
-            km[(size_t)slot * P + q] = tot;
-            for (int g = 0; g < NGa; ++g) rows[(size_t)g * P + q] = T(0);
-        }
-        __syncthreads();
-        return act ? lj : T(0);
-    };
-    T lam = T(0);
-    if (dl) lam = add_rows(0, lam);
-    int mc = 0;   // mu[mc] holds μ (zero)
-    T kl[7];
-    kl[0] = adj(0.0, lam, 0);
-    int64_t nf = 1;
-    double h = a.dt;
-    if (a.adaptive && !(a.dt > 0)) {   // Hairer-Wanner on [λ; μ]
-        double s0 = 0.0, s1 = 0.0;
-        {
-            const double sk = ::fma(a.reltol, kabs((double)lam), a.abstol);
-            const double r0 = (double)lam / sk, r1 = (double)kl[0] / sk;
-            s0 = act ? r0 * r0 : 0.0;
-            s1 = act ? r1 * r1 : 0.0;
-        }
-        for (int q = threadIdx.x; q < P; q += blockDim.x) {
-            const double m = (double)mu[q];
-            const double sk = ::fma(a.reltol, kabs(m), a.abstol);
-            const double r0 = m / sk, r1 = (double)km[q] / sk;
-            s0 += r0 * r0;
-            s1 += r1 * r1;
-        }
-        const double d0 = ::sqrt(bsum(s0) / (double)ntot), d1 = ::sqrt(bsum(s1) / (double)ntot);
-        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
-        h0 = ::fmin(h0, TT);
-        kl[1] = adj(h0, kfma<T>((T)h0, kl[0], lam), 1);
-        ++nf;
-        double s2 = 0.0;
-        {
-            const double sk = ::fma(a.reltol, kabs((double)lam), a.abstol);
-            const double e = ::fma(-1.0, (double)kl[0], (double)kl[1]) / sk;
-            s2 = act ? e * e : 0.0;
-        }
-        for (int q = threadIdx.x; q < P; q += blockDim.x) {
-            const double sk = ::fma(a.reltol, kabs((double)mu[q]), a.abstol);
-            const double e = ::fma(-1.0, (double)km[q], (double)km[P + q]) / sk;
-            s2 += e * e;
-        }
-        const double d2 = ::sqrt(bsum(s2) / (double)ntot) / h0;
-        const double mx = ::fmax(d1, d2);
-        const double h1 = mx <= 1e-15 ? ::fmax(1e-6, h0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
-        h = ::fmin(::fmin(100 * h0, h1), TT);
-    }
-    double qold = a.qoldinit, tau = 0.0;
-    int64_t si = 0, naccept = 0, nreject = 0, it = 0, status = 0;
-    int k0 = 0;   // km slot of kμ_1 (FSAL swaps slots 0 and 6)
-    for (; it < a.maxiters; ++it) {
-        if (tau >= TT - 1e-14 * ::fmax(1.0, TT)) break;
-        h = ::fmin(h, a.stops[si] - tau);
-        int ks[7];
-        ks[0] = k0;
-#pragma unroll
-        for (int m = 1; m < 6; ++m) ks[m] = m;
-        ks[6] = k0 == 0 ? 6 : 0;
-        T ls = lam;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            ls = lam;
-#pragma unroll
-            for (int m = 0; m <= i; ++m) ls = kfma<T>((T)(h * TA[i][m]), kl[m], ls);
-            kl[i + 1] = adj(i == 5 ? tau + h : tau + TC[i] * h, ls, ks[i + 1]);
-        }
-        nf += 6;
-        // μ_new = μ + h Σ a_6j kμ_j (and its error), λ error
-        T* __restrict__ mu0 = mu + (size_t)mc * P;
-        T* __restrict__ mu1 = mu + (size_t)(mc ^ 1) * P;
-        double s = 0.0;
-        for (int q = threadIdx.x; q < P; q += blockDim.x) {
-            T v = mu0[q];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) v = kfma<T>((T)(h * TA[5][m]), km[(size_t)ks[m] * P + q], v);
-            mu1[q] = v;
-            if (a.adaptive) {
-                double ev = 0.0;
-#pragma unroll
-                for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], (double)km[(size_t)ks[m] * P + q], ev);
-                const double e = ::fma(h * BT[6], (double)km[(size_t)ks[6] * P + q], ev);
-                const double sk = ::fma(a.reltol, ::fmax(kabs((double)mu0[q]), kabs((double)v)), a.abstol);
-                s += (e / sk) * (e / sk);
-            }
-        }
-        double hnew = h;
-        if (a.adaptive) {
-            if (act) {
-                double ev = 0.0;
-#pragma unroll
-                for (int m = 0; m < 6; ++m) ev = ::fma(h * BT[m], (double)kl[m], ev);
-                const double e = ::fma(h * BT[6], (double)kl[6], ev);
-                const double sk = ::fma(a.reltol, ::fmax(kabs((double)lam), kabs((double)ls)), a.abstol);
-                s += (e / sk) * (e / sk);
-            }
-            const double eest = ::sqrt(bsum(s) / (double)ntot);
-            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
-            if (eest > 1.0 && h > a.dtmin) {
-                ++nreject;
-                h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
-                __syncthreads();   // mu1 is rewritten by the retry
-                continue;
-            }
-            double q = q11 / ::pow(qold, a.beta2);
-            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
-            if (1.0 <= q && q <= 1.0) q = 1.0;
-            hnew = q > 0 ? h / q : h * a.qmax;
-            qold = ::fmax(eest, a.qoldinit);
-        }
-        __syncthreads();   // mu1 complete
-        tau = tau + h;
-        lam = ls;          // λ <- the last stage input (λ + h Σ a_6j kλ_j)
-        mc ^= 1;
-        kl[0] = kl[6];     // FSAL
-        k0 = ks[6];
-        ++naccept;
-        if (::fabs(tau - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT)) {
-            tau = a.stops[si];
-            if (si + 1 < a.nstops) {
-                if (dl && a.joff[si + 2] > a.joff[si + 1]) {
-                    lam = add_rows((int)si + 1, lam);   // callback: λ += ∂L/∂u(t_j)
-                    kl[0] = adj(tau, lam, k0);          // u_modified!: FSAL re-evaluated
-                    ++nf;
-                }
-            }
-            si = si + 1 < a.nstops ? si + 1 : a.nstops - 1;
-        }
-        h = hnew;
-    }
-    if (it == a.maxiters && !(tau >= TT - 1e-14 * ::fmax(1.0, TT))) status = 1;
-    if (dl) lam = add_rows((int)a.nstops, lam);
-    if (a.du0 && act) reinterpret_cast<T*>(a.du0)[idx] = lam;
-    if (a.dp)
-        for (int q = threadIdx.x; q < P; q += blockDim.x) reinterpret_cast<T*>(a.dp)[q] = mu[(size_t)mc * P + q];
-    if (threadIdx.x == 0) {
-        a.out[0] = naccept;
-        a.out[1] = nreject;
-        a.out[2] = nf;
-        a.out[3] = status;
-    }
+    const int64_t col = threadIdx.x / kChainDim;
+    ChainModel<T, NORM, PATH, S> m{M, lcl, nl, ps, rows, P, j, NGa, col < B && j < N, (int64_t)N * col + j,
+                                   (int64_t)N * B};
+    onewg_adjoint<T>(m, a, mu, km, tsl, dtsl, red);
 }
 #pragma clang diagnostic pop
+
+// ---- one trajectory over a whole workgroup (LV_driver_KANODE.jl:180-184,279-291) ------------
+// At B = 1 the group model above runs every adjoint stage as one 16-lane group's serial chain (~1,900
+// dependent VALU per stage, one wave, the other 240 lanes idle).  Here the four waves split the pullback of a
+// two-layer chain [I -> H -> O] by (output, basis feature): row r (16 lanes) of the block owns hidden unit r of
+// layer 1 and lane c its feature c = (input i, knot g | swish); wave o owns output o of layer 2 and lane c its
+// feature c.  Every lane evaluates ONE basis function (the reference formula, utils.jl:8-13, one exp), the
+// sums over features are DPP row / wave sums and LDS gathers, and every parameter cotangent (∂f/∂p)ᵀλ is
+// one lane's single product: kμ needs no reduction at all.  Seven block barriers per adjoint stage.
+constexpr int kWideF1 = 16;   // layer-1 features per hidden unit (one DPP row)
+constexpr int kWideF2 = 64;   // layer-2 features per output (one wave)
+struct WideShape {
+    int I, H, O, G1, G2;
+};
+__host__ __device__ inline bool wide_fits(const WideShape& w) {
+    return w.I >= 1 && w.O >= 1 && w.I == w.O && w.H <= kChainBlock / kWideF1 && w.I * (w.G1 + 1) <= kWideF1 &&
+           w.H * (w.G2 + 1) <= kWideF2 && w.O <= kChainBlock / kWave;
+}
+
+// One feature of a layer at input value x: c < G -> basis g = c of N(x), c == G -> swish(x).  feat, and the
+// rrule factors: for a basis the pullback factor -2·y·φ (times φ̄·invh later), for swish swish'(x).
+template <typename T, int NORM>
+__device__ __forceinline__ void wide_feature(const Math<T>& M, const LayerConst& lc, int g, T x, T& feat, T& pull,
+                                             T& dnorm) {
+    const T n = normalize<NORM, T>(M, lc.norm, x);
+    dnorm = dnormalize<NORM, T>(lc.norm, n);
+    if (g < lc.G) {
+        const T y = (n - (T)lc.grid[g]) * (T)lc.invh;
+        const T phi = M.exp_neg(-(y * y));
+        feat = phi;
+        pull = T(-2) * y * phi;   // basis_pull(BASIS_RBF, ·, y, φ, ·, 1)
+    } else {
+        T om, d;
+        swish_and_grad<T>(M, x, om, d);
+        feat = om;
+        pull = d;
+    }
+}
+
+template <typename T, int NORM>
+struct WideModel {
+    const Math<T>& M;
+    const LayerConst* lcl;   // [2] (LDS)
+    const T* ps;             // parameters (LDS)
+    T* sx;                   // LDS scratch (kWideScratch T)
+    int P;
+    bool act;
+    int64_t idx, n;
+    static constexpr int kX = 0, kYb = 16, kH = 32, kHb = 48, kY = 64, kCb2 = 80, kV2 = kCb2 + 4 * kWideF2,
+                         kCb1 = kV2 + kWideF2, kV1 = kCb1 + 16 * kWideF1, kEnd = kV1 + kWideF1;
+
+    // layer 1 row r, lane c: its feature of the inputs in sx[kX..]; returns the row sum h_r (all lanes)
+    __device__ T layer1(int r, int c, T& feat, T& pull, T& dnorm, T& coef) const {
+        const LayerConst& L1 = lcl[0];
+        const int per = L1.G + 1, H = L1.O;
+        const bool on = r < H && c < L1.I * per;
+        const int i = on ? c / per : 0, g = on ? c % per : 0;
+        wide_feature<T, NORM>(M, L1, g, sx[kX + i], feat, pull, dnorm);
+        coef = on ? (g < L1.G ? ps[L1.p_off + r + H * (g + L1.G * i)] : ps[L1.w_off + r + H * i]) : T(0);
+        return row16_sum(coef * feat);
+    }
+    __device__ T rhs(T y) {
+        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+        const int t = threadIdx.x, lane = t & (kWave - 1), r = t / kWideF1, c = t & (kWideF1 - 1), w = t / kWave;
+        if (act) sx[kX + idx] = y;
+        __syncthreads();
+        T f1, p1, d1, k1;
+        const T h = layer1(r, c, f1, p1, d1, k1);
+        if (c == 0 && r < L1.O) sx[kH + r] = h;
+        __syncthreads();
+        const int per = L2.G + 1, O = L2.O;
+        const bool on = w < O && lane < L2.I * per;
+        const int i = on ? lane / per : 0, g = on ? lane % per : 0;
+        T f2, p2, d2;
+        wide_feature<T, NORM>(M, L2, g, sx[kH + i], f2, p2, d2);
+        const T coef = on ? (g < L2.G ? ps[L2.p_off + w + O * (g + L2.G * i)] : ps[L2.w_off + w + O * i]) : T(0);
+        const T yo = wave_sum(coef * f2);
+        if (lane == 0 && w < O) sx[kY + w] = yo;
+        __syncthreads();
+        return act ? sx[kY + idx] : T(0);
+    }
+    __device__ T vjp(T y, T ls, T* __restrict__ km) {
+        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+        const int t = threadIdx.x, lane = t & (kWave - 1), r = t / kWideF1, c = t & (kWideF1 - 1), w = t / kWave;
+        if (act) {
+            sx[kX + idx] = y;
+            sx[kYb + idx] = ls;
+        }
+        __syncthreads();
+        // layer 1 forward: h_r, this lane's feature kept for its cotangent and the pullback
+        T f1, p1, d1, k1;
+        const T h = layer1(r, c, f1, p1, d1, k1);
+        if (c == 0 && r < L1.O) sx[kH + r] = h;
+        __syncthreads();
+        // layer 2: wave o lane c: dC2 / dW2 = ȳ_o·feature, and the feature's share of φ̄ = C2ᵀȳ
+        const int per2 = L2.G + 1, O = L2.O, H = L2.I;
+        {
+            const bool on = w < O && lane < H * per2;
+            const int i = on ? lane / per2 : 0, g = on ? lane % per2 : 0;
+            T f2, p2, d2;
+            wide_feature<T, NORM>(M, L2, g, sx[kH + i], f2, p2, d2);
+            if (on) {
+                const T yb = sx[kYb + w];
+                const int64_t q = g < L2.G ? L2.p_off + w + O * (g + L2.G * i) : L2.w_off + w + O * i;
+                km[q] = yb * f2;
+                sx[kCb2 + w * kWideF2 + lane] = ps[q] * yb;
+            }
+            __syncthreads();
+            // φ̄ of feature `lane` (Σ_o in order) and its rrule term: basis z̄·invh, swish swish'·φ̄
+            if (t < H * per2) {   // (waves >= O left their rows at zero: adding them is exact)
+                T pb = sx[kCb2 + t];
+#pragma unroll
+                for (int o = 1; o < kChainBlock / kWave; ++o) pb = pb + sx[kCb2 + o * kWideF2 + t];
+                sx[kV2 + t] = g < L2.G ? p2 * pb * (T)L2.invh : p2 * pb;
+                if (g == 0) sx[kHb + i] = d2;   // N'(h_i) (every basis lane of input i holds it)
+            }
+            __syncthreads();
+            // h̄_i = N'(h_i)·Σ_g z̄_g·invh + swish'(h_i)·φ̄_sw
+            if (t < H) {
+                T sb = T(0);
+#pragma unroll
+                for (int gg = 0; gg < kWideF1; ++gg)
+                    if (gg < L2.G) sb = sb + sx[kV2 + t * per2 + gg];
+                sx[kHb + t] = sx[kHb + t] * sb + sx[kV2 + t * per2 + L2.G];
+            }
+            __syncthreads();
+        }
+        // layer 1 backward: row r lane c: dC1 / dW1 = h̄_r·feature, and its share of φ̄ = C1ᵀh̄
+        const int per1 = L1.G + 1, I = L1.I;
+        {
+            const bool on = r < H && c < I * per1;
+            if (on) {
+                const int i = c / per1, g = c % per1;
+                const T hb = sx[kHb + r];
+                const int64_t q = g < L1.G ? L1.p_off + r + H * (g + L1.G * i) : L1.w_off + r + H * i;
+                km[q] = hb * f1;
+                sx[kCb1 + r * kWideF1 + c] = k1 * hb;
+            }
+            __syncthreads();
+            if (t < I * per1) {   // (rows >= H left their entries at zero: adding them is exact)
+                const int g = t % per1;
+                T pb = sx[kCb1 + t];
+#pragma unroll
+                for (int rr = 1; rr < kChainBlock / kWideF1; ++rr) pb = pb + sx[kCb1 + rr * kWideF1 + t];
+                sx[kV1 + t] = g < L1.G ? p1 * pb * (T)L1.invh : p1 * pb;
+            }
+            __syncthreads();
+        }
+        T xb = T(0);
+        if (act) {   // x̄_i = N'(x_i)·Σ_g z̄_g·invh + swish'(x_i)·φ̄_sw  (thread i = input i)
+            T sb = T(0);
+#pragma unroll
+            for (int gg = 0; gg < kWideF1; ++gg)
+                if (gg < L1.G) sb = sb + sx[kV1 + idx * per1 + gg];
+            // N'(x_i): lane c = i·per1 of row 0 evaluated it; recompute (one normalizer) rather than gather
+            const T nn = normalize<NORM, T>(M, L1.norm, y);
+            xb = dnormalize<NORM, T>(L1.norm, nn) * sb + sx[kV1 + idx * per1 + L1.G];
+        }
+        __syncthreads();   // (sx and km complete before the next stage / the caller's reads)
+        return xb;
+    }
+};
+
+// The adjoint of one trajectory of a two-layer chain over the whole workgroup (WideModel): the forward's dense
+// output is staged in LDS too (a single trajectory's is a few KB).
+template <typename T, int NORM>
+__global__ void __launch_bounds__(kChainBlock)
+kd_chain_adjoint_wide_kernel(const LayerConst* __restrict__ lcs, const T* __restrict__ p, int P, ChainAdjointArgs a,
+                             int stage_rec) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cw_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cw_raw);
+    T* ps = reinterpret_cast<T*>(cw_raw + 2 * sizeof(LayerConst));
+    T* sx = ps + P;                                  // WideModel scratch
+    T* mu = sx + WideModel<T, NORM>::kEnd;           // [2][P]
+    T* km = mu + 2 * (size_t)P;                      // [7][P]
+    double* tsl = reinterpret_cast<double*>(km + 7 * (size_t)P);
+    double* dtsl = tsl + a.nsteps;
+    {
+        const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cw_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int i = threadIdx.x; i < WideModel<T, NORM>::kEnd + 9 * P; i += blockDim.x) sx[i] = T(0);
+        for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
+            tsl[i] = a.ts[i];
+            dtsl[i] = a.dts[i];
+        }
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    __shared__ double red[kChainBlock / kWave];
+    const Math<T> M{tab};
+    const int N = lcl[0].I;
+    T* recl = nullptr;
+    if (stage_rec) {
+        recl = reinterpret_cast<T*>(dtsl + a.nsteps);
+        onewg_stage_rec<T>(recl, a, N);
+    }
+    WideModel<T, NORM> m{M, lcl, ps, sx, P, (int)threadIdx.x < N, (int64_t)threadIdx.x, (int64_t)N};
+    onewg_adjoint<T>(m, a, mu, km, tsl, dtsl, red, recl);
+}
 
 // The one-workgroup adjoint (kd_chain_adjoint_kernel): the small-chain conditions of
 // launch_kd_chain_tsit5 plus nsteps <= kChainAdjointMaxSteps and the LDS budget.
 template <typename T>
 hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
-                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st) {
+                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st, bool wide) {
     if (nl < 1 || nl > kChainMaxLayers || B < 1 || B > kChainSolveMaxBatch || I_ne_O(hlcs, nl) || a.nsteps < 1 ||
         a.nsteps > kChainAdjointMaxSteps)
         return hipErrorNotSupported;
+    // one trajectory of a two-layer chain with base activations: the whole workgroup on it (WideModel)
+    if (wide && B == 1 && nl == 2 && hlcs[0].use_base && hlcs[1].use_base && hlcs[0].norm == hlcs[1].norm &&
+        hlcs[1].I == hlcs[0].O && wide_fits(WideShape{hlcs[0].I, hlcs[0].O, hlcs[1].O, hlcs[0].G, hlcs[1].G}) &&
+        (hlcs[0].norm == NORM_TANH_FAST || hlcs[0].norm == NORM_SOFTSIGN)) {
+        const size_t pre = 2 * sizeof(LayerConst) + sizeof(T) * ((size_t)P * 10 + WideModel<T, NORM_SOFTSIGN>::kEnd);
+        size_t lds = pre + 2 * sizeof(double) * a.nsteps;
+        const size_t rec = sizeof(T) * ((size_t)a.nsteps * 7 + 1) * hlcs[0].I;   // the dense output, staged
+        const int stage_rec = lds + rec <= 60 * 1024 ? 1 : 0;
+        if (stage_rec) lds += rec;
+        if (pre % 8 == 0 && lds <= 60 * 1024) {
+            if (hlcs[0].norm == NORM_TANH_FAST)
+                hipLaunchKernelGGL((kd_chain_adjoint_wide_kernel<T, NORM_TANH_FAST>), dim3(1), dim3(kChainBlock), lds, st,
+                                   lcs, p, (int)P, a, stage_rec);
+            else
+                hipLaunchKernelGGL((kd_chain_adjoint_wide_kernel<T, NORM_SOFTSIGN>), dim3(1), dim3(kChainBlock), lds, st,
+                                   lcs, p, (int)P, a, stage_rec);
+            return hipGetLastError();
+        }
+    }
     for (int l = 0; l < nl; ++l) {
         const LayerConst& h = hlcs[l];
         if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
@@ -1539,7 +1465,7 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
     template hipError_t launch_kd_chain_tsit5<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,   \
                                                  const T*, int64_t, const ChainSolveArgs&, hipStream_t);         \
     template hipError_t launch_kd_chain_adjoint<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t, \
-                                                   int64_t, const ChainAdjointArgs&, hipStream_t);               \
+                                                   int64_t, const ChainAdjointArgs&, hipStream_t, bool);         \
     template hipError_t launch_kd_fwd_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, T*,        \
                                              int64_t, hipStream_t);                                               \
     template hipError_t launch_kd_vjp_col<T>(const LayerConst&, const LayerConst*, const T*, const T*, const T*,  \

@@ -349,13 +349,29 @@ struct PairAdjArgs {
     int max_wg;       // co-resident workgroups assumed at most (0: the occupancy query's capacity)
     int force_abort;  // tests: the abort word raised at launch (as an exchange time-out raises it)
 };
+// The Fisher-KPP problem at small sizes (kan_small.hip): the whole forward solve / adjoint in one workgroup,
+// wave = trajectory (B <= kFkSmallMaxBatch), lane = grid point (Nx <= 64, even), the pointwise KAN from the
+// piecewise-polynomial tables (built by the caller: PP_PHI for the solve, PP_DPHI + PP_SWISH for the adjoint).
+constexpr int kFkSmallMaxBatch = 16;
+struct FkSmallArgs {
+    int Nx, ni;
+    double inv_w, x0;   // PPConst
+    double cd, co;      // D·(-2/dx²), D/dx²
+};
+bool fk_small_supported(const LayerConst& hlc, const PPConst& hpc, int Nx, int64_t B);
+hipError_t launch_fk_small_tsit5(const LayerConst& hlc, const PPConst& hpc, const LayerConst* lc, const double* p,
+                                 const double* tables, const FkSmallArgs& s, const double* u0, int64_t B,
+                                 const ChainSolveArgs& a, hipStream_t st);
+hipError_t launch_fk_small_adjoint(const LayerConst& hlc, const PPConst& hpc, const LayerConst* lc, const double* p,
+                                   const double* tables, const FkSmallArgs& s, int64_t B, const ChainAdjointArgs& a,
+                                   hipStream_t st);
 int pair_adjoint_workgroups(const LayerConst* hl, int64_t B, int S);
 hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, const double* p, int64_t B,
                                   PairAdjArgs pa, hipStream_t st);
 constexpr int kChainAdjointMaxSteps = 1024;   // forward steps held in LDS
 template <typename T>
 hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
-                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st);
+                                   int64_t B, const ChainAdjointArgs& a, hipStream_t st, bool wide);
 // One Tsit5 step of a small chain per trajectory column (kd_chain_step_kernel, kan_col.hip)
 struct ChainStepArgs {
     double a[6][6];   // dt·a_sj

@@ -69,6 +69,7 @@ struct kanode_handle {
     int pair_persist_max_wg = 0;      // KANODE_OPT_PAIR_PERSIST_MAX_WG (0: the device's co-resident capacity)
     bool pair_persist_abort = false;  // KANODE_OPT_PAIR_PERSIST_ABORT (tests: raise the abort word at launch)
     int last_adjoint = KANODE_ADJ_NONE;   // KANODE_OPT_LAST_ADJOINT (read-only)
+    bool chain_wide = true;           // KANODE_OPT_CHAIN_WIDE
     bool adj_fused_finish = false;    // KANODE_OPT_ADJ_FUSED_FINISH (measured even with the finish launch)
     unsigned* fin_ctr = nullptr;      // its two arrival counters (device, zeroed at allocation)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
@@ -1093,6 +1094,7 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_PAIR_PERSIST_MAX_WG: return count(h->pair_persist_max_wg, "PAIR_PERSIST_MAX_WG", 1 << 20);
     case KANODE_OPT_PAIR_PERSIST_ABORT: return flag(h->pair_persist_abort, "PAIR_PERSIST_ABORT");
     case KANODE_OPT_LAST_ADJOINT: return fail(h, KANODE_ERR_INVALID_ARG, "LAST_ADJOINT is read-only");
+    case KANODE_OPT_CHAIN_WIDE: return flag(h->chain_wide, "CHAIN_WIDE");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -1116,6 +1118,7 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_PAIR_PERSIST_MAX_WG: return h->pair_persist_max_wg;
     case KANODE_OPT_PAIR_PERSIST_ABORT: return h->pair_persist_abort ? 1 : 0;
     case KANODE_OPT_LAST_ADJOINT: return h->last_adjoint;
+    case KANODE_OPT_CHAIN_WIDE: return h->chain_wide ? 1 : 0;
     }
     return -1;
 }
@@ -1349,7 +1352,24 @@ void kanode_internal_vjp_discard(kanode_handle* h) {
     h->njobs = 0;
     h->pend_valid = false;
 }
+// the Fisher-KPP RHS at the reference's own sizes (kan_small.hip): one workgroup per solve / adjoint
+static bool fk_small_ok(const kanode_handle* h, int64_t batch) {
+    return h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->spec.dtype == KANODE_F64 && h->pp_on &&
+           h->fused_solve && kan::fk_small_supported(h->hlc[0], h->hpc, (int)h->spec.nx, batch);
+}
+static kan::FkSmallArgs fk_small_args(const kanode_handle* h) {
+    kan::FkSmallArgs s{};
+    const double dx2 = h->spec.dx * h->spec.dx;
+    s.Nx = (int)h->spec.nx;
+    s.ni = h->hpc.ni;
+    s.inv_w = h->hpc.inv_w;
+    s.x0 = h->hpc.x0;
+    s.cd = h->spec.diffusion * (-2.0 / dx2);
+    s.co = h->spec.diffusion * (1.0 / dx2);
+    return s;
+}
 bool kanode_internal_chain_tsit5_ok(const kanode_handle* h, int64_t batch) {
+    if (fk_small_ok(h, batch)) return true;
     if (h->spec.rhs_kind != KANODE_RHS_CHAIN || batch < 1 || batch > kan::kChainSolveMaxBatch) return false;
     if (!h->fused_solve) return false;
     for (int l = 0; l < h->n_layers; ++l)
@@ -1543,10 +1563,23 @@ kanode_status kanode_internal_chain_adjoint(kanode_handle* h, const void* p, int
                                             const kan::ChainAdjointArgs* a, void* stream, bool& launched) {
     launched = false;
     const hipStream_t st = (hipStream_t)stream;
+    if (fk_small_ok(h, batch)) {
+        const int fns[2] = {kan::PP_DPHI, kan::PP_SWISH};
+        if (table_build(h, h->built_vjp))
+            HIP_TRY(h, kan::launch_fk_pp_build(h->hpc, h->dlc, h->dpc, (const double*)p, h->dtable, fns, 2, st));
+        const hipError_t e = kan::launch_fk_small_adjoint(h->hlc[0], h->hpc, h->dlc, (const double*)p, h->dtable,
+                                                          fk_small_args(h), batch, *a, st);
+        if (e == hipErrorNotSupported) return KANODE_OK;
+        if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_fk_small_adjoint: ") + hipGetErrorString(e));
+        launched = true;
+        return KANODE_OK;
+    }
     const hipError_t e =
         h->spec.dtype == KANODE_F64
-            ? kan::launch_kd_chain_adjoint<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P, batch, *a, st)
-            : kan::launch_kd_chain_adjoint<float>(h->hlc, h->n_layers, h->dlc, (const float*)p, h->P, batch, *a, st);
+            ? kan::launch_kd_chain_adjoint<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P, batch, *a, st,
+                                                   h->chain_wide)
+            : kan::launch_kd_chain_adjoint<float>(h->hlc, h->n_layers, h->dlc, (const float*)p, h->P, batch, *a, st,
+                                                  h->chain_wide);
     if (e == hipErrorNotSupported) return KANODE_OK;
     if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_adjoint: ") + hipGetErrorString(e));
     launched = true;
@@ -1578,6 +1611,17 @@ kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched) {
     launched = false;
     const hipStream_t st = (hipStream_t)stream;
+    if (fk_small_ok(h, batch)) {
+        const int fn = kan::PP_PHI;
+        if (table_build(h, h->built_phi))
+            HIP_TRY(h, kan::launch_fk_pp_build(h->hpc, h->dlc, h->dpc, (const double*)p, h->dtable, &fn, 1, st));
+        const hipError_t e = kan::launch_fk_small_tsit5(h->hlc[0], h->hpc, h->dlc, (const double*)p, h->dtable,
+                                                        fk_small_args(h), (const double*)u0, batch, *a, st);
+        if (e == hipErrorNotSupported) return KANODE_OK;
+        if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_fk_small_tsit5: ") + hipGetErrorString(e));
+        launched = true;
+        return KANODE_OK;
+    }
     const hipError_t e =
         h->spec.dtype == KANODE_F64
             ? kan::launch_kd_chain_tsit5<double>(h->hlc, h->n_layers, h->dlc, (const double*)p, h->P,

@@ -96,13 +96,15 @@ OPT_ADJ_FUSED_FINISH = 13
 OPT_PAIR_PERSIST_MAX_WG = 14
 OPT_PAIR_PERSIST_ABORT = 15
 OPT_LAST_ADJOINT = 16      # read-only: a kanode_adjoint_path value
+OPT_CHAIN_WIDE = 17
 ADJ_NONE, ADJ_HOST_LOOP, ADJ_CHAIN_WG, ADJ_PAIR_PERSIST, ADJ_PAIR_FALLBACK = 0, 1, 2, 3, 4   # kanode_adjoint_path
 OPTIONS = {"pointwise_table": OPT_POINTWISE_TABLE, "fused_step": OPT_FUSED_STEP, "fused_solve": OPT_FUSED_SOLVE,
            "fused_solve_cap": OPT_FUSED_SOLVE_CAP, "grid_rhs": OPT_GRID_RHS, "grid_vjp": OPT_GRID_VJP,
            "grid_adj_step": OPT_GRID_ADJ_STEP, "adj_step_rows": OPT_ADJ_STEP_ROWS, "pair_vjp": OPT_PAIR_VJP,
            "pair_fuse": OPT_PAIR_FUSE, "pair_persist": OPT_PAIR_PERSIST, "pair_persist_s": OPT_PAIR_PERSIST_S,
            "adj_fused_finish": OPT_ADJ_FUSED_FINISH, "pair_persist_max_wg": OPT_PAIR_PERSIST_MAX_WG,
-           "pair_persist_abort": OPT_PAIR_PERSIST_ABORT, "last_adjoint": OPT_LAST_ADJOINT}
+           "pair_persist_abort": OPT_PAIR_PERSIST_ABORT, "last_adjoint": OPT_LAST_ADJOINT,
+           "chain_wide": OPT_CHAIN_WIDE}
 
 SIGNATURES = [
     ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),

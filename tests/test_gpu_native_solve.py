@@ -855,3 +855,85 @@ def test_dense_saveat_batches_per_step(name):
     else:
         assert abs(nat.stats["naccept"] - py.stats["naccept"]) <= 2
         assert (nat.u - py.u).abs().max().item() <= 20 * opt.reltol * scale
+
+
+@pytest.mark.parametrize("nx,B,G,norm", [(26, 1, 10, "softsign"), (64, 3, 10, "softsign"), (16, 16, 5, "tanh_fast"),
+                                         (40, 5, 10, "tanh_fast")])
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_fk_small_one_workgroup_matches_host_loop(nx, B, G, norm, adaptive):
+    """the Fisher-KPP problem at the reference's own size (Fisher-KPP_Source.jl:34-49: 26 points,
+    one IC) runs the whole forward solve and the whole InterpolatingAdjoint as one workgroup each
+    (kan_small.hip: wave = trajectory, lane = grid point, KAN from the LDS tables) instead of the host loop's
+    per-step launches.  Against the host loop (KANODE_OPT_FUSED_SOLVE = 0): the forward RHS is the same
+    arithmetic per point (pp_pair_finish's order), so at fixed steps the saveat values are equal to the
+    error-norm-free rounding (bitwise in practice); the adjoint's per-point pullback is the table one
+    (pp_vjp_point) where the host loop at these Nx runs the recurrence kernel, both within 1e-14 of the
+    derivative scale (test_gpu_pp.py), so the gradients agree to ~n_steps·1e-14.  Adaptive: the block-summed
+    error norms round differently from the host loop's, so the step sizes differ at rounding level: the
+    solutions agree to the tolerance, and where that leaves an accept/reject elsewhere (a stability-limited
+    adjoint of a few hundred steps) the step counts to 1% and the gradients to 50·reltol (as
+    test_native_adjoint_matches_python_adjoint)."""
+    rhs = _fk_cfg(nx, G, norm)
+    u0 = t(fk_u0(nx, B, 9))
+    p0 = t(np.random.default_rng(nx + B).uniform(-1.0, 1.0, G + 1))
+    ts = [0.0, 0.5, 1.0, 1.5, 2.0]
+    opt = kanode.Tsit5Options(abstol=1e-9, reltol=1e-9) if adaptive else kanode.Tsit5Options(adaptive=False, dt=0.02)
+    w = t(np.random.default_rng(5).normal(size=(len(ts),) + tuple(u0.shape)))
+    out = []
+    for fused in (1, 0):
+        with rhs.hd.options(fused_solve=fused):
+            p = p0.clone().requires_grad_(True)
+            x0 = u0.clone().requires_grad_(True)
+            sol = kanode.solve(rhs, x0, (0.0, 2.0), p, ts, opt, sensealg="interpolating_adjoint")
+            g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
+            out.append((sol.u.detach(), g, gu, sol.stats, rhs.hd.get_option("last_adjoint")))
+    (u1, g1, gu1, s1, path1), (u0_, g0, gu0, s0, path0) = out
+    assert path1 == L.ADJ_CHAIN_WG and path0 == L.ADJ_HOST_LOOP
+    scale = u0_.abs().max().item()
+    if not adaptive:
+        assert s1["naccept"] == s0["naccept"] and s1["adjoint"]["naccept"] == s0["adjoint"]["naccept"]
+        assert (u1 - u0_).abs().max().item() <= 1e-13 * scale
+        bar = 1e-11
+    else:
+        assert s1["naccept"] == s0["naccept"]
+        assert (u1 - u0_).abs().max().item() <= 10 * opt.reltol * scale
+        na, nb = s1["adjoint"]["naccept"], s0["adjoint"]["naccept"]
+        assert abs(na - nb) <= 0.01 * nb
+        bar = 1e-9 if na == nb else 50 * opt.reltol
+    assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
+    assert (gu1 - gu0).abs().max().item() <= bar * gu0.abs().max().item()
+
+
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_lv1_wide_adjoint_matches_group_adjoint_and_oracle(adaptive):
+    """one Lotka-Volterra trajectory (LV_driver_KANODE.jl:180-184,279-291, BASELINE configs[0])
+    runs its adjoint with the pullback spread over the whole workgroup (kd_chain_adjoint_wide_kernel: one basis
+    function per lane, every parameter cotangent one lane's product) instead of one 16-lane group.  Against the
+    group kernel (KANODE_OPT_CHAIN_WIDE = 0) and against the Python driver over the CPU oracle chain: equal step
+    counts, gradients to 1e-10 (the basis values come from the per-knot formula here and from the Gaussian
+    recurrence in the group kernel, both within ~3e-15 of each other)."""
+    from oracle_rhs import OracleChainRHS
+    specs = [O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")]
+    u0 = np.array([[1.0, 1.0]])
+    p0 = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5)).setup(np.random.default_rng(4))[0] / 10
+    ts = [0.1 * i for i in range(35)]
+    w = np.random.default_rng(6).normal(size=(len(ts), 1, 2))
+    opt = kanode.Tsit5Options(abstol=1e-9, reltol=1e-9) if adaptive else kanode.Tsit5Options(adaptive=False, dt=0.01)
+
+    def grad(f, dev):
+        p = torch.as_tensor(p0.astype(np.float64), device=dev).requires_grad_(True)
+        x0 = torch.as_tensor(u0, device=dev).requires_grad_(True)
+        sol = kanode.solve(f, x0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
+        g, gu = torch.autograd.grad((sol.u * torch.as_tensor(w, device=dev)).sum(), [p, x0])
+        return g.cpu(), gu.cpu(), sol.stats["adjoint"]["naccept"]
+
+    rhs = lv()
+    gw, guw, nw = grad(rhs, device())
+    assert rhs.hd.get_option("last_adjoint") == L.ADJ_CHAIN_WG
+    with rhs.hd.options(chain_wide=0):
+        gg, gug, ng = grad(rhs, device())
+        assert rhs.hd.get_option("last_adjoint") == L.ADJ_CHAIN_WG
+    gc, guc, nc = grad(OracleChainRHS(specs), "cpu")
+    assert nw == ng == nc
+    for a_, b_ in ((gw, gg), (gw, gc), (guw, gug), (guw, guc)):
+        assert (a_ - b_).abs().max().item() <= 1e-10 * b_.abs().max().item()

@@ -33,7 +33,8 @@ for f in files:
     for r, d in zip(rows, dem):
         if a.grep and a.grep not in d:
             continue
-        d = re.sub(r"\(.*", "", d.replace("kan::", "").replace("void ", ""))
+        d = d.replace("(anonymous namespace)::", "").replace("kan::", "").replace("void ", "")
+        d = re.sub(r"\(.*", "", d)
         print(f"{d[:72]:72s} vgpr={r.get('VGPRs', '?'):>4s} agpr={r.get('AGPRs', '?'):>3s} "
               f"scratch={r.get('ScratchSize [bytes/lane]', '?'):>4s} occ={r.get('Occupancy [waves/SIMD]', '?'):>2s} "
               f"lds={r.get('LDS Size [bytes/block]', '?'):>6s}")
