@@ -193,6 +193,16 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     with base activations (the Lotka-Volterra driver's shape) spreads the pullback over the whole
  *     workgroup, one basis function per lane (kd_chain_adjoint_wide_kernel); 0 = the 16-lane group of
  *     the batched kernel.  Same formulas; sums in another order.
+ *   KANODE_OPT_RECORD_ADJOINT_STEPS (default 0): 1 = kanode_adjoint_tsit5 keeps the accepted step
+ *     sizes of its backward integration on the handle (kanode_adjoint_step_sizes), on every path
+ *     (the one-launch adjoints write them from the device, up to 4 x the forward steps + 1024).
+ *     Diagnostics: two solvers' step sequences show whether their controllers took the same path.
+ *   KANODE_OPT_FK_DEVICE_LOOP (default 1): an adaptive Fisher-KPP table-path solve that keeps its dense
+ *     output (control = auto) runs its step control on the device: each step launch reads its step size
+ *     and writes the next (its last workgroup runs the PI controller), the host queues launches ahead and
+ *     never waits on a step; the saveat values are formed from the dense output afterwards.  0 = the host
+ *     loop (one norm read per step).  Same controller arithmetic; the device's pow may differ from the
+ *     host's in the last bit, so step sizes agree to rounding, not bitwise.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {
@@ -212,7 +222,9 @@ typedef enum {
     KANODE_OPT_PAIR_PERSIST_MAX_WG = 14,
     KANODE_OPT_PAIR_PERSIST_ABORT = 15,
     KANODE_OPT_LAST_ADJOINT = 16,
-    KANODE_OPT_CHAIN_WIDE = 17
+    KANODE_OPT_CHAIN_WIDE = 17,
+    KANODE_OPT_RECORD_ADJOINT_STEPS = 18,
+    KANODE_OPT_FK_DEVICE_LOOP = 19
 } kanode_option;
 typedef enum {
     KANODE_ADJ_NONE = 0,            /* no adjoint on this handle yet */
@@ -324,6 +336,9 @@ typedef struct {
 typedef struct kanode_solution kanode_solution;
 void kanode_solution_free(kanode_solution* sol);
 int64_t kanode_solution_steps(const kanode_solution* sol);
+/* The accepted steps of the solve: ts[i] (start time) and dts[i] (step size) for
+ * i < min(steps, cap) (host arrays, either may be NULL).  Returns the step count, -1 for NULL. */
+int64_t kanode_solution_step_sizes(const kanode_solution* sol, double* ts, double* dts, int64_t cap);
 
 /* u_save[n_save, N, B] (device) <- u(saveat[j]); saveat (host, ascending, within
  * [t0, tf]).  dense: NULL = no dense output kept; else *dense (NULL or an object to
@@ -339,6 +354,10 @@ kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0
 kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,
                                    const void* dl_du, void* du0, void* dp, const kanode_solver_options* opt,
                                    kanode_solve_stats* stats, void* stream);
+/* KANODE_OPT_RECORD_ADJOINT_STEPS: the accepted step sizes of the handle's last kanode_adjoint_tsit5
+ * (in backward order), out[i] for i < min(count, cap) (out may be NULL).  Returns the count (0 when not
+ * recorded), -1 for NULL. */
+int64_t kanode_adjoint_step_sizes(const kanode_handle* h, double* out, int64_t cap);
 
 /* --- the optimiser step after the gradient all-reduce -----------
  * Flux 0.14 Optimise.Adam + update!(opt, x, Δ) (LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:

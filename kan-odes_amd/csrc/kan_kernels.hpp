@@ -133,6 +133,41 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
                              int grid_ovr = 0, int* parts_out = nullptr);
 // (parts_out != nullptr with err_out: the per-block error partials are left in err_slab[0, *parts_out)
 // for the caller to sum -- the host, from mapped memory -- instead of a final reduction launch)
+
+// The adaptive Fisher-KPP solve with the step control on the device (kanode_solve.cpp solve_fk_loop): each
+// launch of the step kernel reads the step size and the step index from `ctl`, takes the step into the
+// dense-output slots of the table, and its last workgroup to finish sums the error partials and runs the PI
+// controller (solve_t's arithmetic): accept/reject, the step record ts/dts, the next step size.  The host
+// enqueues launches ahead without waiting on any of them; a launch after the end returns at once.
+struct StepCoef {
+    double a[6][6];   // dt·a_sj
+    double e[7];      // dt·btilde_j
+    double q[4][7];   // dt·RI[i][m] (qform)
+    double abstol, reltol;
+};
+struct FkLoopCtl {
+    double t, dt, qold;
+    int64_t step, nreject, it;   // accepted steps, rejections, attempts
+    int32_t status;              // 0 running, 1 done, 2 maxiters reached
+    int32_t pad;
+};
+struct FkLoopArgs {
+    FkLoopCtl* ctl;        // device state
+    FkLoopCtl* mirror;     // the host's mapped copy (device address), written with ctl
+    StepCoef* coef;        // [2] the attempt's coefficients, by attempt parity (it & 1)
+    void* const* slots;    // [cap] dense-output slots (u_n, Q_1..Q_4, k_7 of n entries each)
+    const double* k1_0;    // k_1 of the first step
+    double* ts;            // [cap] accepted steps: start time, step size
+    double* dts;
+    double* parts;         // [grid] error partials of a launch
+    unsigned* arrive;      // the launch's arrival counter (0 between launches)
+    int64_t n;             // state entries (Nx·B): the error norm's count and the slot vector stride
+    double tf, abstol, reltol, dtmin, beta1, beta2, gamma, qmin, qmax, qoldinit;
+    int64_t maxiters;
+};
+hipError_t launch_fk_step_pp_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, double cd,
+                                  double co, int Nx, const double* p, const double* table, const FkLoopArgs& la,
+                                  int64_t B, int max_grid, hipStream_t st, int grid_ovr = 0);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,
@@ -333,6 +368,8 @@ struct ChainAdjointArgs {
     void* du0;              // [n] or null
     void* dp;               // [P] or null
     int64_t* out;           // naccept, nreject, nf, status (0 ok, 1 maxiters)
+    double* hs;             // [hs_cap] accepted adjoint step sizes, in order (KANODE_OPT_RECORD_ADJOINT_STEPS), or null
+    int64_t hs_cap;
 };
 // The whole InterpolatingAdjoint of a surrogate pair KDense(N -> H) + KDense(H -> N) in ONE launch
 // (kd_pair_adjoint_kernel, kan_pair_adj.hip): the grid split over workgroups of S points, two exchanges

@@ -21,32 +21,9 @@
 #pragma once
 #include "kan_common.hpp"
 #include "kan_kernels.hpp"
+#include "kan_tsit5.hpp"
 
 namespace kan {
-
-struct Tsit5Tab {
-    static constexpr double TC[6] = {0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0};
-    static constexpr double TA[6][6] = {
-        {0.161, 0, 0, 0, 0, 0},
-        {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
-        {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
-        {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
-        {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
-        {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774},
-    };
-    static constexpr double BT[7] = {-0.00178001105222577714, -0.0008164344596567469, 0.007880878010261995,
-                                     -0.1447110071732629,     0.5823571654525552,     -0.45808210592918697,
-                                     0.015151515151515152};
-    static constexpr double RI[7][4] = {
-        {1.0, -2.763706197274826, 2.9132554618219126, -1.0530884977290216},
-        {0.0, 0.13169999999999998, -0.2234, 0.1017},
-        {0.0, 3.9302962368947516, -5.941033872131505, 2.490627285651253},
-        {0.0, -12.411077166933676, 30.33818863028232, -16.548102889244902},
-        {0.0, 37.50931341651104, -88.1789048947664, 47.37952196281928},
-        {0.0, -27.896526289197286, 65.09189467479366, -34.87065786149661},
-        {0.0, 1.5, -4.0, 2.5},
-    };
-};
 
 // Σ over the block of v (inactive entries give 0), the same ordered total in every thread.  red: LDS of
 // blockDim / 64 doubles.
@@ -238,7 +215,12 @@ __device__ __forceinline__ void onewg_adjoint(Mdl& m, const ChainAdjointArgs& a,
                 y = kfma<T>((T)(b * dti), kv[q], y);
             }
         }
+#ifdef KAN_ONEWG_NOVJP   // timing experiment only: the driver without the model's pullback (wrong results)
+        (void)slot;
+        return y * ls;
+#else
         return m.vjp(y, act ? ls : T(0), km + (size_t)slot * P);
+#endif
     };
     T lam = T(0);
     if (dl) lam = add_rows(0, lam);
@@ -351,6 +333,7 @@ __device__ __forceinline__ void onewg_adjoint(Mdl& m, const ChainAdjointArgs& a,
         mc ^= 1;
         kl[0] = kl[6];     // FSAL
         k0 = ks[6];
+        if (a.hs && threadIdx.x == 0 && naccept < a.hs_cap) a.hs[naccept] = h;
         ++naccept;
         if (::fabs(tau - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT)) {
             tau = a.stops[si];

@@ -711,6 +711,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
                 for (int e = t; e < SB; e += kPA) lam[e] = lsv[e];   // λ <- λ_new + ∂L/∂u(t_j)
                 mc ^= 1;
                 k0 = ks[6];
+                if (a.hs && blockIdx.x == 0 && t == 0 && naccept < a.hs_cap) a.hs[naccept] = h;
                 ++naccept;
                 xbar(5, k0, k0);   // u_modified!: FSAL re-evaluated at τ (stage slot 5's forward half)
                 ++nf;
@@ -725,6 +726,7 @@ kd_pair_adjoint_kernel(const LayerConst* __restrict__ lcs, const double* __restr
         mc ^= 1;
         k0 = ks[6];        // FSAL: kλ_7, kμ_7 become the next step's first stage values
         __syncthreads();
+        if (a.hs && blockIdx.x == 0 && t == 0 && naccept < a.hs_cap) a.hs[naccept] = h;
         ++naccept;
         if (::fabs(tau - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT)) {
             tau = a.stops[si];

@@ -22,6 +22,7 @@
 #include "kan_kernels.hpp"
 #include "kan_lap.hpp"
 #include "kan_pp_point.hpp"
+#include "kan_tsit5.hpp"
 
 #include <cstdlib>
 
@@ -940,9 +941,6 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
 #ifndef KAN_VROWS_L2LOAD
 #define KAN_VROWS_L2LOAD 0
 #endif
-#ifndef KAN_VROWS_PF
-#define KAN_VROWS_PF 0
-#endif
 // NI > 0: the table's interval count compiled in, so the Horner coefficients' LDS offsets are instruction
 // immediates (as fk_vjp_pp_wave_kernel; round 4: the per-point address arithmetic of the runtime count
 // was ~8 VALU per point and stage)
@@ -1126,9 +1124,6 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     const RecScalars<double> rc(lc);
     const int P = GT + (lc.use_base ? 1 : 0);
     double eacc = 0.0;
-#if KAN_VROWS_PF
-    double pf0 = 0.0, pf1 = 0.0;
-#endif
     // (a runtime flag: a compile-time one made the fixed-step instantiation spill 1.2 KB/lane, and the
     // adaptive one, which is launched only to combine, 168 B/lane: round 5, 57 -> 69 us per step)
     const bool combine = a.combine != 0;
@@ -1158,24 +1153,6 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
                     for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[s][m] + rbl + kOff * k);
                 }
             }
-#if KAN_VROWS_PF
-            // The row this wave's slot takes in the next dispatch round (block + gridDim: the same XCD under
-            // the round-robin workgroup placement) is pulled into L2 during the last stage: one 8-byte load per
-            // 128-byte line of its seven input arrays (16 lines each), issued after this stage's own loads so
-            // their waits do not include it; the values are consumed only at the very end of the kernel.
-            if (last) {
-                const int64_t nb = b + (int64_t)gridDim.x * (kVjpBlock / kWave);
-                if (nb < B) {
-                    // lines 0..111 of the 7 x 16: lane l takes line l (arrays 0..3) and line 64 + l (arrays 4..6)
-                    const int q = lane >> 4;
-                    const double* a0 = q == 0 ? a.lam : q == 1 ? a.kl[0] : q == 2 ? a.su_u[0] : a.su_q[0][0];
-                    const double* a1 = q == 0 ? a.su_q[0][1] : q == 1 ? a.su_q[0][2] : a.su_q[0][3];
-                    const int64_t off = nb * Nx + (lane & 15) * 16;
-                    pf0 = a0[off];
-                    if (q < 3) pf1 = a1[off];
-                }
-            }
-#endif
             kd2 uv[NP], lv[NP], ev[NP];
             // λs first (registers only): a reloaded stage's dense output is still in flight
 #pragma unroll
@@ -1332,9 +1309,6 @@ fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __rest
         static_assert(kVjpBlock == kAdjFinBlock, "the fused finish runs adj_finish_kernel's blocks in its order");
         if (a.fin_ctr) rows_fused_finish(a.fin, a.fin_ctr, P);
     }
-#if KAN_VROWS_PF
-    asm volatile("" ::"v"(pf0), "v"(pf1));   // (the prefetch loads' values, so they are issued and awaited)
-#endif
 }
 
 // dp[q] (= or +=) Σ_b slab[b·P + q] for q < P (block q), and err_out[0] = Σ_b err_slab[b]
@@ -1449,12 +1423,6 @@ __device__ __forceinline__ void fk_row_rhs(const Math<double>& M, const LayerCon
 // dense output slot), instead of six stage launches re-reading u and k_1..k_s.  Same
 // arithmetic and order as six fk_stage_pp_wave_kernel launches (bitwise equal results);
 // the embedded-error partial Σ (e/sk)² goes to err_slab[block] (ordered).
-struct StepCoef {
-    double a[6][6];   // dt·a_sj
-    double e[7];      // dt·btilde_j
-    double q[4][7];   // dt·RI[i][m] (qform)
-    double abstol, reltol;
-};
 struct StepOut {
     double* k[6];     // k_2..k_7, or (qform) Q_1..Q_4, -, k_7
     double* u_new;
@@ -1463,15 +1431,93 @@ struct StepOut {
 #ifndef KAN_FSTEP_WPE
 #define KAN_FSTEP_WPE KAN_PP_WPE
 #endif
-template <int NORM, int BASIS, int NP>
+
+// The step control of a device-controlled solve (FkLoopArgs), run by the last workgroup of the step launch to
+// arrive: every workgroup has stored its error partial (agent-scope stores, drained) and counts itself in;
+// the last sums the partials in block order, then thread 0 applies solve_t's PI controller to the step and
+// writes the state for the next launch (and its host mirror).  Nothing waits: the other workgroups leave.
+__device__ __forceinline__ void fk_loop_coef(StepCoef* k, double dt) {
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) k->a[i][j] = j <= i ? dt * Tsit5Tab::TA[i][j] : 0.0;
+    for (int j = 0; j < 7; ++j) k->e[j] = dt * Tsit5Tab::BT[j];
+    for (int m = 0; m < 4; ++m)
+        for (int i = 0; i < 7; ++i) k->q[m][i] = dt * Tsit5Tab::RI[i][m];
+}
+__device__ __forceinline__ void fk_loop_control(const FkLoopArgs& la) {
+    __shared__ unsigned arr;
+    __shared__ double fred[kBlock / kWave];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's partial has landed
+    __syncthreads();
+    if (threadIdx.x == 0) arr = __hip_atomic_fetch_add(la.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned G = gridDim.x;
+    if (arr != G - 1u) return;
+    double s = 0.0;
+    for (unsigned b = threadIdx.x; b < G; b += kBlock) s += ld_agent(la.parts + b);
+    const double v[1] = {s};
+    block_sum_to<double, 1>(v, 1, fred, fred);   // (fred[0] <- the total; the block's order is fixed)
+    if (threadIdx.x != 0) return;
+    FkLoopCtl c = *la.ctl;
+    const double eest = ::sqrt(fred[0] / (double)la.n);
+    const double q11 = eest > 0 ? ::pow(eest, la.beta1) : 0.0;
+    ++c.it;
+    if (eest > 1.0 && c.dt > la.dtmin) {
+        ++c.nreject;
+        c.dt = c.dt / ::fmin(1.0 / la.qmin, q11 / la.gamma);
+    } else {
+        double q = q11 / ::pow(c.qold, la.beta2);
+        q = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, q / la.gamma));
+        if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
+        const double dtnew = q > 0 ? c.dt / q : c.dt * la.qmax;
+        c.qold = ::fmax(eest, la.qoldinit);
+        la.ts[c.step] = c.t;
+        la.dts[c.step] = c.dt;
+        c.t = c.t + c.dt;
+        ++c.step;
+        c.dt = dtnew;
+    }
+    if (c.t >= la.tf - 1e-14 * ::fmax(1.0, ::fabs(la.tf))) c.status = 1;
+    else if (c.it >= la.maxiters) c.status = 2;
+    else c.dt = ::fmin(c.dt, la.tf - c.t);   // (solve_t clips at the top of its next iteration)
+    if (c.status == 0) fk_loop_coef(la.coef + (c.it & 1), c.dt);
+    *la.ctl = c;
+    *la.mirror = c;
+    __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// DEV (FkLoopArgs, solve_fk_loop): the step index comes from la.ctl, the coefficients from la.coef (the
+// controller's products of dt and the tableau, as the host forms them), the vectors are the slots of the
+// table, and the last workgroup to finish runs the step control (fk_loop_control).
+template <int NORM, int BASIS, int NP, bool DEV = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_FSTEP_WPE)))
 fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                        const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
                        const double* __restrict__ u, const double* __restrict__ k1, StepOut so, StepCoef sc,
-                       double* __restrict__ err_slab, int64_t B) {
+                       double* __restrict__ err_slab, int64_t B, FkLoopArgs la) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[kBlock / kWave];
+    // DEV: the attempt's coefficients, read through the constant address space (scalar loads the compiler may
+    // repeat anywhere, as it does for kernel arguments: the controller writes the other buffer)
+    typedef const __attribute__((address_space(4))) StepCoef ConstCoef;
+    ConstCoef* cf = nullptr;
+    if constexpr (DEV) {
+        const FkLoopCtl* c = la.ctl;
+        if (c->status != 0) return;   // the solve has ended: a launch the host queued ahead
+        const int64_t step = c->step;
+        cf = (ConstCoef*)(la.coef + (c->it & 1));
+        double* const cur = static_cast<double*>(la.slots[step]);
+        u = cur;
+        k1 = step == 0 ? la.k1_0 : static_cast<const double*>(la.slots[step - 1]) + 5 * la.n;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) so.k[m] = cur + (m + 1) * la.n;
+        so.k[5] = cur + 5 * la.n;
+        so.u_new = static_cast<double*>(la.slots[step + 1]);
+        err_slab = la.parts;
+    }
+    auto ca = [&](int s_, int j) { return DEV ? cf->a[s_][j] : sc.a[s_][j]; };   // dt·a_sj
+    auto ce = [&](int j) { return DEV ? cf->e[j] : sc.e[j]; };                     // dt·btilde_j
+    auto cq = [&](int m, int i) { return DEV ? cf->q[m][i] : sc.q[m][i]; };        // dt·RI[i][m]
+    const double abstol = DEV ? la.abstol : sc.abstol, reltol = DEV ? la.reltol : sc.reltol;
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
@@ -1495,17 +1541,17 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                 y[k] = uv[k];
 #pragma unroll
                 for (int j = 0; j <= s; ++j) {
-                    y[k].x = ::fma(sc.a[s][j], kk[j][k].x, y[k].x);
-                    y[k].y = ::fma(sc.a[s][j], kk[j][k].y, y[k].y);
+                    y[k].x = ::fma(ca(s, j), kk[j][k].x, y[k].x);
+                    y[k].y = ::fma(ca(s, j), kk[j][k].y, y[k].y);
                 }
             }
             fk_row_rhs<NORM, BASIS, NP>(M, lc, p, tl, ni, inv_w, x0, cd, co, lane, y, kk[s + 1]);
-            if (!so.qform) {
+            if (!DEV && !so.qform) {
 #pragma unroll
                 for (int k = 0; k < NP; ++k) st_stream(so.k[s] + rb + 128 * k, kk[s + 1][k]);
             }
         }
-        if (so.qform) {   // the interpolation polynomials of the dense output, then k_7 (FSAL)
+        if (DEV || so.qform) {   // the interpolation polynomials of the dense output, then k_7 (FSAL)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
 #pragma unroll
@@ -1513,8 +1559,8 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                     kd2 q{0.0, 0.0};
 #pragma unroll
                     for (int i = 0; i < 7; ++i) {
-                        q.x = ::fma(sc.q[m][i], kk[i][k].x, q.x);
-                        q.y = ::fma(sc.q[m][i], kk[i][k].y, q.y);
+                        q.x = ::fma(cq(m, i), kk[i][k].x, q.x);
+                        q.y = ::fma(cq(m, i), kk[i][k].y, q.y);
                     }
                     st_stream(so.k[m] + rb + 128 * k, q);
                 }
@@ -1529,19 +1575,23 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                 kd2 e{0.0, 0.0};
 #pragma unroll
                 for (int j = 0; j < 6; ++j) {
-                    e.x = ::fma(sc.e[j], kk[j][k].x, e.x);
-                    e.y = ::fma(sc.e[j], kk[j][k].y, e.y);
+                    e.x = ::fma(ce(j), kk[j][k].x, e.x);
+                    e.y = ::fma(ce(j), kk[j][k].y, e.y);
                 }
-                const double ex = ::fma(sc.e[6], kk[6][k].x, e.x), ey = ::fma(sc.e[6], kk[6][k].y, e.y);
-                const double sx = ::fma(sc.reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), sc.abstol);
-                const double sy = ::fma(sc.reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), sc.abstol);
+                const double ex = ::fma(ce(6), kk[6][k].x, e.x), ey = ::fma(ce(6), kk[6][k].y, e.y);
+                const double sx = ::fma(reltol, fmax(kabs(uv[k].x), kabs(y[k].x)), abstol);
+                const double sy = ::fma(reltol, fmax(kabs(uv[k].y), kabs(y[k].y)), abstol);
                 const double rx = ex / sx, ry = ey / sy;
                 eacc = ::fma(rx, rx, eacc);
                 eacc = ::fma(ry, ry, eacc);
             }
         }
     }
-    if (want_err) {
+    if constexpr (DEV) {
+        const double v[1] = {eacc};
+        block_sum_to<double, 1, true>(v, 1, red, err_slab + blockIdx.x);
+        fk_loop_control(la);
+    } else if (want_err) {
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
     }
@@ -1756,7 +1806,8 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
         const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
         grid = grid_for(B, kBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,  \
-                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, k1, so, sc, slab, B);    \
+                           (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, k1, so, sc, slab, B,    \
+                           FkLoopArgs{});                                                                        \
     } while (0)
 #define KAN_STEP_GO(NORM, BASIS)                                                                                 \
     do {                                                                                                         \
@@ -1776,6 +1827,37 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
         return hipSuccess;
     }
     return launch_stage_error_final(err_slab, grid, err_out, st);
+}
+
+// One attempt of the device-controlled solve (FkLoopArgs): the step kernel's DEV instantiation over a grid of
+// at most max_grid workgroups (la.parts holds that many partials).  The tables must already be built.
+hipError_t launch_fk_step_pp_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, double cd,
+                                  double co, int Nx, const double* p, const double* table, const FkLoopArgs& la,
+                                  int64_t B, int max_grid, hipStream_t st, int grid_ovr) {
+    if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
+    const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+#define KAN_LOOP_WAVE(NORM, BASIS, NP)                                                                           \
+    do {                                                                                                         \
+        static int cap = 0;                                                                                      \
+        if (!cap) cap = pp_grid_cap(fk_step_pp_wave_kernel<NORM, BASIS, NP, true>, lds);                        \
+        const int gcap = grid_ovr > 0 ? grid_ovr : cap;                                                          \
+        const int grid = grid_for(B, kBlock / kWave, gcap < max_grid ? gcap : max_grid);                        \
+        hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP, true>), dim3(grid), dim3(kBlock), lds, st,  \
+                           lc, p, (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, nullptr, nullptr,  \
+                           StepOut{}, StepCoef{}, nullptr, B, la);                                               \
+    } while (0)
+#define KAN_LOOP_GO(NORM, BASIS)                                                                                 \
+    do {                                                                                                         \
+        if (Nx == 256) KAN_LOOP_WAVE(NORM, BASIS, 2);                                                            \
+        else if (Nx == 128) KAN_LOOP_WAVE(NORM, BASIS, 1);                                                       \
+        else KAN_LOOP_WAVE(NORM, BASIS, 4);                                                                      \
+    } while (0)
+    if (hlc.basis == BASIS_RBF && hlc.norm == NORM_SOFTSIGN) KAN_LOOP_GO(NORM_SOFTSIGN, BASIS_RBF);
+    else if (hlc.basis == BASIS_RBF && hlc.norm == NORM_TANH_FAST) KAN_LOOP_GO(NORM_TANH_FAST, BASIS_RBF);
+    else KAN_LOOP_GO(NORM_RUNTIME, -1);
+#undef KAN_LOOP_GO
+#undef KAN_LOOP_WAVE
+    return hipGetLastError();
 }
 
 // The table VJP covers the recurrence configurations the Fisher-KPP drivers use.

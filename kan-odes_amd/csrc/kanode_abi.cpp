@@ -70,6 +70,9 @@ struct kanode_handle {
     bool pair_persist_abort = false;  // KANODE_OPT_PAIR_PERSIST_ABORT (tests: raise the abort word at launch)
     int last_adjoint = KANODE_ADJ_NONE;   // KANODE_OPT_LAST_ADJOINT (read-only)
     bool chain_wide = true;           // KANODE_OPT_CHAIN_WIDE
+    bool record_adj_steps = false;    // KANODE_OPT_RECORD_ADJOINT_STEPS
+    bool fk_loop = true;              // KANODE_OPT_FK_DEVICE_LOOP
+    std::vector<double> adj_steps;    // the last kanode_adjoint_tsit5's accepted step sizes (when recorded)
     bool adj_fused_finish = false;    // KANODE_OPT_ADJ_FUSED_FINISH (measured even with the finish launch)
     unsigned* fin_ctr = nullptr;      // its two arrival counters (device, zeroed at allocation)
     // the surrogate pair's deferred adjoint stage: its second launch, held until the next stage is issued
@@ -1095,6 +1098,8 @@ kanode_status kanode_set_option(kanode_handle* h, int32_t option, int64_t value)
     case KANODE_OPT_PAIR_PERSIST_ABORT: return flag(h->pair_persist_abort, "PAIR_PERSIST_ABORT");
     case KANODE_OPT_LAST_ADJOINT: return fail(h, KANODE_ERR_INVALID_ARG, "LAST_ADJOINT is read-only");
     case KANODE_OPT_CHAIN_WIDE: return flag(h->chain_wide, "CHAIN_WIDE");
+    case KANODE_OPT_RECORD_ADJOINT_STEPS: return flag(h->record_adj_steps, "RECORD_ADJOINT_STEPS");
+    case KANODE_OPT_FK_DEVICE_LOOP: return flag(h->fk_loop, "FK_DEVICE_LOOP");
     }
     return fail(h, KANODE_ERR_INVALID_ARG, "unknown option " + std::to_string(option));
 }
@@ -1119,6 +1124,8 @@ int64_t kanode_get_option(const kanode_handle* h, int32_t option) {
     case KANODE_OPT_PAIR_PERSIST_ABORT: return h->pair_persist_abort ? 1 : 0;
     case KANODE_OPT_LAST_ADJOINT: return h->last_adjoint;
     case KANODE_OPT_CHAIN_WIDE: return h->chain_wide ? 1 : 0;
+    case KANODE_OPT_RECORD_ADJOINT_STEPS: return h->record_adj_steps ? 1 : 0;
+    case KANODE_OPT_FK_DEVICE_LOOP: return h->fk_loop ? 1 : 0;
     }
     return -1;
 }
@@ -1381,6 +1388,20 @@ bool kanode_internal_fk_step_ok(const kanode_handle* h) {
     return h->spec.dtype == KANODE_F64 && h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->pp_on &&
            kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) && h->fused_step;
 }
+bool kanode_internal_fk_loop_ok(const kanode_handle* h) { return h->fk_loop && kanode_internal_fk_step_ok(h); }
+kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t batch,
+                                           void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    if (table_build(h, h->built_phi)) {
+        const int fn_phi = kan::PP_PHI;
+        HIP_TRY(h, kan::launch_fk_pp_build(h->hpc, h->dlc, h->dpc, (const double*)p, h->dtable, &fn_phi, 1, st));
+    }
+    const double dx2 = h->spec.dx * h->spec.dx;
+    const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+    HIP_TRY(h, kan::launch_fk_step_pp_loop(h->hpc, h->hlc[0], h->dlc, cd, co, (int)h->spec.nx, (const double*)p,
+                                           h->dtable, *la, batch, kSlabBlocks, st, h->grid_ovr.rhs));
+    return KANODE_OK;
+}
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
@@ -1604,6 +1625,17 @@ kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int6
     return KANODE_OK;
 }
 void kanode_internal_set_last_adjoint(kanode_handle* h, int path) { h->last_adjoint = path; }
+
+std::vector<double>* kanode_internal_adjoint_steps(kanode_handle* h) {
+    return h->record_adj_steps ? &h->adj_steps : nullptr;
+}
+
+extern "C" int64_t kanode_adjoint_step_sizes(const kanode_handle* h, double* out, int64_t cap) {
+    if (!h) return -1;
+    const int64_t n = (int64_t)h->adj_steps.size();
+    if (out && cap > 0) std::memcpy(out, h->adj_steps.data(), (size_t)std::min(n, cap) * sizeof(double));
+    return n;
+}
 int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch) {
     return kan::pair_adjoint_workgroups(h->hlc, batch, h->pair_persist_s);
 }

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
@@ -15,6 +16,7 @@ struct ChainSolveArgs;
 struct ChainAdjointArgs;
 struct AdjStepArgs;
 struct PairAdjArgs;
+struct FkLoopArgs;
 }
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -51,6 +53,11 @@ kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const
 // false when the handle is not that path (the caller runs the six stages)
 // (q4x7: write the dense output as the interpolation polynomials Q_1..Q_4 and k_7)
 bool kanode_internal_fk_step_ok(const kanode_handle* h);
+// the device-controlled adaptive Fisher-KPP solve (KANODE_OPT_FK_DEVICE_LOOP): whether the handle takes it,
+// and one step attempt (builds the table first when the solve has not)
+bool kanode_internal_fk_loop_ok(const kanode_handle* h);
+kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t batch,
+                                           void* stream);
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,
@@ -104,6 +111,8 @@ int64_t kanode_internal_param_length(const kanode_handle* h);
 int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch);
 // KANODE_OPT_LAST_ADJOINT: record the path kanode_adjoint_tsit5 took (a kanode_adjoint_path value)
 void kanode_internal_set_last_adjoint(kanode_handle* h, int path);
+// KANODE_OPT_RECORD_ADJOINT_STEPS: the handle's record of the accepted adjoint step sizes, or null when off
+std::vector<double>* kanode_internal_adjoint_steps(kanode_handle* h);
 kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int64_t batch, kan::PairAdjArgs* a,
                                            void* stream, bool& launched);
 // kanode_rhs_stage with the stage coefficients (c, ec) multiplied by *cscale (device) in the kernels;

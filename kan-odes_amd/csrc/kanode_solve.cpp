@@ -135,6 +135,22 @@ struct kanode_solution {
     // the persistent pair adjoint's device buffer: [arrival counter, abort word][slot table | ts | dts][exchange slots]
     void* padj = nullptr;
     size_t padj_bytes = 0;
+    double* hs_dev = nullptr;        // KANODE_OPT_RECORD_ADJOINT_STEPS: the one-launch adjoints' step sizes
+    int64_t hs_cap = 0;
+    // the device-controlled Fisher-KPP solve (solve_fk_loop): its state and host mirror, the error partials,
+    // the device copy of the slot table (staged through pinned memory) and the step records
+    struct Loop {
+        kan::FkLoopCtl* ctl = nullptr;
+        kan::FkLoopCtl* hmir = nullptr;    // pinned, mapped
+        kan::FkLoopCtl* dmir = nullptr;    // its device address
+        kan::StepCoef* coef = nullptr;     // [2]
+        double* parts = nullptr;
+        unsigned* arrive = nullptr;
+        void** dslots = nullptr;
+        void** hslots = nullptr;           // pinned
+        double* ts = nullptr;              // [cap] then dts [cap]
+        int64_t cap = 0, synced = 0;
+    } loop;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -175,6 +191,12 @@ struct kanode_solution {
         if (hparts) (void)hipHostFree(hparts);
         if (adj) (void)hipFree(adj);
         if (padj) (void)hipFree(padj);
+        if (hs_dev) (void)hipFree(hs_dev);
+        for (void* q : {(void*)loop.ctl, (void*)loop.coef, (void*)loop.parts, (void*)loop.arrive, (void*)loop.dslots,
+                        (void*)loop.ts})
+            if (q) (void)hipFree(q);
+        for (void* q : {(void*)loop.hmir, (void*)loop.hslots})
+            if (q) (void)hipHostFree(q);
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
         if (g.cap_stream) (void)hipStreamDestroy(g.cap_stream);
         for (void* p : {(void*)g.bufs, (void*)g.ctl, (void*)g.saveat, g.save, (void*)g.slots, (void*)g.ts, (void*)g.dts})
@@ -196,6 +218,13 @@ struct kanode_solution {
 
 extern "C" void kanode_solution_free(kanode_solution* s) { delete s; }
 extern "C" int64_t kanode_solution_steps(const kanode_solution* s) { return s ? (int64_t)s->ts.size() : -1; }
+extern "C" int64_t kanode_solution_step_sizes(const kanode_solution* s, double* ts, double* dts, int64_t cap) {
+    if (!s) return -1;
+    const int64_t n = (int64_t)s->ts.size(), m = std::max<int64_t>(0, std::min(n, cap));
+    if (ts && m) std::memcpy(ts, s->ts.data(), (size_t)m * sizeof(double));
+    if (dts && m) std::memcpy(dts, s->dts.data(), (size_t)m * sizeof(double));
+    return n;
+}
 
 namespace {
 
@@ -380,6 +409,50 @@ kanode_status initdt(kanode_handle* h, kanode_solution* s, const void* p, const 
     return KANODE_OK;
 }
 
+// The saveat values inside step `step` (t, t + dt] from its dense output: one launch for all of them (the same
+// arithmetic as one stage_lincomb / copy each; kan::SaveatStep).  ks: the step's k_1..k_7 (K form).
+template <typename T>
+kanode_status saveat_in_step(kanode_handle* h, kanode_solution* s, int64_t step, double t, double dt,
+                             void* const* ks, const double* saveat, int64_t n_save, int64_t& si, void* u_save,
+                             hipStream_t st) {
+    const size_t sb = s->state_bytes();
+    const double tn = t + dt;
+    kan::SaveatStep<T> sv{};
+    sv.u = (const T*)s->u(step);
+    sv.u_new = (const T*)s->u(step + 1);
+    sv.nk = s->qform ? 4 : 7;
+    for (int j = 0; j < sv.nk; ++j) sv.k[j] = (const T*)(s->qform ? s->q(step, j + 1) : ks[j]);
+    auto flush_sv = [&]() -> kanode_status {
+        if (sv.nsv == 0) return KANODE_OK;
+        SOLVE_HIP(h, kan::launch_saveat_step<T>(sv, s->n, st));
+        sv.nsv = 0;
+        sv.exact = 0;
+        return KANODE_OK;
+    };
+    while (si < n_save && saveat[si] <= tn + 1e-12 * std::max(1.0, std::fabs(tn))) {
+        const double tsv = saveat[si];
+        if (sv.nsv == 0) sv.dst = (T*)((char*)u_save + si * sb);
+        const int jv = sv.nsv;
+        if (std::fabs(tsv - tn) <= 1e-12 * std::max(1.0, std::fabs(tn))) {
+            sv.exact |= 1ull << jv;
+        } else if (s->qform) {
+            const double th = (tsv - t) / dt;
+            sv.w[jv][0] = th;
+            sv.w[jv][1] = th * th;
+            sv.w[jv][2] = th * th * th;
+            sv.w[jv][3] = th * th * th * th;
+        } else {
+            double w[7];
+            interp_weights((tsv - t) / dt, w);
+            for (int j = 0; j < 7; ++j) sv.w[jv][j] = w[j] * dt;
+        }
+        ++sv.nsv;
+        ++si;
+        if (sv.nsv == kan::kSaveatPerLaunch) SOLVE_TRY(flush_sv());
+    }
+    return flush_sv();
+}
+
 template <typename T>
 kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0, double tf, const double* saveat,
                       int64_t n_save, void* u_save, const kanode_solver_options& o, kanode_solution* s,
@@ -488,42 +561,7 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
             qold = std::max(EEst, o.qoldinit);
         }
         const double tn = t + dt;
-        // the saveat values in this step: one launch for all of them (the same arithmetic as one
-        // stage_lincomb / copy each; kan::SaveatStep)
-        kan::SaveatStep<T> sv{};
-        sv.u = (const T*)s->u(step);
-        sv.u_new = (const T*)s->u(step + 1);
-        sv.nk = s->qform ? 4 : 7;
-        for (int j = 0; j < sv.nk; ++j) sv.k[j] = (const T*)(s->qform ? s->q(step, j + 1) : ks[j]);
-        auto flush_sv = [&]() -> kanode_status {
-            if (sv.nsv == 0) return KANODE_OK;
-            SOLVE_HIP(h, kan::launch_saveat_step<T>(sv, s->n, st));
-            sv.nsv = 0;
-            sv.exact = 0;
-            return KANODE_OK;
-        };
-        while (si < n_save && saveat[si] <= tn + 1e-12 * std::max(1.0, std::fabs(tn))) {
-            const double tsv = saveat[si];
-            if (sv.nsv == 0) sv.dst = (T*)((char*)u_save + si * sb);
-            const int jv = sv.nsv;
-            if (std::fabs(tsv - tn) <= 1e-12 * std::max(1.0, std::fabs(tn))) {
-                sv.exact |= 1ull << jv;
-            } else if (s->qform) {
-                const double th = (tsv - t) / dt;
-                sv.w[jv][0] = th;
-                sv.w[jv][1] = th * th;
-                sv.w[jv][2] = th * th * th;
-                sv.w[jv][3] = th * th * th * th;
-            } else {
-                double w[7];
-                interp_weights((tsv - t) / dt, w);
-                for (int j = 0; j < 7; ++j) sv.w[jv][j] = w[j] * dt;
-            }
-            ++sv.nsv;
-            ++si;
-            if (sv.nsv == kan::kSaveatPerLaunch) SOLVE_TRY(flush_sv());
-        }
-        SOLVE_TRY(flush_sv());
+        SOLVE_TRY(saveat_in_step<T>(h, s, step, t, dt, ks, saveat, n_save, si, u_save, st));
         s->ts.push_back(t);
         s->dts.push_back(dt);
         t = tn;
@@ -885,6 +923,145 @@ kanode_status solve_graph_t(kanode_handle* h, const void* p, const void* u0, dou
     return KANODE_OK;
 }
 
+// ---- the adaptive Fisher-KPP solve with the step control on the device ------------------------------
+// KANODE_OPT_FK_DEVICE_LOOP, control = auto, fp64 table path, dense output kept: solve_t's algorithm with every
+// step one launch of the step kernel's DEV instantiation (kan::FkLoopArgs): the launch reads the step size from
+// device memory and its last workgroup runs the controller, so the host queues launches ahead, kKeep batches
+// of kBatch, and only polls the mapped mirror of the state; the queue drains (launches return at once) after
+// the last step.  The saveat values come from the dense output afterwards (saveat_in_step, as solve_t).
+// done = false when not covered (solve_t runs instead).
+kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, double t0, double tf,
+                            const double* saveat, int64_t n_save, void* u_save, const kanode_solver_options& o,
+                            kanode_solution* s, kanode_solve_stats* stats, hipStream_t st, bool& done) {
+    done = false;
+    if (o.control != 0 || !o.adaptive || !s->record || s->dtype != KANODE_F64 || capturing(st) ||
+        !kanode_internal_fk_loop_ok(h) || t0 >= tf - 1e-14 * std::max(1.0, std::fabs(tf)))
+        return KANODE_OK;
+    constexpr int64_t kBatch = 16;
+    const size_t sb = s->state_bytes();
+    auto& L = s->loop;
+    const int64_t cap = std::min<int64_t>(o.maxiters, (int64_t)1 << 22) + 2 * kBatch + 2;
+    if (L.cap < cap) {
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        for (void* q : {(void*)L.dslots, (void*)L.ts})
+            if (q) (void)hipFree(q);
+        if (L.hslots) (void)hipHostFree(L.hslots);
+        L.dslots = nullptr;
+        L.ts = nullptr;
+        L.hslots = nullptr;
+        L.cap = 0;
+        SOLVE_TRY(dev_alloc(h, (void**)&L.dslots, cap * sizeof(void*), "slot table"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.ts, 2 * cap * sizeof(double), "step records"));
+        SOLVE_HIP(h, hipHostMalloc((void**)&L.hslots, cap * sizeof(void*)));
+        L.cap = cap;
+    }
+    if (!L.ctl) {
+        SOLVE_TRY(dev_alloc(h, (void**)&L.ctl, sizeof(kan::FkLoopCtl), "loop state"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.coef, 2 * sizeof(kan::StepCoef), "loop coefficients"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.parts, kanode_internal_max_parts() * sizeof(double), "loop partials"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.arrive, 64, "loop counter"));
+        SOLVE_HIP(h, hipHostMalloc((void**)&L.hmir, sizeof(kan::FkLoopCtl), hipHostMallocMapped | hipHostMallocCoherent));
+        SOLVE_HIP(h, hipHostGetDevicePointer((void**)&L.dmir, L.hmir, 0));
+    }
+    L.synced = 0;
+    int64_t si = 0;
+    while (si < n_save && saveat[si] <= t0 + 1e-14 * std::max(1.0, std::fabs(t0))) {
+        SOLVE_HIP(h, hipMemcpyAsync((char*)u_save + si * sb, u0, sb, hipMemcpyDeviceToDevice, st));
+        ++si;
+    }
+    SOLVE_TRY(ensure_slots(h, s, 2, st));
+    s->qform = true;
+    SOLVE_HIP(h, hipMemcpyAsync(s->u(0), u0, sb, hipMemcpyDeviceToDevice, st));
+    kanode_stage s0{};
+    SOLVE_TRY(kanode_rhs_stage(h, p, s->u(0), &s0, s->k1_0, s->batch, st));   // k1 = f(u0)
+    double dt = o.dt;
+    if (!(o.dt > 0)) SOLVE_TRY(initdt<double>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st, s->q(0, 1)));
+    SOLVE_HIP(h, hipStreamSynchronize(st));   // (the mirror is the init copy's source and the device's target)
+    kan::FkLoopCtl c0{};
+    c0.t = t0;
+    c0.dt = std::min(dt, tf - t0);
+    c0.qold = o.qoldinit;
+    *L.hmir = c0;
+    SOLVE_HIP(h, hipMemcpyAsync(L.ctl, L.hmir, sizeof(c0), hipMemcpyHostToDevice, st));
+    kan::StepCoef k0{};   // the first attempt's coefficients (fk_loop_coef's products, formed here)
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j <= i; ++j) k0.a[i][j] = c0.dt * TA[i][j];
+    for (int j = 0; j < 7; ++j) k0.e[j] = c0.dt * BT[j];
+    for (int m = 0; m < 4; ++m)
+        for (int i = 0; i < 7; ++i) k0.q[m][i] = c0.dt * RI[i][m];
+    SOLVE_HIP(h, hipMemcpy(L.coef, &k0, sizeof(k0), hipMemcpyHostToDevice));
+    SOLVE_HIP(h, hipMemsetAsync(L.arrive, 0, sizeof(unsigned), st));
+    kan::FkLoopArgs la{};
+    la.ctl = L.ctl;
+    la.mirror = L.dmir;
+    la.coef = L.coef;
+    la.slots = L.dslots;
+    la.k1_0 = (const double*)s->k1_0;
+    la.ts = L.ts;
+    la.dts = L.ts + L.cap;
+    la.parts = L.parts;
+    la.arrive = L.arrive;
+    la.n = s->n;
+    la.tf = tf;
+    la.abstol = o.abstol;
+    la.reltol = o.reltol;
+    la.dtmin = o.dtmin;
+    la.beta1 = o.beta1;
+    la.beta2 = o.beta2;
+    la.gamma = o.gamma;
+    la.qmin = o.qmin;
+    la.qmax = o.qmax;
+    la.qoldinit = o.qoldinit;
+    la.maxiters = o.maxiters;
+    const volatile kan::FkLoopCtl* mir = L.hmir;
+    int64_t queued = 0;
+    for (;;) {
+        if (queued + kBatch + 2 > L.cap)
+            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device loop): step table full");
+        // slots for every step the queued launches can take (each launch advances at most one step)
+        SOLVE_TRY(ensure_slots(h, s, queued + kBatch + 2, st));
+        const int64_t ns = (int64_t)s->slots.size();
+        if (L.synced < ns) {
+            std::memcpy(L.hslots + L.synced, s->slots.data() + L.synced, (ns - L.synced) * sizeof(void*));
+            SOLVE_HIP(h, hipMemcpyAsync(L.dslots + L.synced, L.hslots + L.synced, (ns - L.synced) * sizeof(void*),
+                                        hipMemcpyHostToDevice, st));
+            L.synced = ns;
+        }
+        for (int64_t i = 0; i < kBatch; ++i) SOLVE_TRY(kanode_internal_fk_step_loop(h, p, &la, s->batch, st));
+        queued += kBatch;
+        // keep one batch queued behind the running one: wait until the device has taken the previous batch
+        for (uint64_t it = 1; mir->status == 0 && mir->it < queued - kBatch; ++it) {
+            if ((it & 255) == 0) {
+                const hipError_t q = hipStreamQuery(st);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) SOLVE_HIP(h, q);
+            }
+            __builtin_ia32_pause();
+        }
+        if (mir->status != 0) break;
+        if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it < queued - kBatch)
+            return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5 (device loop): the stream drained without progress");
+    }
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    const kan::FkLoopCtl c = *(const kan::FkLoopCtl*)L.hmir;
+    if (c.status == 2) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
+    s->ts.resize(c.step);
+    s->dts.resize(c.step);
+    if (c.step > 0) {
+        SOLVE_HIP(h, hipMemcpy(s->ts.data(), L.ts, c.step * sizeof(double), hipMemcpyDeviceToHost));
+        SOLVE_HIP(h, hipMemcpy(s->dts.data(), L.ts + L.cap, c.step * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    for (int64_t i = 0; i < c.step && si < n_save; ++i)
+        SOLVE_TRY(saveat_in_step<double>(h, s, i, s->ts[i], s->dts[i], nullptr, saveat, n_save, si, u_save, st));
+    if (stats) {
+        stats->naccept = c.step;
+        stats->nreject = c.nreject;
+        stats->nf = 6 * c.it + 1;
+    }
+    done = true;
+    return KANODE_OK;
+}
+
 // ---- InterpolatingAdjoint -----------------------------------------------------------
 template <typename T>
 kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, const void* dl_du, void* du0, void* dp,
@@ -1027,6 +1204,8 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     double qold = o.qoldinit, tau = 0.0;
     size_t si = 0;
     int64_t naccept = 0, nreject = 0, it = 0;
+    std::vector<double>* hrec = kanode_internal_adjoint_steps(h);
+    if (hrec) hrec->clear();
     for (; it < o.maxiters; ++it) {
         if (tau >= TT - 1e-14 * std::max(1.0, TT)) break;
         hstep = std::min(hstep, stops[si] - tau);
@@ -1153,6 +1332,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         mcur ^= 1;
         std::swap(kl[0], kl[6]);   // FSAL
         std::swap(km[0], km[6]);
+        if (hrec) hrec->push_back(hstep);
         ++naccept;
         if (std::fabs(tau - stops[si]) <= 1e-12 * std::max(1.0, TT)) {
             tau = stops[si];
@@ -1287,6 +1467,27 @@ kanode_status one_launch_adj_args(kanode_handle* h, kanode_solution* s, const vo
     a.du0 = du0;
     a.dp = dp;
     a.out = f.out;
+    if (kanode_internal_adjoint_steps(h)) {
+        const int64_t cap = 4 * (int64_t)s->ts.size() + 1024;
+        if (s->hs_cap < cap) {
+            if (s->hs_dev) SOLVE_HIP(h, hipFree(s->hs_dev));
+            s->hs_dev = nullptr;
+            s->hs_cap = 0;
+            SOLVE_HIP(h, hipMalloc((void**)&s->hs_dev, (size_t)cap * sizeof(double)));
+            s->hs_cap = cap;
+        }
+        a.hs = s->hs_dev;
+        a.hs_cap = s->hs_cap;
+    }
+    return KANODE_OK;
+}
+
+// the step sizes a one-launch adjoint wrote (a.hs) into the handle's record
+kanode_status fetch_adjoint_steps(kanode_handle* h, const kan::ChainAdjointArgs& a, int64_t naccept) {
+    std::vector<double>* rec = kanode_internal_adjoint_steps(h);
+    if (!rec || !a.hs) return KANODE_OK;
+    rec->resize((size_t)std::min(naccept, a.hs_cap));
+    if (!rec->empty()) SOLVE_HIP(h, hipMemcpy(rec->data(), a.hs, rec->size() * sizeof(double), hipMemcpyDeviceToHost));
     return KANODE_OK;
 }
 
@@ -1323,6 +1524,7 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
         stats->nreject = res[1];
         stats->nf = res[2];
     }
+    SOLVE_TRY(fetch_adjoint_steps(h, a, res[0]));
     done = true;
     return KANODE_OK;
 }
@@ -1390,6 +1592,7 @@ kanode_status adjoint_pair_t(kanode_handle* h, const void* p, kanode_solution* s
         stats->nreject = res[1];
         stats->nf = res[2];
     }
+    SOLVE_TRY(fetch_adjoint_steps(h, pa.c, res[0]));
     done = true;
     return KANODE_OK;
 }
@@ -1490,6 +1693,8 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
                 r = dtype == KANODE_F64
                         ? solve_fused_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st, done)
                         : solve_fused_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st, done);
+            if (r == KANODE_OK && !done)   // auto: the adaptive Fisher-KPP table path with the control on the device
+                r = solve_fk_loop(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st, done);
             if (r == KANODE_OK && !done)
                 r = dtype == KANODE_F64 ? solve_t<double>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st)
                                         : solve_t<float>(h, p, u0, t0, tf, saveat, n_save, u_save, o, s, stats, st);
@@ -1521,6 +1726,7 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
     TableHold hold(h);
     bool done = false;
     kanode_internal_set_last_adjoint(h, KANODE_ADJ_NONE);
+    if (std::vector<double>* rec = kanode_internal_adjoint_steps(h)) rec->clear();
     kanode_status r = s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
                                              : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done);
     if (r == KANODE_OK && done) kanode_internal_set_last_adjoint(h, KANODE_ADJ_CHAIN_WG);

@@ -97,6 +97,8 @@ OPT_PAIR_PERSIST_MAX_WG = 14
 OPT_PAIR_PERSIST_ABORT = 15
 OPT_LAST_ADJOINT = 16      # read-only: a kanode_adjoint_path value
 OPT_CHAIN_WIDE = 17
+OPT_RECORD_ADJOINT_STEPS = 18
+OPT_FK_DEVICE_LOOP = 19
 ADJ_NONE, ADJ_HOST_LOOP, ADJ_CHAIN_WG, ADJ_PAIR_PERSIST, ADJ_PAIR_FALLBACK = 0, 1, 2, 3, 4   # kanode_adjoint_path
 OPTIONS = {"pointwise_table": OPT_POINTWISE_TABLE, "fused_step": OPT_FUSED_STEP, "fused_solve": OPT_FUSED_SOLVE,
            "fused_solve_cap": OPT_FUSED_SOLVE_CAP, "grid_rhs": OPT_GRID_RHS, "grid_vjp": OPT_GRID_VJP,
@@ -104,7 +106,8 @@ OPTIONS = {"pointwise_table": OPT_POINTWISE_TABLE, "fused_step": OPT_FUSED_STEP,
            "pair_fuse": OPT_PAIR_FUSE, "pair_persist": OPT_PAIR_PERSIST, "pair_persist_s": OPT_PAIR_PERSIST_S,
            "adj_fused_finish": OPT_ADJ_FUSED_FINISH, "pair_persist_max_wg": OPT_PAIR_PERSIST_MAX_WG,
            "pair_persist_abort": OPT_PAIR_PERSIST_ABORT, "last_adjoint": OPT_LAST_ADJOINT,
-           "chain_wide": OPT_CHAIN_WIDE}
+           "chain_wide": OPT_CHAIN_WIDE, "record_adjoint_steps": OPT_RECORD_ADJOINT_STEPS,
+           "fk_device_loop": OPT_FK_DEVICE_LOOP}
 
 SIGNATURES = [
     ("kanode_create", C.c_int, [C.POINTER(SpecC), C.POINTER(C.c_void_p)]),
@@ -126,9 +129,11 @@ SIGNATURES = [
     ("kanode_solver_options_default", None, [C.POINTER(SolverOptsC)]),
     ("kanode_solution_free", None, [_P]),
     ("kanode_solution_steps", C.c_int64, [_P]),
+    ("kanode_solution_step_sizes", C.c_int64, [_P, _P, _P, C.c_int64]),
     ("kanode_solve_tsit5", C.c_int, [_H, _P, _P, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_double), C.c_int64,
                                      _P, C.POINTER(SolverOptsC), C.POINTER(C.c_void_p), C.POINTER(SolveStatsC), _P]),
     ("kanode_adjoint_tsit5", C.c_int, [_H, _P, _P, _P, _P, _P, C.POINTER(SolverOptsC), C.POINTER(SolveStatsC), _P]),
+    ("kanode_adjoint_step_sizes", C.c_int64, [_H, _P, C.c_int64]),
     ("kanode_rhs_host", C.c_int, [_H, _P, _P, _P, C.c_int64]),
     ("kanode_vjp_host", C.c_int, [_H, _P, _P, _P, _P, _P, C.c_int64]),
     ("kanode_layer_forward", C.c_int, [_H, C.c_int32, _P, _P, _P, C.c_int64, _P]),

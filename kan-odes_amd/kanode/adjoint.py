@@ -110,6 +110,7 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
     tau = 0.0
     si = 0
     naccept = nreject = 0
+    hs = []
     for _ in range(opt.maxiters):
         if tau >= T - 1e-14 * max(1.0, T):
             break
@@ -157,6 +158,7 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
         tau = tau + h
         lam, mu = lam_new, mu_new
         k1l, k1m = kl[6], km[6]
+        hs.append(h)
         naccept += 1
         if abs(tau - stops[si]) <= 1e-12 * max(1.0, T):
             tau = stops[si]
@@ -173,7 +175,7 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
     for ts in list(jumps):                                   # a saveat at t0 adds to dL/du0 only
         if abs(ts - t0) <= eps:
             lam = lam + jumps.pop(ts)
-    return lam, mu, dict(naccept=naccept, nreject=nreject, nf=nf)
+    return lam, mu, dict(naccept=naccept, nreject=nreject, nf=nf, dts=hs)
 
 
 class _InterpAdjointSolve(torch.autograd.Function):
@@ -188,6 +190,7 @@ class _InterpAdjointSolve(torch.autograd.Function):
         ctx.f, ctx.rec, ctx.tspan, ctx.saveat, ctx.opt, ctx.stats = f, rec, tspan, sol.t, opt, stats
         ctx.save_for_backward(p)
         stats.update(sol.stats)
+        stats["dts"] = [float(x) for x in rec.dt]
         return sol.u
 
     @staticmethod
@@ -219,12 +222,15 @@ class _NativeAdjointSolve(torch.autograd.Function):
         ctx.hd, ctx.dense, ctx.oc, ctx.stats, ctx.u_shape = hd, dense, oc, stats, tuple(u0.shape)
         ctx.save_for_backward(p)
         stats.update(st)
+        stats["dts"] = dense.step_sizes()[1].tolist()   # accepted step sizes (the solve's host copy)
         return u_save
 
     @staticmethod
     def backward(ctx, g):
         (p,) = ctx.saved_tensors
         du0, dp, st = ctx.hd.adjoint_tsit5(p.detach().contiguous(), ctx.dense, g.contiguous(), ctx.oc, ctx.u_shape)
+        if ctx.hd.get_option("record_adjoint_steps"):
+            st["dts"] = ctx.hd.adjoint_step_sizes().tolist()
         ctx.stats["adjoint"] = st
         ctx.hd.release_dense(ctx.dense)
         ctx.dense = None

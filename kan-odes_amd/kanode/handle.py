@@ -69,6 +69,14 @@ class DenseOutput:
     def steps(self) -> int:
         return int(L.lib().kanode_solution_steps(self.ptr)) if self.ptr.value else 0
 
+    def step_sizes(self):
+        """(t_n, dt_n) of the accepted steps, float64 numpy arrays (kanode_solution_step_sizes)."""
+        n = self.steps
+        ts, dts = np.zeros(n), np.zeros(n)
+        if n:
+            L.lib().kanode_solution_step_sizes(self.ptr, ts.ctypes.data, dts.ctypes.data, n)
+        return ts, dts
+
     def __del__(self):
         if getattr(self, "ptr", None) is not None and self.ptr.value:
             try:
@@ -329,6 +337,14 @@ class KanodeHandle:
                                              C.byref(opts), C.byref(st), _stream(self.device)),
                 self._h, "kanode_adjoint_tsit5")
         return du0, dp, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf)
+
+    def adjoint_step_sizes(self):
+        """The accepted step sizes of the last adjoint_tsit5 (option record_adjoint_steps; else empty)."""
+        n = int(L.lib().kanode_adjoint_step_sizes(self._h, None, 0))
+        hs = np.zeros(max(n, 0))
+        if n > 0:
+            L.lib().kanode_adjoint_step_sizes(self._h, hs.ctypes.data, n)
+        return hs
 
     def release_dense(self, dense: "DenseOutput") -> None:
         """Return a dense output's device storage for reuse by the next solve."""

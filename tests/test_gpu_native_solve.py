@@ -611,6 +611,39 @@ def test_adjoint_fused_finish_bitwise(nx, B):
     assert torch.equal(g2, g1) and torch.equal(gu2, gu1)
 
 
+@pytest.mark.parametrize("nx,B", [(256, 64), (128, 300), (512, 5)])
+def test_fk_device_loop_matches_host_loop(nx, B):
+    """KANODE_OPT_FK_DEVICE_LOOP (the default for an adaptive table-path solve that keeps its dense output):
+    every step launch reads its step size from device memory and the launch's last workgroup runs the PI
+    controller, the host queues 16-launch batches ahead and the saveat values come from the dense output
+    afterwards.  Against the host loop (FK_DEVICE_LOOP = 0, one norm read per step): the same step sequence
+    (the device's pow may round the last bit differently: step sizes to 1e-13), the solution, dense output
+    and gradients to 1e-12 of their scale; the saveat points fall inside steps, on step ends and at t0; the
+    solve ends mid-batch (the launches queued behind return at once); two solves on one handle (the arrival
+    counter is back at zero), and maxiters ends the device loop with the host loop's error."""
+    rhs = _fk_cfg(nx, 10, "softsign")
+    u0 = t(fk_u0(nx, B, 4))
+    p0 = t(np.random.default_rng(9).uniform(-1.0, 1.0, 11))
+    opt = kanode.Tsit5Options(abstol=1e-9, reltol=1e-8)
+    tspan, ts = (0.0, 0.4), [0.0, 0.1, 0.25, 0.3, 0.4]
+    assert rhs.hd.get_option("fk_device_loop") == 1
+    sd, gd, gud = _solve_grad(rhs, u0, p0, tspan, ts, opt)
+    sd2, gd2, gud2 = _solve_grad(rhs, u0, p0, tspan, ts, opt)
+    sh, gh, guh = _solve_grad(rhs, u0, p0, tspan, ts, opt, fk_device_loop=0)
+    assert torch.equal(sd.u, sd2.u) and torch.equal(gd, gd2) and torch.equal(gud, gud2)
+    assert sd.stats["naccept"] == sh.stats["naccept"] and sd.stats["nreject"] == sh.stats["nreject"]
+    assert sd.stats["nf"] == sh.stats["nf"] and sd.stats["naccept"] > 16
+    assert np.abs(np.divide(sd.stats["dts"], sh.stats["dts"]) - 1).max() <= 1e-13
+    for a_, b_ in ((sd.u, sh.u), (gd, gh), (gud, guh)):
+        assert (a_ - b_).abs().max().item() <= 1e-12 * b_.abs().max().item()
+    # the native forward alone (no gradient): the same values
+    with torch.no_grad():
+        nd = kanode.solve(rhs, u0, tspan, p0, ts, opt)
+    assert (nd.u - sh.u).abs().max().item() <= 1e-12 * sh.u.abs().max().item()
+    with pytest.raises(RuntimeError, match="maxiters"):
+        _solve_grad(rhs, u0, p0, tspan, ts, dataclasses.replace(opt, maxiters=5))
+
+
 def test_adjoint_step_rows_kernel_batch_cap():
     """Above 8192 rows (one row per wave: 4 rows x the 2048 slab blocks) the adjoint step falls back
     to the persistent-grid kernel: both settings of KANODE_OPT_ADJ_STEP_ROWS then run the same
@@ -718,13 +751,23 @@ def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, persist, 
     ~6·n_steps such evaluations times h, and dp = μ(t0) a sum of ~6·n_adjoint_steps stage VJPs times h, so
     both stay within n_evals·1e-13 of their scale over this short span (T·Lipschitz < 1, no growth), i.e.
     1e-13 × the evaluation count: 1.2e-11 for the solution (120 RHS) and 2.6e-11 for the gradients here.
-    Adaptive: equal accepted-step counts, and the same bars times 10^3 (the step sizes themselves move
-    with rounding-level differences in the embedded error, which the fixed-step runs exclude)."""
+    Adaptive: equal accepted-step counts, and the fixed-step bars plus the effect of the MEASURED step-size
+    perturbation: the controllers see the embedded error estimate, a difference of nearly
+    equal terms, so rounding moves each step by a relative δ (measured from both step sequences, forward and
+    adjoint: kanode_solution_step_sizes / KANODE_OPT_RECORD_ADJOINT_STEPS against the driver's own).  A step
+    scaled by 1+δ changes its local error, which the controller holds at ≈ tol = reltol + abstol/|u|, by
+    ≈ 5δ (Tsit5's local error is O(h⁵)), so the grids' difference moves the solution by at most
+    5·δ_f·n_steps·tol, and the gradients by 5·δ_a·n_adj·tol plus the forward term (the dense output they
+    read).  δ itself must stay small (≤ 1e-3): the stage values' 1e-13 differences enter the error estimate,
+    a difference that cancels down to ~tol, amplified by |h·k|/tol, and the PI controller's memory carries
+    them from step to step (measured up to 2.3e-5, the Schrödinger adjoint); a controller that diverged
+    while keeping the step count moves steps by percents."""
     from oracle_rhs import OracleChainRHS
     specs = [O.LayerSpec(N, 10, G, "softsign"), O.LayerSpec(10, N, G, "softsign")]
     chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
     rhs = kanode.ChainRHS(chain, device=device())
     rhs.hd.set_option("pair_persist", persist)   # 1: the one-launch adjoint where it fits (Burgers), else per stage
+    rhs.hd.set_option("record_adjoint_steps", 1)
     u0 = t(_surrogate_ics(name, N, B, 11))
     p0 = t(chain.setup(np.random.default_rng(0))[0].astype(np.float64))
     T = 0.05
@@ -740,13 +783,24 @@ def test_full_size_surrogate_adjoint_matches_cpu_oracle(name, N, G, B, persist, 
         res.append((sol.u.detach().cpu(), g.cpu(), gu.cpu(), sol.stats))
     (ug, gg, gug, sg), (uc, gc, guc, sc) = res
     assert sg["naccept"] == sc["naccept"] and sg["adjoint"]["naccept"] == sc["adjoint"]["naccept"]
-    amp = 1e3 if adaptive else 1.0
-    bar_u = amp * 1e-13 * sc["nf"]
-    bar_g = amp * 1e-13 * sc["adjoint"]["nf"]
+    assert len(sg["dts"]) == sg["naccept"] and len(sg["adjoint"]["dts"]) == sg["adjoint"]["naccept"]
+    d_f = float(np.max(np.abs(np.divide(sg["dts"], sc["dts"]) - 1.0)))
+    d_a = float(np.max(np.abs(np.divide(sg["adjoint"]["dts"], sc["adjoint"]["dts"]) - 1.0)))
+    bar_u = 1e-13 * sc["nf"]
+    bar_g = 1e-13 * sc["adjoint"]["nf"]
+    if adaptive:
+        assert d_f <= 1e-3 and d_a <= 1e-3, (d_f, d_a)
+        tol = opt.reltol + opt.abstol / uc.abs().max().item()
+        pert_u = 5 * d_f * sc["naccept"] * tol
+        bar_u += pert_u
+        bar_g += 5 * d_a * sc["adjoint"]["naccept"] * tol + pert_u
+    else:
+        assert d_f <= 1e-12 and d_a <= 1e-12, (d_f, d_a)
     eu = (ug - uc).abs().max().item() / uc.abs().max().item()
     eg = (gg - gc).abs().max().item() / gc.abs().max().item()
     egu = (gug - guc).abs().max().item() / guc.abs().max().item()
-    print(f"{name} adaptive={adaptive}: steps {sg['naccept']}/{sg['adjoint']['naccept']}, rel err u {eu:.2e} "
+    print(f"{name} adaptive={adaptive}: steps {sg['naccept']}/{sg['adjoint']['naccept']} (step perturbation "
+          f"{d_f:.1e} / {d_a:.1e}), rel err u {eu:.2e} "
           f"(bar {bar_u:.1e}), dp {eg:.2e}, du0 {egu:.2e} (bar {bar_g:.1e})")
     assert eu <= bar_u
     assert eg <= bar_g and egu <= bar_g
@@ -796,7 +850,8 @@ def test_persistent_pair_adjoint_falls_back(adaptive):
     PAIR_PERSIST_MAX_WG = 8 (a device with room for 8 resident workgroups: the launch is refused up front) and
     PAIR_PERSIST_ABORT = 1 (the abort word raised at launch, as a time-out raises it: the kernel drains and
     the host re-runs).  Both give the launch path's gradient bitwise, and the handle then still takes the
-    one-launch path when allowed."""
+    one-launch path when allowed.  KANODE_OPT_RECORD_ADJOINT_STEPS: every path records its accepted backward
+    steps (the one-launch kernel from the device), which tile the span and agree between the paths."""
     N, G, B = 512, 5, 4
     chain = kanode.Chain(kanode.KDense(N, 10, G, normalizer="softsign"), kanode.KDense(10, N, G, normalizer="softsign"))
     rhs = kanode.ChainRHS(chain, device=device())
@@ -814,20 +869,24 @@ def test_persistent_pair_adjoint_falls_back(adaptive):
             x0 = u0.detach().clone().requires_grad_(True)
             sol = kanode.solve(rhs, x0, (0.0, 0.05), p, ts, opt, sensealg="interpolating_adjoint")
             g, gu = torch.autograd.grad((sol.u * w).sum(), [p, x0])
-            return g, gu, rhs.hd.get_option("last_adjoint")
+            hs = np.asarray(sol.stats["adjoint"]["dts"])
+            assert len(hs) == sol.stats["adjoint"]["naccept"] and abs(hs.sum() - 0.05) <= 1e-12
+            return g, gu, rhs.hd.get_option("last_adjoint"), hs
 
-    g0, gu0, path0 = grad(pair_persist=0)
-    assert path0 == L.ADJ_HOST_LOOP
-    gc, guc, pathc = grad(pair_persist_max_wg=8)
-    assert pathc == L.ADJ_HOST_LOOP
-    ga, gua, patha = grad(pair_persist_abort=1)
-    assert patha == L.ADJ_PAIR_FALLBACK
-    for g, gu in ((gc, guc), (ga, gua)):
-        assert torch.equal(g, g0) and torch.equal(gu, gu0)
-    g1, gu1, path1 = grad()
-    assert path1 == L.ADJ_PAIR_PERSIST
+    with rhs.hd.options(record_adjoint_steps=1):
+        g0, gu0, path0, hs0 = grad(pair_persist=0)
+        assert path0 == L.ADJ_HOST_LOOP
+        gc, guc, pathc, hsc = grad(pair_persist_max_wg=8)
+        assert pathc == L.ADJ_HOST_LOOP
+        ga, gua, patha, hsa = grad(pair_persist_abort=1)
+        assert patha == L.ADJ_PAIR_FALLBACK
+        for g, gu, hs in ((gc, guc, hsc), (ga, gua, hsa)):
+            assert torch.equal(g, g0) and torch.equal(gu, gu0) and np.array_equal(hs, hs0)
+        g1, gu1, path1, hs1 = grad()
+        assert path1 == L.ADJ_PAIR_PERSIST
     bar = 1e-9 if adaptive else 1e-11
     assert (g1 - g0).abs().max().item() <= bar * g0.abs().max().item()
+    assert len(hs1) == len(hs0) and np.abs(hs1 / hs0 - 1).max() <= (1e-6 if adaptive else 1e-12)
 
 
 
@@ -881,7 +940,7 @@ def test_fk_small_one_workgroup_matches_host_loop(nx, B, G, norm, adaptive):
     w = t(np.random.default_rng(5).normal(size=(len(ts),) + tuple(u0.shape)))
     out = []
     for fused in (1, 0):
-        with rhs.hd.options(fused_solve=fused):
+        with rhs.hd.options(fused_solve=fused, record_adjoint_steps=1):
             p = p0.clone().requires_grad_(True)
             x0 = u0.clone().requires_grad_(True)
             sol = kanode.solve(rhs, x0, (0.0, 2.0), p, ts, opt, sensealg="interpolating_adjoint")
@@ -889,6 +948,9 @@ def test_fk_small_one_workgroup_matches_host_loop(nx, B, G, norm, adaptive):
             out.append((sol.u.detach(), g, gu, sol.stats, rhs.hd.get_option("last_adjoint")))
     (u1, g1, gu1, s1, path1), (u0_, g0, gu0, s0, path0) = out
     assert path1 == L.ADJ_CHAIN_WG and path0 == L.ADJ_HOST_LOOP
+    for st in (s1, s0):   # both record their backward steps (the one-workgroup kernel from the device)
+        hs = np.asarray(st["adjoint"]["dts"])
+        assert len(hs) == st["adjoint"]["naccept"] and abs(hs.sum() - 2.0) <= 1e-12
     scale = u0_.abs().max().item()
     if not adaptive:
         assert s1["naccept"] == s0["naccept"] and s1["adjoint"]["naccept"] == s0["adjoint"]["naccept"]
@@ -925,15 +987,18 @@ def test_lv1_wide_adjoint_matches_group_adjoint_and_oracle(adaptive):
         x0 = torch.as_tensor(u0, device=dev).requires_grad_(True)
         sol = kanode.solve(f, x0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
         g, gu = torch.autograd.grad((sol.u * torch.as_tensor(w, device=dev)).sum(), [p, x0])
-        return g.cpu(), gu.cpu(), sol.stats["adjoint"]["naccept"]
+        return g.cpu(), gu.cpu(), sol.stats["adjoint"]["naccept"], np.asarray(sol.stats["adjoint"]["dts"])
 
     rhs = lv()
-    gw, guw, nw = grad(rhs, device())
+    rhs.hd.set_option("record_adjoint_steps", 1)
+    gw, guw, nw, hw = grad(rhs, device())
     assert rhs.hd.get_option("last_adjoint") == L.ADJ_CHAIN_WG
     with rhs.hd.options(chain_wide=0):
-        gg, gug, ng = grad(rhs, device())
+        gg, gug, ng, hg = grad(rhs, device())
         assert rhs.hd.get_option("last_adjoint") == L.ADJ_CHAIN_WG
-    gc, guc, nc = grad(OracleChainRHS(specs), "cpu")
-    assert nw == ng == nc
+    gc, guc, nc, hc = grad(OracleChainRHS(specs), "cpu")
+    assert nw == ng == nc == len(hw) == len(hg) == len(hc)
+    for h_ in (hw, hg):   # the device-recorded backward steps against the driver's
+        assert np.abs(h_ / hc - 1).max() <= (1e-6 if adaptive else 1e-12)
     for a_, b_ in ((gw, gg), (gw, gc), (guw, gug), (guw, guc)):
         assert (a_ - b_).abs().max().item() <= 1e-10 * b_.abs().max().item()

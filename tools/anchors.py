@@ -138,7 +138,9 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
         with torch.no_grad():
             return float(kanode.mse_loss(kanode.solve(rhs, u0, pr["tspan"], p, pr["saveat"]).u, Xn))
 
+    fit_rho = pr["fitted"](pr["rho"])
     curve = [(0, post_loss(tr.p))]
+    dev_curve = [(0, float(np.max(np.abs(learned(tr.p) - fit_rho))))]   # max |kan1_(ρ) - recorded fit| per log point
     t0 = time.perf_counter()
     last = t0
     done = 0
@@ -147,6 +149,7 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
         done = i
         if i % log_every == 0 or i == iters:
             curve.append((i, post_loss(tr.p)))           # l[end] = loss(p) after update! (:204)
+            dev_curve.append((i, float(np.max(np.abs(learned(tr.p) - fit_rho)))))
             now = time.perf_counter()
             if now - last > 30 or i == iters:
                 _progress(f"{pr['name']}: iteration {i}/{iters} loss {curve[-1][1]:.4e} ({now - t0:.0f} s)")
@@ -171,6 +174,9 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
         "log_every": log_every,
         "loss_initial": curve[0][1], "loss_final": curve[-1][1], "loss_min": min(l for _, l in curve),
         "loss_curve": curve,
+        "dev_curve": dev_curve,
+        "first_iter_within_0.01": next((i for i, d in dev_curve if d <= 0.01), None),
+        "first_iter_within_0.005": next((i for i, d in dev_curve if d <= 0.005), None),
         "forward_steps": sol.stats["naccept"], "adjoint_steps": sol.stats["adjoint"]["naccept"],
         "rho": pr["rho"].tolist(), "learned_source": lr.tolist(),
         "recorded_fit": pr["fitted_text"], "recorded_fit_values": fit.tolist(),
@@ -245,7 +251,7 @@ def main() -> None:
     ap.add_argument("--max-seconds", type=float, default=0.0, help="stop at the first log point past this")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    path = os.path.join(a.out, f"{a.problem}.json")
+    path = os.path.join(a.out, f"{a.problem}_seed{a.seed}.json")
     if a.problem == "lv":
         o = run_lv(a.iters or None, a.seed, a.log_every, out_path=path)
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_train_final",
@@ -253,7 +259,8 @@ def main() -> None:
     else:
         o = run_source(a.problem, a.iters or None, a.seed, a.log_every, out_path=path, max_seconds=a.max_seconds)
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_final",
-                                            "max_abs_dev_from_recorded_fit", "max_abs_dev_from_true_source")}))
+                                            "max_abs_dev_from_recorded_fit", "max_abs_dev_from_true_source",
+                                            "first_iter_within_0.01", "first_iter_within_0.005")}))
 
 
 if __name__ == "__main__":
