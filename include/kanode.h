@@ -197,12 +197,15 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch);
  *     sizes of its backward integration on the handle (kanode_adjoint_step_sizes), on every path
  *     (the one-launch adjoints write them from the device, up to 4 x the forward steps + 1024).
  *     Diagnostics: two solvers' step sequences show whether their controllers took the same path.
- *   KANODE_OPT_FK_DEVICE_LOOP (default 1): an adaptive Fisher-KPP table-path solve that keeps its dense
- *     output (control = auto) runs its step control on the device: each step launch reads its step size
- *     and writes the next (its last workgroup runs the PI controller), the host queues launches ahead and
- *     never waits on a step; the saveat values are formed from the dense output afterwards.  0 = the host
- *     loop (one norm read per step).  Same controller arithmetic; the device's pow may differ from the
- *     host's in the last bit, so step sizes agree to rounding, not bitwise.
+ *   KANODE_OPT_FK_DEVICE_LOOP (default 1): the adaptive Fisher-KPP table path (control = auto, dense
+ *     output kept) runs its step control on the device.  Forward: launch q of the step kernel decides
+ *     attempt q - 1 at its head (every workgroup sums the same error partials and applies the PI
+ *     controller) and takes the next step; the saveat values are formed from the dense output afterwards.
+ *     Adjoint (the combined rows step, Nx = 128 / 256): the finish launch's last workgroup decides the
+ *     attempt and plans the next one; a step landing on a saveat stop pauses the loop for the host's jump.
+ *     The host queues launches ahead and never waits on a step.  0 = the host loops (one norm read per
+ *     step).  Same controller arithmetic; the device sums the terms in another order and its pow may round
+ *     differently, so step sizes agree to rounding, not bitwise.
  * Options are read when a call is issued (never from the environment).  kanode_get_option
  * returns the current value, or -1 for an unknown option. */
 typedef enum {

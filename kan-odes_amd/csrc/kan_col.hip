@@ -1292,6 +1292,160 @@ kd_chain_adjoint_wide_kernel(const LayerConst* __restrict__ lcs, const T* __rest
     onewg_adjoint<T>(m, a, mu, km, tsl, dtsl, red, recl);
 }
 
+// One trajectory of the Lotka-Volterra chain [2 -> 10 -> 2] (G = 5, base activations; LV_driver_KANODE.jl:
+// 139-143) on ONE wave: no barriers at all.  A lane evaluates one basis feature of a layer (the reference formula,
+// utils.jl:8-13, as WideModel): layer 1's 12 features of (x_0, x_1) on lanes 0..11, layer 2's 60 features of
+// (h_0..h_9) on lanes 0..59; every cross-lane value is a readlane (uniform) or a ds_bpermute.  Each lane keeps
+// the layer coefficients it multiplies in registers for the whole adjoint (C1 row r on lane r, C1 column c on
+// lane c, C2 column c on lane c).  kμ: the parameter cotangents go straight to km (one product each).
+template <typename T>
+__device__ __forceinline__ T lane_read(T v, int l) {   // v of lane l (l uniform)
+    if constexpr (sizeof(T) == 8) {
+        const long long x = __double_as_longlong((double)v);
+        const int lo = __builtin_amdgcn_readlane((int)x, l), hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+        return (T)__longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    } else {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+    }
+}
+struct LvWaveShape {
+    static constexpr int I = 2, H = 10, O = 2, G = 5, per = G + 1, F1 = I * per, F2 = H * per;
+};
+template <typename T, int NORM>
+struct LvWaveModel {
+    using S = LvWaveShape;
+    const Math<T>& M;
+    const LayerConst* lcl;   // [2] (LDS)
+    int P;
+    bool act;
+    int64_t idx, n;
+    int lane;
+    T c1r[S::F1];   // lane r < H: C1[r][c], c < F1 (feature c = input c / per, knot c % per)
+    T c1c[S::H];    // lane c < F1: C1[r][c], r < H
+    T c2c[S::O];    // lane c < F2: C2[o][c]
+
+    __device__ static int64_t q1(const LayerConst& L, int r, int c) {
+        const int i = c / S::per, g = c % S::per;
+        return g < S::G ? L.p_off + r + S::H * (g + S::G * i) : L.w_off + r + S::H * i;
+    }
+    __device__ static int64_t q2(const LayerConst& L, int o, int c) {
+        const int i = c / S::per, g = c % S::per;
+        return g < S::G ? L.p_off + o + S::O * (g + S::G * i) : L.w_off + o + S::O * i;
+    }
+    __device__ LvWaveModel(const Math<T>& M_, const LayerConst* lcl_, const T* ps, int P_)
+        : M(M_), lcl(lcl_), P(P_), act((int)threadIdx.x < S::I), idx(threadIdx.x), n(S::I), lane(threadIdx.x) {
+        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+#pragma unroll
+        for (int c = 0; c < S::F1; ++c) c1r[c] = lane < S::H ? ps[q1(L1, lane, c)] : T(0);
+#pragma unroll
+        for (int r = 0; r < S::H; ++r) c1c[r] = lane < S::F1 ? ps[q1(L1, r, lane)] : T(0);
+#pragma unroll
+        for (int o = 0; o < S::O; ++o) c2c[o] = lane < S::F2 ? ps[q2(L2, o, lane)] : T(0);
+    }
+    // layer 1: this lane's feature of (x_0, x_1) (lanes < F1) and h_r on lane r < H
+    __device__ T layer1(T y, T& f1, T& p1, T& d1) const {
+        const T x0 = lane_read(y, 0), x1 = lane_read(y, 1);
+        const int c = lane < S::F1 ? lane : 0;
+        wide_feature<T, NORM>(M, lcl[0], c % S::per, c / S::per == 0 ? x0 : x1, f1, p1, d1);
+        T h = T(0);
+#pragma unroll
+        for (int k = 0; k < S::F1; ++k) h = kfma<T>(c1r[k], lane_read(f1, k), h);
+        return h;
+    }
+    // layer 2: this lane's feature of h_{lane / per} (lanes < F2)
+    __device__ void layer2(T h, T& f2, T& p2, T& d2) const {
+        const int c = lane < S::F2 ? lane : 0;
+        const T hi = __shfl(h, c / S::per, kWave);
+        wide_feature<T, NORM>(M, lcl[1], c % S::per, hi, f2, p2, d2);
+        if (lane >= S::F2) f2 = T(0);
+    }
+    __device__ T rhs(T y) {
+        T f1, p1, d1, f2, p2, d2;
+        const T h = layer1(y, f1, p1, d1);
+        layer2(h, f2, p2, d2);
+        const T y0 = wave_sum(c2c[0] * f2), y1 = wave_sum(c2c[1] * f2);
+        return lane == 0 ? y0 : (lane == 1 ? y1 : T(0));
+    }
+    __device__ T vjp(T y, T ls, T* __restrict__ km) {
+        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+        T f1, p1, d1, f2, p2, d2;
+        const T h = layer1(y, f1, p1, d1);
+        layer2(h, f2, p2, d2);
+        // layer 2: dC2[o][c] = ȳ_o·f2_c, φ̄2_c = Σ_o C2[o][c]·ȳ_o, z̄ = rrule factor·φ̄2
+        const T yb0 = lane_read(ls, 0), yb1 = lane_read(ls, 1);
+        const int g2 = lane % S::per;
+        T z2 = T(0);
+        if (lane < S::F2) {
+            km[q2(L2, 0, lane)] = yb0 * f2;
+            km[q2(L2, 1, lane)] = yb1 * f2;
+            const T pb = c2c[0] * yb0 + c2c[1] * yb1;
+            z2 = g2 < S::G ? p2 * pb * (T)L2.invh : p2 * pb;
+        }
+        // h̄_r = N'(h_r)·Σ_g z̄_(r,g) + z̄_(r,swish) on lane r < H (the group's lanes per·r .. per·r + G)
+        const int r = lane < S::H ? lane : 0;
+        T sb = T(0);
+#pragma unroll
+        for (int g = 0; g < S::G; ++g) sb = sb + __shfl(z2, S::per * r + g, kWave);
+        const T zsw = __shfl(z2, S::per * r + S::G, kWave);
+        const T dn = __shfl(d2, S::per * r, kWave);
+        const T hb = lane < S::H ? dn * sb + zsw : T(0);
+        // layer 1: dC1[r][c] = h̄_r·f1_c, φ̄1_c = Σ_r C1[r][c]·h̄_r on lane c < F1
+        const int g1 = lane % S::per;
+        T pb1 = T(0);
+#pragma unroll
+        for (int rr = 0; rr < S::H; ++rr) {
+            const T hbr = lane_read(hb, rr);
+            if (lane < S::F1) km[q1(L1, rr, lane)] = hbr * f1;
+            pb1 = kfma<T>(c1c[rr], hbr, pb1);
+        }
+        const T z1 = lane < S::F1 ? (g1 < S::G ? p1 * pb1 * (T)L1.invh : p1 * pb1) : T(0);
+        // x̄_i = N'(x_i)·Σ_g z̄_(i,g) + z̄_(i,swish) on lane i < I
+        const int i = lane < S::I ? lane : 0;
+        T sx = T(0);
+#pragma unroll
+        for (int g = 0; g < S::G; ++g) sx = sx + __shfl(z1, S::per * i + g, kWave);
+        const T xsw = __shfl(z1, S::per * i + S::G, kWave);
+        const T dx = __shfl(d1, S::per * i, kWave);
+        __syncthreads();   // (one wave: km complete before the driver reads it)
+        return act ? dx * sx + xsw : T(0);
+    }
+};
+
+template <typename T, int NORM>
+__global__ void __launch_bounds__(kWave)
+kd_chain_adjoint_lvwave_kernel(const LayerConst* __restrict__ lcs, const T* __restrict__ p, int P, ChainAdjointArgs a,
+                               int stage_rec) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cv_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cv_raw);
+    T* ps = reinterpret_cast<T*>(cv_raw + 2 * sizeof(LayerConst));
+    T* mu = ps + P;                                  // [2][P]
+    T* km = mu + 2 * (size_t)P;                      // [7][P]
+    double* tsl = reinterpret_cast<double*>(km + 7 * (size_t)P);
+    double* dtsl = tsl + a.nsteps;
+    {
+        const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int i = threadIdx.x; i < 9 * P; i += blockDim.x) mu[i] = T(0);
+        for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
+            tsl[i] = a.ts[i];
+            dtsl[i] = a.dts[i];
+        }
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    __shared__ double red[1];
+    const Math<T> M{tab};
+    T* recl = nullptr;
+    if (stage_rec) {
+        recl = reinterpret_cast<T*>(dtsl + a.nsteps);
+        onewg_stage_rec<T>(recl, a, LvWaveShape::I);
+    }
+    LvWaveModel<T, NORM> m(M, lcl, ps, P);
+    onewg_adjoint<T>(m, a, mu, km, tsl, dtsl, red, recl);
+}
+
 // The one-workgroup adjoint (kd_chain_adjoint_kernel): the small-chain conditions of
 // launch_kd_chain_tsit5 plus nsteps <= kChainAdjointMaxSteps and the LDS budget.
 template <typename T>
@@ -1300,6 +1454,27 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
     if (nl < 1 || nl > kChainMaxLayers || B < 1 || B > kChainSolveMaxBatch || I_ne_O(hlcs, nl) || a.nsteps < 1 ||
         a.nsteps > kChainAdjointMaxSteps)
         return hipErrorNotSupported;
+    // one Lotka-Volterra trajectory: the chain on one wave (LvWaveModel)
+    if (wide && B == 1 && nl == 2 && hlcs[0].use_base && hlcs[1].use_base && hlcs[0].norm == hlcs[1].norm &&
+        hlcs[0].I == LvWaveShape::I && hlcs[0].O == LvWaveShape::H && hlcs[1].I == LvWaveShape::H &&
+        hlcs[1].O == LvWaveShape::O && hlcs[0].G == LvWaveShape::G && hlcs[1].G == LvWaveShape::G &&
+        hlcs[0].basis == BASIS_RBF && hlcs[1].basis == BASIS_RBF &&
+        (hlcs[0].norm == NORM_TANH_FAST || hlcs[0].norm == NORM_SOFTSIGN)) {
+        const size_t pre = 2 * sizeof(LayerConst) + sizeof(T) * (size_t)P * 9;
+        size_t lds = pre + 2 * sizeof(double) * a.nsteps;
+        const size_t rec = sizeof(T) * ((size_t)a.nsteps * 7 + 1) * LvWaveShape::I;
+        const int stage_rec = lds + rec <= 60 * 1024 ? 1 : 0;
+        if (stage_rec) lds += rec;
+        if (pre % 8 == 0 && lds <= 60 * 1024) {
+            if (hlcs[0].norm == NORM_TANH_FAST)
+                hipLaunchKernelGGL((kd_chain_adjoint_lvwave_kernel<T, NORM_TANH_FAST>), dim3(1), dim3(kWave), lds, st,
+                                   lcs, p, (int)P, a, stage_rec);
+            else
+                hipLaunchKernelGGL((kd_chain_adjoint_lvwave_kernel<T, NORM_SOFTSIGN>), dim3(1), dim3(kWave), lds, st,
+                                   lcs, p, (int)P, a, stage_rec);
+            return hipGetLastError();
+        }
+    }
     // one trajectory of a two-layer chain with base activations: the whole workgroup on it (WideModel)
     if (wide && B == 1 && nl == 2 && hlcs[0].use_base && hlcs[1].use_base && hlcs[0].norm == hlcs[1].norm &&
         hlcs[1].I == hlcs[0].O && wide_fits(WideShape{hlcs[0].I, hlcs[0].O, hlcs[1].O, hlcs[0].G, hlcs[1].G}) &&

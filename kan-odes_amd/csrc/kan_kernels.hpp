@@ -134,11 +134,11 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
 // (parts_out != nullptr with err_out: the per-block error partials are left in err_slab[0, *parts_out)
 // for the caller to sum -- the host, from mapped memory -- instead of a final reduction launch)
 
-// The adaptive Fisher-KPP solve with the step control on the device (kanode_solve.cpp solve_fk_loop): each
-// launch of the step kernel reads the step size and the step index from `ctl`, takes the step into the
-// dense-output slots of the table, and its last workgroup to finish sums the error partials and runs the PI
-// controller (solve_t's arithmetic): accept/reject, the step record ts/dts, the next step size.  The host
-// enqueues launches ahead without waiting on any of them; a launch after the end returns at once.
+// The adaptive Fisher-KPP solve with the step control on the device (kanode_solve.cpp solve_fk_loop): launch q
+// of the step kernel decides launch q - 1's attempt at its head (every workgroup sums the same error partials
+// and applies solve_t's PI controller: accept/reject, the step record, the next step size), then takes the
+// next attempt into the dense-output slots.  The host enqueues launches ahead without waiting on any of them;
+// a launch after the end passes the final state on and returns.
 struct StepCoef {
     double a[6][6];   // dt·a_sj
     double e[7];      // dt·btilde_j
@@ -147,27 +147,36 @@ struct StepCoef {
 };
 struct FkLoopCtl {
     double t, dt, qold;
-    int64_t step, nreject, it;   // accepted steps, rejections, attempts
+    int64_t step, nreject, it;   // accepted steps, rejections, decided attempts
     int32_t status;              // 0 running, 1 done, 2 maxiters reached
-    int32_t pad;
+    int32_t pending;             // the launch that wrote this state took an attempt (the next launch decides it)
+    void* cand[4];               // slots[step - 1 .. step + 2] (cand[0]: none at step 0)
 };
 struct FkLoopArgs {
-    FkLoopCtl* ctl;        // device state
-    FkLoopCtl* mirror;     // the host's mapped copy (device address), written with ctl
-    StepCoef* coef;        // [2] the attempt's coefficients, by attempt parity (it & 1)
-    void* const* slots;    // [cap] dense-output slots (u_n, Q_1..Q_4, k_7 of n entries each)
+    FkLoopCtl* state;      // [2]: launch q reads state[(q + 1) & 1] (launch q - 1's, the host's for q = 0); its
+                           // workgroup 0 writes state[q & 1] and the host's mirror
+    FkLoopCtl* mirror;     // the host's mapped copy (device address)
+    void* const* slots;    // dense-output slots (u_n, Q_1..Q_4, k_7 of n entries each), up to step + 2
     const double* k1_0;    // k_1 of the first step
-    double* ts;            // [cap] accepted steps: start time, step size
+    double* ts;            // accepted steps: start time, step size
     double* dts;
-    double* parts;         // [grid] error partials of a launch
-    unsigned* arrive;      // the launch's arrival counter (0 between launches)
+    double* parts;         // [2][max_grid] error partials, by launch parity
+    int64_t max_grid;
     int64_t n;             // state entries (Nx·B): the error norm's count and the slot vector stride
     double tf, abstol, reltol, dtmin, beta1, beta2, gamma, qmin, qmax, qoldinit;
     int64_t maxiters;
 };
+struct AdjLoopArgs;
+struct AdjLoopCtl;
+struct AdjLoopPlan;
+bool fk_adjoint_loop_supported(const PPConst& hpc, const LayerConst& hlc, int Nx);
+int fk_adjoint_loop_grid(int64_t B, int slab_blocks);
+hipError_t launch_fk_adjoint_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                  const double* p, double* tables, double cd, double co, int Nx, const AdjLoopArgs& la,
+                                  int64_t B, hipStream_t st, bool build);
 hipError_t launch_fk_step_pp_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, double cd,
                                   double co, int Nx, const double* p, const double* table, const FkLoopArgs& la,
-                                  int64_t B, int max_grid, hipStream_t st, int grid_ovr = 0);
+                                  int64_t lq, int64_t B, hipStream_t st, int grid_ovr = 0);
 hipError_t launch_fk_vjp_pp(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
                             const double* p, double* tables, double cd, double co, int Nx, const double* u,
                             const double* lam, double* lamJ, double* dp, double* slab, int slab_blocks, int64_t B,

@@ -22,6 +22,7 @@
 #include "kan_kernels.hpp"
 #include "kan_lap.hpp"
 #include "kan_pp_point.hpp"
+#include "kan_adjloop.hpp"
 #include "kan_tsit5.hpp"
 
 #include <cstdlib>
@@ -961,8 +962,8 @@ __device__ __forceinline__ double fin_ld(const double* p) {
     if constexpr (AG) return ld_agent(p);
     else return *p;
 }
-template <bool AG>
-__device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, int64_t q, double* red, double* sums) {
+template <bool AG, bool AGW = false, class F = AdjFinish>
+__device__ __forceinline__ void adj_finish_block(const F& f, int64_t P, int64_t q, double* red, double* sums) {
     // four of each thread's rows per pass, all loads issued before the adds (same order of the adds)
     const int64_t bs = blockDim.x;
     if (q == P) {   // the λ error partials
@@ -979,7 +980,10 @@ __device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, 
         const double v[1] = {s};
         block_sum_to<double, 1>(v, 1, red, sums);
         __syncthreads();
-        if (threadIdx.x == 0) f.out[0] = sums[0];
+        if (threadIdx.x == 0) {
+            if constexpr (AGW) st_agent(f.out, sums[0]);   // (read by the controller of this launch)
+            else f.out[0] = sums[0];
+        }
         return;
     }
     double acc[6];
@@ -1025,7 +1029,8 @@ __device__ __forceinline__ void adj_finish_block(const AdjFinish& f, int64_t P, 
         f.km7[q] = k7;
         const double e = ::fma(f.e0, k1, ce);
         const double r = e / ::fma(f.reltol, fmax(kabs(m0), kabs(mn)), f.abstol);
-        f.out[1 + q] = r * r;
+        if constexpr (AGW) st_agent(f.out + 1 + q, r * r);
+        else f.out[1 + q] = r * r;
     }
 }
 
@@ -1070,245 +1075,31 @@ __device__ __forceinline__ void rows_fused_finish(const AdjFinish& f, unsigned* 
     }
 }
 
+// The rows step's body (kan_rows_body.inc) reads its arguments as `a`: the kernel's own (by value), or in
+// fk_vjp_step_rows_loop_kernel (the device step control, kan_adjloop.hpp) the attempt's plan through the
+// constant address space.  (A reference to the by-value argument made the compiler form the arguments'
+// products per use: +23% VALU.)
 template <int NORM, int PATH, int GT, int NP, int CMB, int NI = 0>
 __global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
 fk_vjp_step_rows_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                         const double2* __restrict__ tables, int ni_rt, double inv_w, double x0, double cd, double co,
                         int64_t B, AdjStepArgs a) {
-    constexpr int Nx = 128 * NP;
-    const int ni = NI > 0 ? NI : ni_rt;
-    extern __shared__ double2 tl[];
-    __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t b = (int64_t)blockIdx.x * (kVjpBlock / kWave) + (threadIdx.x >> 6);
-    const bool live = b < B;
-    // KAN_VROWS_CONTIG: lane l holds the row's points [2·NP·l, 2·NP·(l + 1)) (pair k at 2·NP·l + 2k), so
-    // the stencil's only cross-lane values are the two ends of each lane's run; otherwise pair k at 128k + 2l
-    constexpr int kOff = KAN_VROWS_CONTIG ? 2 : 128;
-    const int64_t rb = (live ? b : 0) * Nx + (KAN_VROWS_CONTIG ? 2 * NP : 2) * lane;
-#if KAN_VROWS_L2LOAD   // timing experiment only: every wave loads one of 64 rows (L2-resident), stores its own
-    const int64_t rbl = ((live ? b : 0) & 63) * Nx + (KAN_VROWS_CONTIG ? 2 * NP : 2) * lane;
-#else
-    const int64_t rbl = rb;
-#endif
-    // the row's loads are in flight while the block stages its tables
-    kd2 lam0[NP], kl[6][NP], ui[NP], qi[4][NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        lam0[k] = kd2{0.0, 0.0};
-        kl[0][k] = kd2{0.0, 0.0};
-        ui[k] = kd2{0.0, 0.0};
-#pragma unroll
-        for (int m = 0; m < 4; ++m) qi[m][k] = kd2{0.0, 0.0};
-    }
-    if (live) {
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            lam0[k] = ld_vstep(a.lam + rbl + kOff * k);
-            kl[0][k] = ld_vstep(a.kl[0] + rbl + kOff * k);
-            ui[k] = ld_vstep(a.su_u[0] + rbl + kOff * k);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[0][m] + rbl + kOff * k);
-        }
-    }
-    const int tsz = (kPPCoef / 2) * ni;
-    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
-        tl[i] = tables[PP_DPHI * tsz + i];
-        tl[tsz + i] = tables[PP_SWISH * tsz + i];
-    }
-    KAN_EXP_TABLE_LDS(tab);
-    const Math<double> M{tab};
-    const double2* __restrict__ td = tl;
-    const double2* __restrict__ ts = tl + tsz;
-    const LayerConst& lc = *lcp;
-    const RecScalars<double> rc(lc);
-    const int P = GT + (lc.use_base ? 1 : 0);
-    double eacc = 0.0;
-    // (a runtime flag: a compile-time one made the fixed-step instantiation spill 1.2 KB/lane, and the
-    // adaptive one, which is launched only to combine, 168 B/lane: round 5, 57 -> 69 us per step)
-    const bool combine = a.combine != 0;
-    double comb[GT + 1];
-#pragma unroll
-    for (int j = 0; j <= GT; ++j) comb[j] = 0.0;
-    // CMB == 2: the μ error combination E is accumulated in this thread's LDS column (in registers it
-    // pushed the kernel past 256 VGPRs: 260 B/lane of scratch)
-    __shared__ double combe[CMB == 2 ? (GT + 1) * kVjpBlock : 1];
-    if constexpr (CMB == 2) {
-#pragma unroll
-        for (int j = 0; j <= GT; ++j) combe[j * kVjpBlock + threadIdx.x] = 0.0;
-    }
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-        double S0[GT];   // (set by the stage's first point; zeros for an idle wave)
-        float S1[GT], S2[GT];
-        double dW;
-        const bool last = s == 5;
-        const bool want_err = last && a.err_slab != nullptr;
-        if (live) {
-            if (s > 0 && a.reload[s]) {
-#pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    ui[k] = ld_vstep(a.su_u[s] + rbl + kOff * k);
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) qi[m][k] = ld_vstep(a.su_q[s][m] + rbl + kOff * k);
-                }
-            }
-            kd2 uv[NP], lv[NP], ev[NP];
-            // λs first (registers only): a reloaded stage's dense output is still in flight
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {   // λs = λ + Σ_{j<=s} h a_sj kλ_j (and the error sum)
-                kd2 t{0.0, 0.0}, e{0.0, 0.0};
-#pragma unroll
-                for (int j = 0; j <= s; ++j) {
-                    const double c = a.a[s][j], ce = a.ec[j];
-                    t.x = ::fma(c, kl[j][k].x, t.x);
-                    t.y = ::fma(c, kl[j][k].y, t.y);
-                    if (want_err) {
-                        e.x = ::fma(ce, kl[j][k].x, e.x);
-                        e.y = ::fma(ce, kl[j][k].y, e.y);
-                    }
-                }
-                lv[k].x = ::fma(1.0, t.x, lam0[k].x);
-                lv[k].y = ::fma(1.0, t.y, lam0[k].y);
-                ev[k] = e;
-            }
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {   // u(t_s) = u_i + Σ_m θ^m Q_m
-                kd2 t{0.0, 0.0};
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    t.x = ::fma(a.su_c[s][m], qi[m][k].x, t.x);
-                    t.y = ::fma(a.su_c[s][m], qi[m][k].y, t.y);
-                }
-                uv[k].x = ::fma(1.0, t.x, ui[k].x);
-                uv[k].y = ::fma(1.0, t.y, ui[k].y);
-            }
-            if (last && a.lam_out) {
-#pragma unroll
-                for (int k = 0; k < NP; ++k) st_vstep(a.lam_out + rb + kOff * k, lv[k]);
-            }
-#if KAN_VROWS_CONTIG
-            double la[2 * NP];
-            lap_lane<NP>(lv, lane, cd, co, la);
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                const double a0 = la[2 * k], a1 = la[2 * k + 1];
-#else
-            double rr[NP], rl[NP];
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                rr[k] = wave_ror1(lv[k].y);
-                rl[k] = wave_rol1(lv[k].x);
-            }
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                const double lm = lane == 0 ? rr[(k + NP - 1) % NP] : rr[k];
-                const double lp = lane == kWave - 1 ? rl[(k + 1) % NP] : rl[k];
-                double a0, a1;
-                lap_pair<double>(lm, lv[k].x, lv[k].y, lp, 128 * k + 2 * lane, Nx, cd, co, a0, a1);
-#endif
-#if KAN_VROWS_SKEL   // timing experiment only: the memory and reduction skeleton without the pullback
-                const double x0b = uv[k].x * lv[k].x, x1b = uv[k].y * lv[k].y;
-#pragma unroll
-                for (int j = 0; j < GT; ++j) {
-                    S0[j] = k == 0 ? x0b : S0[j] + x0b;
-                    S1[j] = S2[j] = (float)x1b;
-                }
-                dW = x1b;
-#else
-#if KAN_VROWS_SB
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                const double x0b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].x, lv[k].x,
-                                                               S0, S1, S2, dW, k == 0);
-#if KAN_VROWS_SB
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                const double x1b = pp_vjp_point<NORM, PATH, GT>(M, lc, p, rc, td, ts, ni, inv_w, x0, uv[k].y, lv[k].y,
-                                                               S0, S1, S2, dW);
-#endif
-                kd2 o;
-                o.x = a0 + x0b;
-                o.y = a1 + x1b;
-                if (!last) {
-                    kl[s + 1 < 6 ? s + 1 : 5][k] = o;
-                } else {
-                    st_vstep(a.kl[6] + rb + kOff * k, o);
-                    if (want_err) {
-                        const double en = a.ec[6];
-                        const double ex = ::fma(en, o.x, ev[k].x), ey = ::fma(en, o.y, ev[k].y);
-                        const double sx = ::fma(a.reltol, fmax(kabs(lam0[k].x), kabs(lv[k].x)), a.abstol);
-                        const double sy = ::fma(a.reltol, fmax(kabs(lam0[k].y), kabs(lv[k].y)), a.abstol);
-                        const double rx = ex / sx, ry = ey / sy;
-                        eacc = ::fma(rx, rx, eacc);
-                        eacc = ::fma(ry, ry, eacc);
-                    }
-                }
-            }
-        }
-        else {
-#pragma unroll
-            for (int j = 0; j < GT; ++j) {
-                S0[j] = 0.0;
-                S1[j] = S2[j] = 0.0f;
-            }
-            dW = 0.0;
-        }
-        double acc[GT + 1];
-#pragma unroll
-        for (int j = 0; j < GT; ++j) {
-            const double e = lc.e[j];
-            acc[j] = PATH == PATH_REC_CORR ? lc.K[j] * ::fma(lc.h2[j], (double)S2[j], ::fma(e, (double)S1[j], S0[j]))
-                                           : lc.K[j] * S0[j];
-        }
-        acc[GT] = dW;
-#if KAN_VROWS_NORED   // timing experiment only: no moment reduction (wrong dp)
-        {
-            double t = 0.0;
-#pragma unroll
-            for (int j = 0; j <= GT; ++j) t += acc[j];
-            if (threadIdx.x == 0) a.slab[s][(int64_t)blockIdx.x * P] = t;
-        }
-#else
-        if constexpr (CMB == 2) {   // the μ error combination over all six stages
-#pragma unroll
-            for (int j = 0; j <= GT; ++j)
-                combe[j * kVjpBlock + threadIdx.x] = ::fma(a.ec[s + 1], acc[j], combe[j * kVjpBlock + threadIdx.x]);
-        }
-        if (combine && s < 5) {
-#pragma unroll
-            for (int j = 0; j <= GT; ++j) comb[j] = ::fma(a.a[5][s + 1], acc[j], comb[j]);
-        } else {
-            // a combined step's rows go parameter-major, [P][grid] (AdjFinish::tr, FinishJob::tr): the finish
-            // reads them coalesced
-            if constexpr (CMB == 2)
-                block_sum_to<double, GT + 1, true>(acc, P, red, a.slab[s] + blockIdx.x, gridDim.x);
-            else if (combine)
-                block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + blockIdx.x, gridDim.x);
-            else
-                block_sum_to<double, GT + 1>(acc, P, red, a.slab[s] + (int64_t)blockIdx.x * P);
-        }
-#endif
-    }
-    if (combine) {
-        __syncthreads();   // red is reused
-        block_sum_to<double, GT + 1, CMB == 2>(comb, P, red, a.slab[0] + blockIdx.x, gridDim.x);
-    }
-    if constexpr (CMB == 2) {
-        double ce[GT + 1];
-#pragma unroll
-        for (int j = 0; j <= GT; ++j) ce[j] = combe[j * kVjpBlock + threadIdx.x];
-        __syncthreads();
-        block_sum_to<double, GT + 1, true>(ce, P, red, a.slab[1] + blockIdx.x, gridDim.x);
-    }
-    if (a.err_slab) {
-        const double v[1] = {eacc};
-        block_sum_to<double, 1, CMB == 2>(v, 1, red, a.err_slab + blockIdx.x);
-    }
-    if constexpr (CMB == 2) {
-        static_assert(kVjpBlock == kAdjFinBlock, "the fused finish runs adj_finish_kernel's blocks in its order");
-        if (a.fin_ctr) rows_fused_finish(a.fin, a.fin_ctr, P);
-    }
+#define KAN_ROWS_BODY_DEV 0
+#include "kan_rows_body.inc"
+#undef KAN_ROWS_BODY_DEV
+}
+
+template <int NORM, int PATH, int GT, int NP, int CMB, int NI = 0>
+__global__ void __launch_bounds__(kVjpBlock) __attribute__((amdgpu_waves_per_eu(KAN_VROWS_WPE)))
+fk_vjp_step_rows_loop_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                             const double2* __restrict__ tables, int ni_rt, double inv_w, double x0, double cd,
+                             double co, int64_t B, const AdjLoopCtl* __restrict__ lctl, const AdjLoopPlan* lplan) {
+    if (lctl->status != 0) return;   // the adjoint has ended or paused: a launch the host queued ahead
+    typedef const __attribute__((address_space(4))) AdjStepArgs CArgs;
+    const CArgs& a = *(CArgs*)&lplan[lctl->it & 1].a;
+#define KAN_ROWS_BODY_DEV 1
+#include "kan_rows_body.inc"
+#undef KAN_ROWS_BODY_DEV
 }
 
 // dp[q] (= or +=) Σ_b slab[b·P + q] for q < P (block q), and err_out[0] = Σ_b err_slab[b]
@@ -1384,6 +1175,109 @@ hipError_t launch_adj_finish(const AdjFinish& f, int64_t P, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---- the adjoint's device step control (kan_adjloop.hpp) --------------------------------------------------
+// The forward steps the next plan's stages can fall in, staged in LDS by the controlling workgroup: the window
+// ends a few steps above the last planned stage's (the adjoint runs backward in t); beyond it, global loads.
+constexpr int kAdjWin = 256;
+struct AdjFwWindow {
+    const double* wts;
+    const double* wdts;
+    void* const* wsl;
+    int64_t w0, wn;
+    const double* gts;
+    const double* gdts;
+    void* const* gsl;
+    __device__ bool in(int64_t i) const { return i >= w0 && i < w0 + wn; }
+    __device__ double ts(int64_t i) const { return in(i) ? wts[i - w0] : gts[i]; }
+    __device__ double dts(int64_t i) const { return in(i) ? wdts[i - w0] : gdts[i]; }
+    __device__ const void* slot(int64_t i) const { return in(i) ? wsl[i - w0] : gsl[i]; }
+};
+
+// The finish launch of an attempt: each workgroup runs its block of adj_finish_kernel (the error terms by
+// agent-scope stores), then counts itself in; the last to arrive sums the terms in adjoint_t's order, applies
+// its PI controller (thread 0) and plans the next attempt into LDS, which the whole workgroup then stores.
+// Every workgroup stages the forward-step window and reads the state at its start, so the controller's
+// inputs are on chip when the last one arrives (its only wait is the terms' round trip).
+constexpr int kAdjMaxTerms = kMaxGrid + 2;   // 1 + P, P <= G + 1
+__global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopArgs la) {
+    __shared__ double red[(kAdjFinBlock / kWave) * 6];
+    __shared__ double sums[6];
+    __shared__ double wts[kAdjWin], wdts[kAdjWin];
+    __shared__ void* wsl[kAdjWin];
+    __shared__ double terms[kAdjMaxTerms];
+    __shared__ unsigned arr;
+    __shared__ AdjLoopPlan lp;
+    __shared__ int go;
+    __shared__ int64_t nit;   // the planned attempt's index (thread 0's state)
+    const AdjLoopCtl* cp = la.ctl;
+    if (cp->status != 0) return;
+    AdjLoopCtl c = *cp;
+    int64_t w0 = c.fi - (kAdjWin - 8);
+    if (w0 < 0) w0 = 0;
+    const int64_t wn = la.nsteps - w0 < kAdjWin ? la.nsteps - w0 : kAdjWin;
+    for (int64_t i = threadIdx.x; i < wn; i += blockDim.x) {   // (published by the finish block's barriers)
+        wts[i] = la.fts[w0 + i];
+        wdts[i] = la.fdts[w0 + i];
+        wsl[i] = la.slots[w0 + i];
+    }
+    typedef const __attribute__((address_space(4))) AdjFinish CFin;
+    adj_finish_block<false, true>(*(CFin*)&la.plan[c.it & 1].f, la.P, blockIdx.x, red, sums);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's error term has landed
+    __syncthreads();
+    if (threadIdx.x == 0) arr = __hip_atomic_fetch_add(la.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (arr != gridDim.x - 1u) return;
+    if (threadIdx.x <= la.P) terms[threadIdx.x] = ld_agent(la.out + threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double mus = 0.0;   // the μ terms in order, then the λ total (adjoint_t)
+        for (int64_t q = 0; q < la.P; ++q) mus += terms[1 + q];
+        const double sumsq = terms[0] + mus;
+        const double eest = ::sqrt(sumsq / la.ntot);
+        const double q11 = eest > 0 ? ::pow(eest, la.beta1) : 0.0;
+        ++c.it;
+        c.nf += 6;
+        if (eest > 1.0 && c.h > la.dtmin) {
+            ++c.nreject;
+            c.h = c.h / ::fmin(1.0 / la.qmin, q11 / la.gamma);
+        } else {
+            double q = q11 / ::pow(c.qold, la.beta2);
+            q = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, q / la.gamma));
+            const double hnew = q > 0 ? c.h / q : c.h * la.qmax;
+            c.qold = ::fmax(eest, la.qoldinit);
+            if (la.hs && c.naccept < la.hs_cap) la.hs[c.naccept] = c.h;
+            c.tau = c.tau + c.h;
+            c.lc ^= 1;
+            c.mc ^= 1;
+            c.fs ^= 1;   // FSAL: kλ_7, kμ_7 become the next step's first stage values
+            ++c.naccept;
+            c.h = hnew;
+            if (::fabs(c.tau - la.stops[c.si]) <= 1e-12 * ::fmax(1.0, la.TT)) {
+                c.tau = la.stops[c.si];
+                if (c.si + 1 < la.nstops) c.status = 3;   // the host takes the saveat jump and the next stop
+            }
+        }
+        if (c.status == 0) adj_loop_top(la, c);
+        go = c.status == 0;
+        nit = c.it;
+        if (go) {
+            const AdjFwWindow fw{wts, wdts, wsl, w0, wn, la.fts, la.fdts, la.slots};
+            adj_loop_plan(la, c, lp, fw);
+        }
+        *la.ctl = c;
+        *la.mirror = c;
+        __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (go) {   // the plan, 8 bytes per thread (the next launches read it after this one ends)
+        constexpr int nw = sizeof(AdjLoopPlan) / sizeof(uint64_t);
+        static_assert(sizeof(AdjLoopPlan) % sizeof(uint64_t) == 0, "plan words");
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(&lp);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(la.plan + (nit & 1));
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
 // du = D·lap·y + KAN(y) for one trajectory row held by one wave (lane: pairs 128k + 2·lane),
 // stencil neighbours by wave rotation, the KAN from the LDS table (direct formula off-table)
 template <int NORM, int BASIS, int NP>
@@ -1432,91 +1326,96 @@ struct StepOut {
 #define KAN_FSTEP_WPE KAN_PP_WPE
 #endif
 
-// The step control of a device-controlled solve (FkLoopArgs), run by the last workgroup of the step launch to
-// arrive: every workgroup has stored its error partial (agent-scope stores, drained) and counts itself in;
-// the last sums the partials in block order, then thread 0 applies solve_t's PI controller to the step and
-// writes the state for the next launch (and its host mirror).  Nothing waits: the other workgroups leave.
-__device__ __forceinline__ void fk_loop_coef(StepCoef* k, double dt) {
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 6; ++j) k->a[i][j] = j <= i ? dt * Tsit5Tab::TA[i][j] : 0.0;
-    for (int j = 0; j < 7; ++j) k->e[j] = dt * Tsit5Tab::BT[j];
-    for (int m = 0; m < 4; ++m)
-        for (int i = 0; i < 7; ++i) k->q[m][i] = dt * Tsit5Tab::RI[i][m];
-}
-__device__ __forceinline__ void fk_loop_control(const FkLoopArgs& la) {
-    __shared__ unsigned arr;
-    __shared__ double fred[kBlock / kWave];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's partial has landed
-    __syncthreads();
-    if (threadIdx.x == 0) arr = __hip_atomic_fetch_add(la.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const unsigned G = gridDim.x;
-    if (arr != G - 1u) return;
+// The step control of a device-controlled solve (FkLoopArgs), at the head of the NEXT launch: every workgroup
+// of launch q sums launch q - 1's error partials in the same order and applies solve_t's PI controller to its
+// attempt, so all reach the same decision with no grid-wide wait; workgroup 0 records an accepted step and
+// writes the state launch q + 1 reads (and the host's mirror).  Returns false when the solve has ended.
+__device__ __forceinline__ bool fk_loop_decide(const FkLoopArgs& la, int64_t q, FkLoopCtl& c, double* red,
+                                               double* lsum) {
+    // the previous launch's partials are loaded with the state, not after it (one round trip)
+    const double* pp = la.parts + ((q + 1) & 1) * la.max_grid;
     double s = 0.0;
-    for (unsigned b = threadIdx.x; b < G; b += kBlock) s += ld_agent(la.parts + b);
-    const double v[1] = {s};
-    block_sum_to<double, 1>(v, 1, fred, fred);   // (fred[0] <- the total; the block's order is fixed)
-    if (threadIdx.x != 0) return;
-    FkLoopCtl c = *la.ctl;
-    const double eest = ::sqrt(fred[0] / (double)la.n);
-    const double q11 = eest > 0 ? ::pow(eest, la.beta1) : 0.0;
-    ++c.it;
-    if (eest > 1.0 && c.dt > la.dtmin) {
-        ++c.nreject;
-        c.dt = c.dt / ::fmin(1.0 / la.qmin, q11 / la.gamma);
-    } else {
-        double q = q11 / ::pow(c.qold, la.beta2);
-        q = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, q / la.gamma));
-        if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
-        const double dtnew = q > 0 ? c.dt / q : c.dt * la.qmax;
-        c.qold = ::fmax(eest, la.qoldinit);
-        la.ts[c.step] = c.t;
-        la.dts[c.step] = c.dt;
-        c.t = c.t + c.dt;
-        ++c.step;
-        c.dt = dtnew;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += kBlock) s += pp[b];
+    const FkLoopCtl* sp = la.state + ((q + 1) & 1);
+    c = *sp;
+    const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
+    FkLoopCtl* out = la.state + (q & 1);
+    if (c.status != 0) {   // ended earlier: a launch queued ahead passes the state on
+        if (w0) *out = c;
+        return false;
+    }
+    if (c.pending) {
+        const double v[1] = {s};
+        block_sum_to<double, 1>(v, 1, red, lsum);   // (the same order in every workgroup)
+        const double eest = ::sqrt(*lsum / (double)la.n);
+        const double q11 = eest > 0 ? ::pow(eest, la.beta1) : 0.0;
+        ++c.it;
+        if (eest > 1.0 && c.dt > la.dtmin) {
+            ++c.nreject;
+            c.dt = c.dt / ::fmin(1.0 / la.qmin, q11 / la.gamma);
+        } else {
+            double qq = q11 / ::pow(c.qold, la.beta2);
+            qq = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, qq / la.gamma));
+            if (1.0 <= qq && qq <= 1.0) qq = 1.0;   // qsteady_min = qsteady_max = 1
+            const double dtnew = qq > 0 ? c.dt / qq : c.dt * la.qmax;
+            c.qold = ::fmax(eest, la.qoldinit);
+            if (w0) {
+                la.ts[c.step] = c.t;
+                la.dts[c.step] = c.dt;
+            }
+            c.t = c.t + c.dt;
+            ++c.step;
+            c.dt = dtnew;
+            for (int k = 0; k < 3; ++k) c.cand[k] = c.cand[k + 1];   // slots[step - 1 .. step + 1]
+            c.cand[3] = nullptr;
+        }
     }
     if (c.t >= la.tf - 1e-14 * ::fmax(1.0, ::fabs(la.tf))) c.status = 1;
     else if (c.it >= la.maxiters) c.status = 2;
     else c.dt = ::fmin(c.dt, la.tf - c.t);   // (solve_t clips at the top of its next iteration)
-    if (c.status == 0) fk_loop_coef(la.coef + (c.it & 1), c.dt);
-    *la.ctl = c;
-    *la.mirror = c;
-    __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c.pending = c.status == 0 ? 1 : 0;
+    if (w0) {
+        FkLoopCtl o = c;
+        if (o.status == 0) o.cand[3] = la.slots[o.step + 2];
+        *out = o;
+        *la.mirror = o;
+    }
+    return c.status == 0;
 }
-// DEV (FkLoopArgs, solve_fk_loop): the step index comes from la.ctl, the coefficients from la.coef (the
-// controller's products of dt and the tableau, as the host forms them), the vectors are the slots of the
-// table, and the last workgroup to finish runs the step control (fk_loop_control).
+// DEV (FkLoopArgs, solve_fk_loop, launch q): the attempt's step and size come from fk_loop_decide, its
+// coefficients (dt times the tableau, as the host forms them) from LDS, its vectors are the slots of the
+// table, and the error partials go to la.parts for launch q + 1.
 template <int NORM, int BASIS, int NP, bool DEV = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KAN_FSTEP_WPE)))
 fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
                        const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co,
                        const double* __restrict__ u, const double* __restrict__ k1, StepOut so, StepCoef sc,
-                       double* __restrict__ err_slab, int64_t B, FkLoopArgs la) {
+                       double* __restrict__ err_slab, int64_t B, FkLoopArgs la, int64_t lq) {
     constexpr int Nx = 128 * NP;
     extern __shared__ double2 tl[];
     __shared__ double red[kBlock / kWave];
-    // DEV: the attempt's coefficients, read through the constant address space (scalar loads the compiler may
-    // repeat anywhere, as it does for kernel arguments: the controller writes the other buffer)
-    typedef const __attribute__((address_space(4))) StepCoef ConstCoef;
-    ConstCoef* cf = nullptr;
+    // DEV: the attempt's coefficients in LDS (published by the table staging's barrier below)
+    __shared__ StepCoef lsc[1];
+    __shared__ double lsum;
     if constexpr (DEV) {
-        const FkLoopCtl* c = la.ctl;
-        if (c->status != 0) return;   // the solve has ended: a launch the host queued ahead
-        const int64_t step = c->step;
-        cf = (ConstCoef*)(la.coef + (c->it & 1));
-        double* const cur = static_cast<double*>(la.slots[step]);
+        FkLoopCtl c;
+        if (!fk_loop_decide(la, lq, c, red, &lsum)) return;   // the solve has ended: a launch queued ahead
+        double* const cur = static_cast<double*>(c.cand[1]);
         u = cur;
-        k1 = step == 0 ? la.k1_0 : static_cast<const double*>(la.slots[step - 1]) + 5 * la.n;
+        k1 = c.step == 0 ? la.k1_0 : static_cast<const double*>(c.cand[0]) + 5 * la.n;
 #pragma unroll
         for (int m = 0; m < 4; ++m) so.k[m] = cur + (m + 1) * la.n;
         so.k[5] = cur + 5 * la.n;
-        so.u_new = static_cast<double*>(la.slots[step + 1]);
-        err_slab = la.parts;
+        so.u_new = static_cast<double*>(c.cand[2]);
+        err_slab = la.parts + (lq & 1) * la.max_grid;
+        const int t = threadIdx.x;
+        if (t < 36) lsc[0].a[t / 6][t % 6] = t % 6 <= t / 6 ? c.dt * Tsit5Tab::TA[t / 6][t % 6] : 0.0;
+        else if (t < 43) lsc[0].e[t - 36] = c.dt * Tsit5Tab::BT[t - 36];
+        else if (t < 71) lsc[0].q[(t - 43) / 7][(t - 43) % 7] = c.dt * Tsit5Tab::RI[(t - 43) % 7][(t - 43) / 7];
     }
-    auto ca = [&](int s_, int j) { return DEV ? cf->a[s_][j] : sc.a[s_][j]; };   // dt·a_sj
-    auto ce = [&](int j) { return DEV ? cf->e[j] : sc.e[j]; };                     // dt·btilde_j
-    auto cq = [&](int m, int i) { return DEV ? cf->q[m][i] : sc.q[m][i]; };        // dt·RI[i][m]
+    auto ca = [&](int s_, int j) { return DEV ? lsc[0].a[s_][j] : sc.a[s_][j]; };   // dt·a_sj
+    auto ce = [&](int j) { return DEV ? lsc[0].e[j] : sc.e[j]; };                     // dt·btilde_j
+    auto cq = [&](int m, int i) { return DEV ? lsc[0].q[m][i] : sc.q[m][i]; };        // dt·RI[i][m]
     const double abstol = DEV ? la.abstol : sc.abstol, reltol = DEV ? la.reltol : sc.reltol;
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
@@ -1589,8 +1488,7 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     }
     if constexpr (DEV) {
         const double v[1] = {eacc};
-        block_sum_to<double, 1, true>(v, 1, red, err_slab + blockIdx.x);
-        fk_loop_control(la);
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
     } else if (want_err) {
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
@@ -1807,7 +1705,7 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
         grid = grid_for(B, kBlock / kWave, gcap < slab_blocks ? gcap : slab_blocks);                            \
         hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP>), dim3(grid), dim3(kBlock), lds, st, lc, p,  \
                            (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, u, k1, so, sc, slab, B,    \
-                           FkLoopArgs{});                                                                        \
+                           FkLoopArgs{}, (int64_t)0);                                                            \
     } while (0)
 #define KAN_STEP_GO(NORM, BASIS)                                                                                 \
     do {                                                                                                         \
@@ -1829,11 +1727,12 @@ hipError_t launch_fk_step_pp(const PPConst& hpc, const LayerConst& hlc, const La
     return launch_stage_error_final(err_slab, grid, err_out, st);
 }
 
-// One attempt of the device-controlled solve (FkLoopArgs): the step kernel's DEV instantiation over a grid of
-// at most max_grid workgroups (la.parts holds that many partials).  The tables must already be built.
+// Launch lq of the device-controlled solve (FkLoopArgs): the step kernel's DEV instantiation over a grid of at
+// most la.max_grid workgroups (the same grid every launch).  The tables must already be built.
 hipError_t launch_fk_step_pp_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, double cd,
                                   double co, int Nx, const double* p, const double* table, const FkLoopArgs& la,
-                                  int64_t B, int max_grid, hipStream_t st, int grid_ovr) {
+                                  int64_t lq, int64_t B, hipStream_t st, int grid_ovr) {
+    const int max_grid = (int)la.max_grid;
     if (!fk_stage_pp_supported(hpc, Nx)) return hipErrorInvalidValue;
     const size_t lds = sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
 #define KAN_LOOP_WAVE(NORM, BASIS, NP)                                                                           \
@@ -1844,7 +1743,7 @@ hipError_t launch_fk_step_pp_loop(const PPConst& hpc, const LayerConst& hlc, con
         const int grid = grid_for(B, kBlock / kWave, gcap < max_grid ? gcap : max_grid);                        \
         hipLaunchKernelGGL((fk_step_pp_wave_kernel<NORM, BASIS, NP, true>), dim3(grid), dim3(kBlock), lds, st,  \
                            lc, p, (const double2*)table, hpc.ni, hpc.inv_w, hpc.x0, cd, co, nullptr, nullptr,  \
-                           StepOut{}, StepCoef{}, nullptr, B, la);                                               \
+                           StepOut{}, StepCoef{}, nullptr, B, la, lq);                                           \
     } while (0)
 #define KAN_LOOP_GO(NORM, BASIS)                                                                                 \
     do {                                                                                                         \
@@ -2027,19 +1926,19 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
                 if (a.combine == 2)                                                                              \
                     hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, 2, 2, 256>), dim3(grid),           \
                                        dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,\
-                                       hpc.x0, cd, co, B, a);                                                    \
+                                       hpc.x0, cd, co, B, a);                                   \
                 else                                                                                             \
                     hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, 2, 0, 256>), dim3(grid),           \
                                        dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,\
-                                       hpc.x0, cd, co, B, a);                                                    \
+                                       hpc.x0, cd, co, B, a);                                   \
             } else if (a.combine == 2)                                                                           \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 2>), dim3(grid),    \
                                    dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
-                                   hpc.x0, cd, co, B, a);                                                        \
+                                   hpc.x0, cd, co, B, a);                                       \
             else                                                                                                 \
                 hipLaunchKernelGGL((fk_vjp_step_rows_kernel<NORM, PATH, GT, (NP < 4 ? NP : 2), 0>), dim3(grid),    \
                                    dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w,    \
-                                   hpc.x0, cd, co, B, a);                                                        \
+                                   hpc.x0, cd, co, B, a);                                       \
             break;                                                                                               \
         }                                                                                                        \
         static int cap = 0;                                                                                      \
@@ -2071,6 +1970,55 @@ hipError_t launch_fk_vjp_step_pp(const PPConst& hpc, const LayerConst& hlc, cons
 #undef KAN_VSTEP_NP
 #undef KAN_VSTEP
     *grid_out = grid;
+    return hipGetLastError();
+}
+
+// One attempt of the device-controlled adaptive adjoint (kan_adjloop.hpp): the rows kernel's DEV instantiation
+// over la.grid workgroups and the finish launch with the controller.  Supported where launch_fk_vjp_step_pp
+// takes the rows kernel with the combined adaptive step (fk_adjoint_loop_supported).
+bool fk_adjoint_loop_supported(const PPConst& hpc, const LayerConst& hlc, int Nx) {
+    return fk_vjp_pp_supported(hlc, Nx) && (Nx == 128 || Nx == 256) && hpc.ni > 0;
+}
+int fk_adjoint_loop_grid(int64_t B, int slab_blocks) {   // the rows step's grid (0: the batch is above its cap)
+    return B >= 1 && B <= (int64_t)(kVjpBlock / kWave) * slab_blocks ? grid_for(B, kVjpBlock / kWave, slab_blocks) : 0;
+}
+hipError_t launch_fk_adjoint_loop(const PPConst& hpc, const LayerConst& hlc, const LayerConst* lc, const PPConst* pc,
+                                  const double* p, double* tables, double cd, double co, int Nx, const AdjLoopArgs& la,
+                                  int64_t B, hipStream_t st, bool build) {
+    if (!fk_adjoint_loop_supported(hpc, hlc, Nx) || la.grid < 1) return hipErrorInvalidValue;
+    const int fns[2] = {PP_DPHI, PP_SWISH};
+    hipError_t e = hipSuccess;
+    if (build && (e = launch_fk_pp_build(hpc, lc, pc, p, tables, fns, 2, st)) != hipSuccess) return e;
+    const size_t lds = 2 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni;
+#define KAN_ALOOP(NORM, PATH, GT)                                                                                 \
+    do {                                                                                                         \
+        if (Nx == 256 && hpc.ni == 256)                                                                          \
+            hipLaunchKernelGGL((fk_vjp_step_rows_loop_kernel<NORM, PATH, GT, 2, 2, 256>), dim3(la.grid),          \
+                               dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0,  \
+                               cd, co, B, la.ctl, la.plan);                                                 \
+        else if (Nx == 256)                                                                                      \
+            hipLaunchKernelGGL((fk_vjp_step_rows_loop_kernel<NORM, PATH, GT, 2, 2, 0>), dim3(la.grid),            \
+                               dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0,  \
+                               cd, co, B, la.ctl, la.plan);                                                 \
+        else                                                                                                     \
+            hipLaunchKernelGGL((fk_vjp_step_rows_loop_kernel<NORM, PATH, GT, 1, 2, 0>), dim3(la.grid),            \
+                               dim3(kVjpBlock), lds, st, lc, p, (const double2*)tables, hpc.ni, hpc.inv_w, hpc.x0,  \
+                               cd, co, B, la.ctl, la.plan);                                                 \
+    } while (0)
+    if (hlc.path == PATH_REC_CORR) {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_ALOOP(NORM_SOFTSIGN, PATH_REC_CORR, 10);
+        else if (hlc.G == 10) KAN_ALOOP(NORM_TANH_FAST, PATH_REC_CORR, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_ALOOP(NORM_SOFTSIGN, PATH_REC_CORR, 5);
+        else KAN_ALOOP(NORM_TANH_FAST, PATH_REC_CORR, 5);
+    } else {
+        if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_ALOOP(NORM_SOFTSIGN, PATH_REC, 10);
+        else if (hlc.G == 10) KAN_ALOOP(NORM_TANH_FAST, PATH_REC, 10);
+        else if (hlc.norm == NORM_SOFTSIGN) KAN_ALOOP(NORM_SOFTSIGN, PATH_REC, 5);
+        else KAN_ALOOP(NORM_TANH_FAST, PATH_REC, 5);
+    }
+#undef KAN_ALOOP
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(adj_finish_loop_kernel, dim3((unsigned)la.P + 1), dim3(kAdjFinBlock), 0, st, la);
     return hipGetLastError();
 }
 

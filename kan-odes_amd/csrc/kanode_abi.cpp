@@ -1389,8 +1389,8 @@ bool kanode_internal_fk_step_ok(const kanode_handle* h) {
            kan::fk_stage_pp_supported(h->hpc, (int)h->spec.nx) && h->fused_step;
 }
 bool kanode_internal_fk_loop_ok(const kanode_handle* h) { return h->fk_loop && kanode_internal_fk_step_ok(h); }
-kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t batch,
-                                           void* stream) {
+kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t lq,
+                                           int64_t batch, void* stream) {
     const hipStream_t st = (hipStream_t)stream;
     if (table_build(h, h->built_phi)) {
         const int fn_phi = kan::PP_PHI;
@@ -1399,7 +1399,7 @@ kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, cons
     const double dx2 = h->spec.dx * h->spec.dx;
     const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
     HIP_TRY(h, kan::launch_fk_step_pp_loop(h->hpc, h->hlc[0], h->dlc, cd, co, (int)h->spec.nx, (const double*)p,
-                                           h->dtable, *la, batch, kSlabBlocks, st, h->grid_ovr.rhs));
+                                           h->dtable, *la, lq, batch, st, h->grid_ovr.rhs));
     return KANODE_OK;
 }
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
@@ -1457,6 +1457,30 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
     if (e == hipErrorNotSupported) return KANODE_OK;
     if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_step: ") + hipGetErrorString(e));
     launched = true;
+    return KANODE_OK;
+}
+kanode_status kanode_internal_fk_adjoint_loop_geometry(kanode_handle* h, int64_t batch, void* stream, bool& ok,
+                                                      double** slab, int64_t* grid) {
+    ok = false;
+    const int P = h->hlc[0].G + (h->hlc[0].use_base ? 1 : 0);
+    if (!h->fk_loop || h->spec.dtype != KANODE_F64 || h->spec.rhs_kind != KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN ||
+        !h->pp_on || !h->fused_step || !kan::fk_adjoint_loop_supported(h->hpc, h->hlc[0], (int)h->spec.nx) ||
+        h->grid_ovr.vstep != 0 || !h->grid_ovr.vstep_rows || h->adj_fused_finish || P > KANODE_MAX_GRID + 1 ||
+        kan::fk_adjoint_loop_grid(batch, kSlabBlocks / 2) < 1)
+        return KANODE_OK;
+    if (kanode_status s = ensure_adjoint_slabs(h, (hipStream_t)stream); s != KANODE_OK) return s;
+    *slab = (double*)h->step_slab;
+    *grid = kan::fk_adjoint_loop_grid(batch, kSlabBlocks / 2);
+    ok = true;
+    return KANODE_OK;
+}
+kanode_status kanode_internal_fk_adjoint_loop(kanode_handle* h, const void* p, const kan::AdjLoopArgs* la,
+                                              int64_t batch, void* stream) {
+    const double dx2 = h->spec.dx * h->spec.dx;
+    const double cd = h->spec.diffusion * (-2.0 / dx2), co = h->spec.diffusion * (1.0 / dx2);
+    HIP_TRY(h, kan::launch_fk_adjoint_loop(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
+                                           (int)h->spec.nx, *la, batch, (hipStream_t)stream,
+                                           table_build(h, h->built_vjp)));
     return KANODE_OK;
 }
 kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, kan::AdjStepArgs* a, void* const* km,

@@ -17,6 +17,7 @@ struct ChainAdjointArgs;
 struct AdjStepArgs;
 struct PairAdjArgs;
 struct FkLoopArgs;
+struct AdjLoopArgs;
 }
 
 kanode_status kanode_internal_fail(kanode_handle* h, kanode_status s, const std::string& msg);
@@ -56,8 +57,14 @@ bool kanode_internal_fk_step_ok(const kanode_handle* h);
 // the device-controlled adaptive Fisher-KPP solve (KANODE_OPT_FK_DEVICE_LOOP): whether the handle takes it,
 // and one step attempt (builds the table first when the solve has not)
 bool kanode_internal_fk_loop_ok(const kanode_handle* h);
-kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t batch,
-                                           void* stream);
+// the adaptive adjoint's device loop (kan_adjloop.hpp): ok when the handle takes it for this batch, with the
+// rows step's slab base and grid (allocating the slabs); one attempt (rows + finish launches)
+kanode_status kanode_internal_fk_adjoint_loop_geometry(kanode_handle* h, int64_t batch, void* stream, bool& ok,
+                                                      double** slab, int64_t* grid);
+kanode_status kanode_internal_fk_adjoint_loop(kanode_handle* h, const void* p, const kan::AdjLoopArgs* la,
+                                              int64_t batch, void* stream);
+kanode_status kanode_internal_fk_step_loop(kanode_handle* h, const void* p, const kan::FkLoopArgs* la, int64_t lq,
+                                           int64_t batch, void* stream);
 kanode_status kanode_internal_fk_step(kanode_handle* h, const void* p, const void* u, const void* k1,
                                       void* const* kout, void* u_new, const double* a6x6, const double* e7,
                                       const double* q4x7, double abstol, double reltol, double* err_out,

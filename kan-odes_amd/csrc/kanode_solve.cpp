@@ -18,8 +18,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <initializer_list>
+#include <type_traits>
 #include <vector>
 
+#include "kan_adjloop.hpp"
 #include "kan_kernels.hpp"
 #include "kanode.h"
 #include "kanode_internal.hpp"
@@ -140,17 +142,26 @@ struct kanode_solution {
     // the device-controlled Fisher-KPP solve (solve_fk_loop): its state and host mirror, the error partials,
     // the device copy of the slot table (staged through pinned memory) and the step records
     struct Loop {
-        kan::FkLoopCtl* ctl = nullptr;
+        kan::FkLoopCtl* ctl = nullptr;     // [2]
         kan::FkLoopCtl* hmir = nullptr;    // pinned, mapped
         kan::FkLoopCtl* dmir = nullptr;    // its device address
-        kan::StepCoef* coef = nullptr;     // [2]
         double* parts = nullptr;
-        unsigned* arrive = nullptr;
         void** dslots = nullptr;
         void** hslots = nullptr;           // pinned
         double* ts = nullptr;              // [cap] then dts [cap]
         int64_t cap = 0, synced = 0;
     } loop;
+    // the device-controlled Fisher-KPP adjoint (adjoint_fk_loop): state, mirror, plans, host staging, tables
+    struct AdjLoop {
+        kan::AdjLoopCtl* ctl = nullptr;
+        kan::AdjLoopCtl* hmir = nullptr;   // pinned, mapped
+        kan::AdjLoopCtl* dmir = nullptr;
+        kan::AdjLoopPlan* plan = nullptr;  // [2]
+        void* hplan = nullptr;             // pinned staging: a plan and a state
+        unsigned* arrive = nullptr;
+        void* meta = nullptr;
+        size_t meta_bytes = 0;
+    } aloop;
     // adjoint scratch (sized on first use)
     void* adj = nullptr;
     size_t adj_bytes = 0;
@@ -192,10 +203,13 @@ struct kanode_solution {
         if (adj) (void)hipFree(adj);
         if (padj) (void)hipFree(padj);
         if (hs_dev) (void)hipFree(hs_dev);
-        for (void* q : {(void*)loop.ctl, (void*)loop.coef, (void*)loop.parts, (void*)loop.arrive, (void*)loop.dslots,
-                        (void*)loop.ts})
+        for (void* q : {(void*)loop.ctl, (void*)loop.parts, (void*)loop.dslots, (void*)loop.ts})
             if (q) (void)hipFree(q);
         for (void* q : {(void*)loop.hmir, (void*)loop.hslots})
+            if (q) (void)hipHostFree(q);
+        for (void* q : {(void*)aloop.ctl, (void*)aloop.plan, (void*)aloop.arrive, aloop.meta})
+            if (q) (void)hipFree(q);
+        for (void* q : {(void*)aloop.hmir, aloop.hplan})
             if (q) (void)hipHostFree(q);
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
         if (g.cap_stream) (void)hipStreamDestroy(g.cap_stream);
@@ -925,10 +939,9 @@ kanode_status solve_graph_t(kanode_handle* h, const void* p, const void* u0, dou
 
 // ---- the adaptive Fisher-KPP solve with the step control on the device ------------------------------
 // KANODE_OPT_FK_DEVICE_LOOP, control = auto, fp64 table path, dense output kept: solve_t's algorithm with every
-// step one launch of the step kernel's DEV instantiation (kan::FkLoopArgs): the launch reads the step size from
-// device memory and its last workgroup runs the controller, so the host queues launches ahead, kKeep batches
-// of kBatch, and only polls the mapped mirror of the state; the queue drains (launches return at once) after
-// the last step.  The saveat values come from the dense output afterwards (saveat_in_step, as solve_t).
+// attempt one launch of the step kernel's DEV instantiation (kan::FkLoopArgs): launch q decides attempt q - 1 at
+// its head (every workgroup, the same sums) and takes the next, so the host queues launches ahead in batches of
+// kBatch and only polls the mapped mirror of the state; launches queued past the end return at once.  The saveat values come from the dense output afterwards (saveat_in_step, as solve_t).
 // done = false when not covered (solve_t runs instead).
 kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, double t0, double tf,
                             const double* saveat, int64_t n_save, void* u_save, const kanode_solver_options& o,
@@ -956,10 +969,8 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
         L.cap = cap;
     }
     if (!L.ctl) {
-        SOLVE_TRY(dev_alloc(h, (void**)&L.ctl, sizeof(kan::FkLoopCtl), "loop state"));
-        SOLVE_TRY(dev_alloc(h, (void**)&L.coef, 2 * sizeof(kan::StepCoef), "loop coefficients"));
-        SOLVE_TRY(dev_alloc(h, (void**)&L.parts, kanode_internal_max_parts() * sizeof(double), "loop partials"));
-        SOLVE_TRY(dev_alloc(h, (void**)&L.arrive, 64, "loop counter"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.ctl, 2 * sizeof(kan::FkLoopCtl), "loop state"));
+        SOLVE_TRY(dev_alloc(h, (void**)&L.parts, 2 * kanode_internal_max_parts() * sizeof(double), "loop partials"));
         SOLVE_HIP(h, hipHostMalloc((void**)&L.hmir, sizeof(kan::FkLoopCtl), hipHostMallocMapped | hipHostMallocCoherent));
         SOLVE_HIP(h, hipHostGetDevicePointer((void**)&L.dmir, L.hmir, 0));
     }
@@ -969,7 +980,7 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
         SOLVE_HIP(h, hipMemcpyAsync((char*)u_save + si * sb, u0, sb, hipMemcpyDeviceToDevice, st));
         ++si;
     }
-    SOLVE_TRY(ensure_slots(h, s, 2, st));
+    SOLVE_TRY(ensure_slots(h, s, 3, st));
     s->qform = true;
     SOLVE_HIP(h, hipMemcpyAsync(s->u(0), u0, sb, hipMemcpyDeviceToDevice, st));
     kanode_stage s0{};
@@ -977,30 +988,24 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
     double dt = o.dt;
     if (!(o.dt > 0)) SOLVE_TRY(initdt<double>(h, s, p, s->u(0), s->k1_0, tf - t0, o, dt, st, s->q(0, 1)));
     SOLVE_HIP(h, hipStreamSynchronize(st));   // (the mirror is the init copy's source and the device's target)
-    kan::FkLoopCtl c0{};
+    kan::FkLoopCtl c0{};   // launch 0 reads state[1]: no attempt pending
     c0.t = t0;
-    c0.dt = std::min(dt, tf - t0);
+    c0.dt = dt;
     c0.qold = o.qoldinit;
+    c0.cand[1] = s->slots[0];
+    c0.cand[2] = s->slots[1];
+    c0.cand[3] = s->slots[2];
     *L.hmir = c0;
-    SOLVE_HIP(h, hipMemcpyAsync(L.ctl, L.hmir, sizeof(c0), hipMemcpyHostToDevice, st));
-    kan::StepCoef k0{};   // the first attempt's coefficients (fk_loop_coef's products, formed here)
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j <= i; ++j) k0.a[i][j] = c0.dt * TA[i][j];
-    for (int j = 0; j < 7; ++j) k0.e[j] = c0.dt * BT[j];
-    for (int m = 0; m < 4; ++m)
-        for (int i = 0; i < 7; ++i) k0.q[m][i] = c0.dt * RI[i][m];
-    SOLVE_HIP(h, hipMemcpy(L.coef, &k0, sizeof(k0), hipMemcpyHostToDevice));
-    SOLVE_HIP(h, hipMemsetAsync(L.arrive, 0, sizeof(unsigned), st));
+    SOLVE_HIP(h, hipMemcpy(L.ctl + 1, &c0, sizeof(c0), hipMemcpyHostToDevice));
     kan::FkLoopArgs la{};
-    la.ctl = L.ctl;
+    la.state = L.ctl;
     la.mirror = L.dmir;
-    la.coef = L.coef;
     la.slots = L.dslots;
     la.k1_0 = (const double*)s->k1_0;
     la.ts = L.ts;
     la.dts = L.ts + L.cap;
     la.parts = L.parts;
-    la.arrive = L.arrive;
+    la.max_grid = kanode_internal_max_parts();
     la.n = s->n;
     la.tf = tf;
     la.abstol = o.abstol;
@@ -1016,10 +1021,11 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
     const volatile kan::FkLoopCtl* mir = L.hmir;
     int64_t queued = 0;
     for (;;) {
-        if (queued + kBatch + 2 > L.cap)
+        if (queued + kBatch + 3 > L.cap)
             return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device loop): step table full");
-        // slots for every step the queued launches can take (each launch advances at most one step)
-        SOLVE_TRY(ensure_slots(h, s, queued + kBatch + 2, st));
+        // slots for every step the queued launches can reach (each launch advances at most one step; a state
+        // names the slots up to its step + 2)
+        SOLVE_TRY(ensure_slots(h, s, queued + kBatch + 3, st));
         const int64_t ns = (int64_t)s->slots.size();
         if (L.synced < ns) {
             std::memcpy(L.hslots + L.synced, s->slots.data() + L.synced, (ns - L.synced) * sizeof(void*));
@@ -1027,10 +1033,12 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
                                         hipMemcpyHostToDevice, st));
             L.synced = ns;
         }
-        for (int64_t i = 0; i < kBatch; ++i) SOLVE_TRY(kanode_internal_fk_step_loop(h, p, &la, s->batch, st));
+        for (int64_t i = 0; i < kBatch; ++i)
+            SOLVE_TRY(kanode_internal_fk_step_loop(h, p, &la, queued + i, s->batch, st));
         queued += kBatch;
-        // keep one batch queued behind the running one: wait until the device has taken the previous batch
-        for (uint64_t it = 1; mir->status == 0 && mir->it < queued - kBatch; ++it) {
+        // keep one batch queued behind the running one: wait until the device has decided the previous batch's
+        // attempts (launch q decides attempt q - 1)
+        for (uint64_t it = 1; mir->status == 0 && mir->it + 1 < queued - kBatch; ++it) {
             if ((it & 255) == 0) {
                 const hipError_t q = hipStreamQuery(st);
                 if (q == hipSuccess) break;
@@ -1039,7 +1047,7 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
             __builtin_ia32_pause();
         }
         if (mir->status != 0) break;
-        if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it < queued - kBatch)
+        if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it + 1 < queued - kBatch)
             return kanode_internal_fail(h, KANODE_ERR_HIP, "Tsit5 (device loop): the stream drained without progress");
     }
     SOLVE_HIP(h, hipStreamSynchronize(st));
@@ -1059,6 +1067,190 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
         stats->nf = 6 * c.it + 1;
     }
     done = true;
+    return KANODE_OK;
+}
+
+// ---- the adaptive Fisher-KPP adjoint with its step control on the device (kan_adjloop.hpp) ----------------
+// adjoint_t's loop for the combined adaptive rows step (KANODE_OPT_FK_DEVICE_LOOP): one attempt = the rows
+// launch + the finish launch, whose last workgroup runs the controller and plans the next attempt; the host
+// queues attempts in batches and only polls the mapped mirror of the state.  A step landing on a saveat stop
+// pauses the loop: the host drains the stream, takes the stop (take_stop: the jump and the FSAL
+// re-evaluation, as its own loop), plans the next attempt and resumes.  On return the loop's variables hold
+// adjoint_t's values at its end.
+template <class TakeStop>
+kanode_status adjoint_fk_loop(kanode_handle* h, const void* p, kanode_solution* s, const kanode_solver_options& o,
+                              const std::vector<double>& stops, double* slab, int64_t grid, void* const* lam,
+                              void* const* kl, void* const* mu, void* const* km, double& hstep, double& qold,
+                              double& tau, size_t& si, int64_t& naccept, int64_t& nreject, int64_t& it, int64_t& nf,
+                              int& lcur, int& mcur, std::vector<double>* hrec, TakeStop& take_stop, hipStream_t st) {
+    constexpr int64_t kBatch = 16;
+    const int64_t nsteps = (int64_t)s->ts.size(), P = kanode_param_length(h), nst = (int64_t)stops.size();
+    auto& A = s->aloop;
+    // device copies: forward slot table | ts | dts | stops, then the error terms [1 + P]
+    const size_t meta = (size_t)(3 * nsteps + nst + 1 + P + 8) * sizeof(double);
+    if (A.meta_bytes < meta) {
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        if (A.meta) (void)hipFree(A.meta);
+        A.meta = nullptr;
+        A.meta_bytes = 0;
+        SOLVE_TRY(dev_alloc(h, &A.meta, meta, "adjoint loop tables"));
+        A.meta_bytes = meta;
+    }
+    if (!A.ctl) {
+        SOLVE_TRY(dev_alloc(h, (void**)&A.ctl, sizeof(kan::AdjLoopCtl), "adjoint loop state"));
+        SOLVE_TRY(dev_alloc(h, (void**)&A.plan, 2 * sizeof(kan::AdjLoopPlan), "adjoint loop plans"));
+        SOLVE_TRY(dev_alloc(h, (void**)&A.arrive, 64, "adjoint loop counter"));
+        SOLVE_HIP(h, hipHostMalloc((void**)&A.hmir, sizeof(kan::AdjLoopCtl), hipHostMallocMapped | hipHostMallocCoherent));
+        SOLVE_HIP(h, hipHostGetDevicePointer((void**)&A.dmir, A.hmir, 0));
+        SOLVE_HIP(h, hipHostMalloc((void**)&A.hplan, sizeof(kan::AdjLoopPlan) + sizeof(kan::AdjLoopCtl)));
+    }
+    void** dslots = (void**)A.meta;
+    double* dts_ = (double*)A.meta + nsteps;   // [ts | dts]
+    double* dstops = dts_ + 2 * nsteps;
+    double* dout = dstops + nst;
+    {
+        std::vector<char> host((3 * nsteps + nst) * sizeof(double));
+        std::memcpy(host.data(), s->slots.data(), nsteps * sizeof(void*));
+        std::memcpy(host.data() + nsteps * sizeof(double), s->ts.data(), nsteps * sizeof(double));
+        std::memcpy(host.data() + 2 * nsteps * sizeof(double), s->dts.data(), nsteps * sizeof(double));
+        std::memcpy(host.data() + 3 * nsteps * sizeof(double), stops.data(), nst * sizeof(double));
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        SOLVE_HIP(h, hipMemcpy(A.meta, host.data(), host.size(), hipMemcpyHostToDevice));
+    }
+    SOLVE_HIP(h, hipMemsetAsync(A.arrive, 0, sizeof(unsigned), st));
+    kan::AdjLoopArgs la{};
+    la.ctl = A.ctl;
+    la.mirror = A.dmir;
+    la.plan = A.plan;
+    la.arrive = A.arrive;
+    for (int i = 0; i < 2; ++i) {
+        la.lam[i] = (double*)lam[i];
+        la.mu[i] = (double*)mu[i];
+    }
+    for (int j = 0; j < 7; ++j) {
+        la.kl[j] = (double*)kl[j];
+        la.km[j] = (double*)km[j];
+    }
+    la.slots = dslots;
+    la.fts = dts_;
+    la.fdts = dts_ + nsteps;
+    la.nsteps = nsteps;
+    la.slab = slab;
+    la.grid = grid;
+    la.P = P;
+    la.n = s->n;
+    la.out = dout;
+    la.stops = dstops;
+    la.nstops = nst;
+    la.tf = s->tf;
+    la.TT = s->tf - s->t0;
+    la.abstol = o.abstol;
+    la.reltol = o.reltol;
+    la.dtmin = o.dtmin;
+    la.beta1 = o.beta1;
+    la.beta2 = o.beta2;
+    la.gamma = o.gamma;
+    la.qmin = o.qmin;
+    la.qmax = o.qmax;
+    la.qoldinit = o.qoldinit;
+    la.ntot = (double)(s->n + P);
+    la.maxiters = o.maxiters;
+    if (hrec) {
+        const int64_t cap = 4 * nsteps + 1024;
+        if (s->hs_cap < cap) {
+            if (s->hs_dev) SOLVE_HIP(h, hipFree(s->hs_dev));
+            s->hs_dev = nullptr;
+            s->hs_cap = 0;
+            SOLVE_HIP(h, hipMalloc((void**)&s->hs_dev, (size_t)cap * sizeof(double)));
+            s->hs_cap = cap;
+        }
+        la.hs = s->hs_dev;
+        la.hs_cap = s->hs_cap;
+    }
+    // the host's view of the forward steps for the plans it builds (the same values as the device's)
+    struct HostFw {
+        const kanode_solution* s;
+        double ts(int64_t i) const { return s->ts[i]; }
+        double dts(int64_t i) const { return s->dts[i]; }
+        const void* slot(int64_t i) const { return s->u(i); }
+    } hfw{s};
+    kan::AdjLoopCtl c{};
+    c.tau = tau;
+    c.h = hstep;
+    c.qold = qold;
+    c.si = (int64_t)si;
+    c.naccept = naccept;
+    c.nreject = nreject;
+    c.it = it;
+    c.nf = nf;
+    c.fi = nsteps - 1;
+    c.lc = lcur;
+    c.mc = mcur;
+    c.fs = 0;
+    const volatile kan::AdjLoopCtl* mir = A.hmir;
+    for (;;) {
+        // (re)start at c: the loop top, the attempt's plan, the state (the stream is drained: the staging is free)
+        kan::adj_loop_top(la, c);
+        if (c.status != 0) break;
+        kan::AdjLoopPlan* hp = (kan::AdjLoopPlan*)A.hplan;
+        kan::adj_loop_plan(la, c, *hp, hfw);
+        std::memcpy((char*)A.hplan + sizeof(kan::AdjLoopPlan), &c, sizeof(c));
+        *A.hmir = c;
+        SOLVE_HIP(h, hipMemcpyAsync(A.plan + (c.it & 1), hp, sizeof(kan::AdjLoopPlan), hipMemcpyHostToDevice, st));
+        SOLVE_HIP(h, hipMemcpyAsync(A.ctl, (char*)A.hplan + sizeof(kan::AdjLoopPlan), sizeof(c), hipMemcpyHostToDevice,
+                                    st));
+        const int64_t base = c.it;
+        int64_t queued = 0;
+        for (;;) {
+            for (int64_t i = 0; i < kBatch; ++i) SOLVE_TRY(kanode_internal_fk_adjoint_loop(h, p, &la, s->batch, st));
+            queued += kBatch;
+            for (uint64_t k = 1; mir->status == 0 && mir->it < base + queued - kBatch; ++k) {
+                if ((k & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(st);
+                    if (q == hipSuccess) break;
+                    if (q != hipErrorNotReady) SOLVE_HIP(h, q);
+                }
+                __builtin_ia32_pause();
+            }
+            if (mir->status != 0) break;
+            if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it < base + queued - kBatch)
+                return kanode_internal_fail(h, KANODE_ERR_HIP, "adjoint Tsit5 (device loop): the stream drained without progress");
+        }
+        SOLVE_HIP(h, hipStreamSynchronize(st));
+        c = *(const kan::AdjLoopCtl*)A.hmir;
+        if (c.status != 3) break;
+        // paused on stops[si]: the stop's jump and FSAL re-evaluation on the host, then the next stop
+        tau = c.tau;
+        si = (size_t)c.si;
+        lcur = c.lc;
+        nf = c.nf;
+        SOLVE_TRY(take_stop(c.fs ? kl[6] : kl[0], c.fs ? km[6] : km[0]));
+        SOLVE_TRY(kanode_internal_vjp_flush(h, st));
+        c.lc = lcur;
+        c.si = (int64_t)si;
+        c.nf = nf;
+        c.status = 0;
+    }
+    if (c.status == 2) {
+        it = o.maxiters;   // (adjoint_t reports it)
+        tau = c.tau;
+        return KANODE_OK;
+    }
+    tau = c.tau;
+    hstep = c.h;
+    qold = c.qold;
+    si = (size_t)c.si;
+    naccept = c.naccept;
+    nreject = c.nreject;
+    it = c.it;
+    nf = c.nf;
+    lcur = c.lc;
+    mcur = c.mc;
+    if (hrec && la.hs) {
+        hrec->resize((size_t)std::min(naccept, la.hs_cap));
+        if (!hrec->empty())
+            SOLVE_HIP(h, hipMemcpy(hrec->data(), la.hs, hrec->size() * sizeof(double), hipMemcpyDeviceToHost));
+    }
     return KANODE_OK;
 }
 
@@ -1206,7 +1398,52 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     int64_t naccept = 0, nreject = 0, it = 0;
     std::vector<double>* hrec = kanode_internal_adjoint_steps(h);
     if (hrec) hrec->clear();
-    for (; it < o.maxiters; ++it) {
+    // A step that landed on stops[si] (tau == stops[si]): the saveat jump there, if any, and the next stop.
+    // k0l / k0m: the current kλ_1 / kμ_1 buffers (the FSAL re-evaluation's outputs).
+    auto take_stop = [&](void* k0l, void* k0m) -> kanode_status {
+        const double tsv = tf - tau;
+        Jump* key = nullptr;
+        for (auto& jm : jumps)
+            if (jm.live && (!key || std::fabs(jm.ts - tsv) < std::fabs(key->ts - tsv))) key = &jm;
+        if (key && std::fabs(key->ts - tsv) <= eps && si + 1 < stops.size()) {
+            if (key->rows.size() <= (size_t)KANODE_MAX_STAGES) {
+                // callback λ += ∂L/∂u(t_j) and the FSAL re-evaluation (u_modified!) as ONE adjoint
+                // stage: λs = λ + Σ_r 1·g_r (the lincombs' fma order) -> λ_new, kλ_1 = λsᵀJ at λs
+                void* g[KANODE_MAX_STAGES];
+                double ones[KANODE_MAX_STAGES];
+                int ng = 0;
+                for (int64_t r : key->rows) {
+                    g[ng] = (char*)dl_du + r * sb;
+                    ones[ng++] = 1.0;
+                }
+                key->live = false;
+                // (deferred where the surrogate pair's stages run lazily: its second launch then runs
+                // together with the next step's first stage, whose λs starts from this kλ_1)
+                SOLVE_TRY(adj_rhs(tau, lam[lcur], ng, g, ones, k0l, k0m, lam[lcur ^ 1], nullptr, nullptr,
+                                  kanode_internal_pair_lazy(h)));
+                lcur ^= 1;
+            } else {
+                SOLVE_TRY(add_jump(*key, lam[lcur]));                   // callback: λ += ∂L/∂u(t_j)
+                SOLVE_TRY(adj_rhs(tau, lam[lcur], 0, nullptr, nullptr, k0l, k0m, nullptr, nullptr, nullptr));
+            }
+            ++nf;                                                      // u_modified!: FSAL re-evaluated
+        }
+        si = std::min(si + 1, stops.size() - 1);
+        return KANODE_OK;
+    };
+    bool dev_loop = false;
+    if constexpr (std::is_same<T, double>::value) {
+        if (s->qform && o.adaptive && o.control == 0 && !capturing(st) && s->record) {
+            double* lslab = nullptr;
+            int64_t lgrid = 0;
+            SOLVE_TRY(kanode_internal_fk_adjoint_loop_geometry(h, s->batch, st, dev_loop, &lslab, &lgrid));
+            if (dev_loop) {
+                SOLVE_TRY(adjoint_fk_loop(h, p, s, o, stops, lslab, lgrid, lam, kl, mu, km, hstep, qold, tau, si,
+                                          naccept, nreject, it, nf, lcur, mcur, hrec, take_stop, st));
+            }
+        }
+    }
+    for (; !dev_loop && it < o.maxiters; ++it) {
         if (tau >= TT - 1e-14 * std::max(1.0, TT)) break;
         hstep = std::min(hstep, stops[si] - tau);
         bool fused_step = false;   // Fisher-KPP table path, Q-form dense output: the six stages in one launch
@@ -1336,34 +1573,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         ++naccept;
         if (std::fabs(tau - stops[si]) <= 1e-12 * std::max(1.0, TT)) {
             tau = stops[si];
-            const double tsv = tf - tau;
-            Jump* key = nullptr;
-            for (auto& jm : jumps)
-                if (jm.live && (!key || std::fabs(jm.ts - tsv) < std::fabs(key->ts - tsv))) key = &jm;
-            if (key && std::fabs(key->ts - tsv) <= eps && si + 1 < stops.size()) {
-                if (key->rows.size() <= (size_t)KANODE_MAX_STAGES) {
-                    // callback λ += ∂L/∂u(t_j) and the FSAL re-evaluation (u_modified!) as ONE adjoint
-                    // stage: λs = λ + Σ_r 1·g_r (the lincombs' fma order) -> λ_new, kλ_1 = λsᵀJ at λs
-                    void* g[KANODE_MAX_STAGES];
-                    double ones[KANODE_MAX_STAGES];
-                    int ng = 0;
-                    for (int64_t r : key->rows) {
-                        g[ng] = (char*)dl_du + r * sb;
-                        ones[ng++] = 1.0;
-                    }
-                    key->live = false;
-                    // (deferred where the surrogate pair's stages run lazily: its second launch then runs
-                    // together with the next step's first stage, whose λs starts from this kλ_1)
-                    SOLVE_TRY(adj_rhs(tau, lam[lcur], ng, g, ones, kl[0], km[0], lam[lcur ^ 1], nullptr, nullptr,
-                                      kanode_internal_pair_lazy(h)));
-                    lcur ^= 1;
-                } else {
-                    SOLVE_TRY(add_jump(*key, lam[lcur]));                   // callback: λ += ∂L/∂u(t_j)
-                    SOLVE_TRY(adj_rhs(tau, lam[lcur], 0, nullptr, nullptr, kl[0], km[0], nullptr, nullptr, nullptr));
-                }
-                ++nf;                                                      // u_modified!: FSAL re-evaluated
-            }
-            si = std::min(si + 1, stops.size() - 1);
+            SOLVE_TRY(take_stop(kl[0], km[0]));
         }
         hstep = hnew;
     }

@@ -104,6 +104,8 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
         mx = max(d1, d2)
         h1 = max(1e-6, h0 * 1e-3) if mx <= 1e-15 else (0.01 / mx) ** (1.0 / 5.0)
         h = min(100 * h0, h1, T)
+    elif opt.replay_adjoint_dts is not None:
+        h = float(opt.replay_adjoint_dts[0])
     else:
         h = opt.dt
     qold = opt.qoldinit
@@ -114,6 +116,8 @@ def interpolating_adjoint(f, p: torch.Tensor, rec: DenseRecord, tspan, saveat, g
     for _ in range(opt.maxiters):
         if tau >= T - 1e-14 * max(1.0, T):
             break
+        if opt.replay_adjoint_dts is not None and not opt.adaptive:
+            h = float(opt.replay_adjoint_dts[naccept])
         h = min(h, stops[si] - tau)
         kl, km = [k1l], [k1m]
         sumsq = None

@@ -91,6 +91,10 @@ class Tsit5Options:
     native: bool = True                # run the loop in libkanode (kanode_solve_tsit5) when f is a kanode RHS
     control: str = "auto"              # native step control: "host", "device" (hipGraph replay) or "auto"
     graph_steps: int = 16              # step slots per graph replay (device control)
+    # tests (Python driver, adaptive=False): take these accepted step sizes, in order, instead of a fixed dt --
+    # another solver's step sequence replayed, so its arithmetic is compared on the same grid
+    replay_dts: tuple | None = None
+    replay_adjoint_dts: tuple | None = None
 
     def to_c(self):
         from . import _lib as L
@@ -211,6 +215,8 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
     k1 = f(u, p, t)
     if opt.adaptive:
         dt = opt.dt if opt.dt is not None else _initdt(f, u0, p, t0, tf - t0, opt, k1)
+    elif opt.replay_dts is not None:
+        dt = float(opt.replay_dts[0])
     else:
         if opt.dt is None:
             raise ValueError("fixed-step Tsit5 needs opt.dt")
@@ -221,6 +227,8 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
     for _ in range(opt.maxiters):
         if t >= tf - 1e-14 * max(1.0, abs(tf)):
             break
+        if opt.replay_dts is not None and not opt.adaptive:
+            dt = float(opt.replay_dts[naccept])
         dt = min(dt, tf - t)
         if fused:
             unew, ks, EEst = _step_fused(f, u, p, t, dt, k1, opt)

@@ -115,3 +115,23 @@ def test_trainer_uses_interpolating_adjoint_by_default():
     for _ in range(5):
         l1 = tr.step()
     assert l1 < l0
+
+
+def test_replayed_step_sequences_reproduce_the_adaptive_run():
+    """Tsit5Options.replay_dts / replay_adjoint_dts (the GPU surrogate test replays the GPU's accepted steps on
+    the oracle): replaying an adaptive run's own forward and adjoint step sizes with adaptive=False takes the
+    same steps and gives the same solution and gradients bitwise (the saveat stops land as before)."""
+    specs = [O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")]
+    f = OracleChainRHS(specs)
+    p0 = torch.as_tensor(np.random.default_rng(2).uniform(-0.3, 0.3, 240))
+    u0 = torch.tensor([[1.0, 1.0]], dtype=torch.float64)
+    ts = [0.0, 0.35, 1.0, 1.7, 2.0]
+    w = torch.as_tensor(np.random.default_rng(3).normal(size=(len(ts), 1, 2)))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8)
+    ga, gua, sa = grads(f, u0, p0, (0.0, 2.0), ts, w, opt, "interpolating_adjoint")
+    rep = kanode.Tsit5Options(abstol=1e-8, reltol=1e-8, adaptive=False, replay_dts=tuple(sa.stats["dts"]),
+                              replay_adjoint_dts=tuple(sa.stats["adjoint"]["dts"]))
+    gr, gur, sr = grads(f, u0, p0, (0.0, 2.0), ts, w, rep, "interpolating_adjoint")
+    assert sr.stats["dts"] == sa.stats["dts"] and sr.stats["adjoint"]["dts"] == sa.stats["adjoint"]["dts"]
+    assert len(sa.stats["adjoint"]["dts"]) == sa.stats["adjoint"]["naccept"] > 5
+    assert torch.equal(sr.u, sa.u) and torch.equal(gr, ga) and torch.equal(gur, gua)
