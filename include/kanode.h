@@ -304,11 +304,15 @@ kanode_status kanode_vjp(kanode_handle* h, const void* p, const void* u, const v
  *     graph is cached in the kanode_solution.  Opt-in (it rarely pays on ROCm 7.2).
  *   control = auto: a chain of small layers (<= 16 wide) with <= 16 trajectories runs
  *     the whole solve in ONE workgroup (controller, saveat and dense output on the
- *     device), and with its dense output kept the whole adjoint too; everything else
- *     runs as control = host.  On the Fisher-KPP table path (fp64, Nx = 128/256/512)
- *     the host loop issues one launch per Tsit5 step (all six stages per trajectory
- *     row) and keeps the dense output as u_n and the interpolation polynomials Q_1..Q_4
- *     (plus k_7), and the adjoint issues one launch per step.
+ *     device), and with its dense output kept the whole adjoint too (one Lotka-Volterra
+ *     trajectory: the adjoint on one wave); so does a Fisher-KPP field of <= 64 points
+ *     (even Nx, <= 16 trajectories, rbf basis, G = 5 or 10, softsign / tanh_fast: one wave
+ *     per trajectory, the pointwise KAN from the tables).  On the Fisher-KPP table path at
+ *     Nx = 128/256/512 (fp64) each Tsit5 step is one launch (all six stages per trajectory
+ *     row), the dense output is kept as u_n and the interpolation polynomials Q_1..Q_4
+ *     (plus k_7), and the adjoint step is one launch (+ its finish); adaptive solves with
+ *     the dense output kept run their step control on the device
+ *     (KANODE_OPT_FK_DEVICE_LOOP).  Everything else runs as control = host.
  * kanode_adjoint_tsit5 is SciMLSensitivity 7.69's InterpolatingAdjoint (the NeuralODE
  * default; the reference's gradients): the adjoint ODE [λ; μ] integrated backward
  * with Tsit5 at the same tolerances, u(t) from the forward dense output, λ += ∂L/∂u

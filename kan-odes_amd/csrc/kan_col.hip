@@ -1308,6 +1308,11 @@ __device__ __forceinline__ T lane_read(T v, int l) {   // v of lane l (l uniform
         return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
     }
 }
+template <typename T>
+__device__ __forceinline__ T wave_sum_rows(T v) {   // Σ over the wave (all lanes): DPP row sums, then the rows
+    v = row16_sum(v);
+    return (lane_read(v, 0) + lane_read(v, 16)) + (lane_read(v, 32) + lane_read(v, 48));
+}
 struct LvWaveShape {
     static constexpr int I = 2, H = 10, O = 2, G = 5, per = G + 1, F1 = I * per, F2 = H * per;
 };
@@ -1363,7 +1368,7 @@ struct LvWaveModel {
         T f1, p1, d1, f2, p2, d2;
         const T h = layer1(y, f1, p1, d1);
         layer2(h, f2, p2, d2);
-        const T y0 = wave_sum(c2c[0] * f2), y1 = wave_sum(c2c[1] * f2);
+        const T y0 = wave_sum_rows(c2c[0] * f2), y1 = wave_sum_rows(c2c[1] * f2);
         return lane == 0 ? y0 : (lane == 1 ? y1 : T(0));
     }
     __device__ T vjp(T y, T ls, T* __restrict__ km) {
@@ -1460,7 +1465,7 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
         hlcs[1].O == LvWaveShape::O && hlcs[0].G == LvWaveShape::G && hlcs[1].G == LvWaveShape::G &&
         hlcs[0].basis == BASIS_RBF && hlcs[1].basis == BASIS_RBF &&
         (hlcs[0].norm == NORM_TANH_FAST || hlcs[0].norm == NORM_SOFTSIGN)) {
-        const size_t pre = 2 * sizeof(LayerConst) + sizeof(T) * (size_t)P * 9;
+        const size_t pre = 2 * sizeof(LayerConst) + sizeof(T) * (size_t)P * 10;   // ps, μ [2], kμ [7]
         size_t lds = pre + 2 * sizeof(double) * a.nsteps;
         const size_t rec = sizeof(T) * ((size_t)a.nsteps * 7 + 1) * LvWaveShape::I;
         const int stage_rec = lds + rec <= 60 * 1024 ? 1 : 0;

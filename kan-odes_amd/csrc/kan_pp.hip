@@ -1397,6 +1397,8 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     // DEV: the attempt's coefficients in LDS (published by the table staging's barrier below)
     __shared__ StepCoef lsc[1];
     __shared__ double lsum;
+    // the table's loads first: under DEV they overlap the state and partials loads of the decision
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     if constexpr (DEV) {
         FkLoopCtl c;
         if (!fk_loop_decide(la, lq, c, red, &lsum)) return;   // the solve has ended: a launch queued ahead
@@ -1417,7 +1419,6 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     auto ce = [&](int j) { return DEV ? lsc[0].e[j] : sc.e[j]; };                     // dt·btilde_j
     auto cq = [&](int m, int i) { return DEV ? lsc[0].q[m][i] : sc.q[m][i]; };        // dt·RI[i][m]
     const double abstol = DEV ? la.abstol : sc.abstol, reltol = DEV ? la.reltol : sc.reltol;
-    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
