@@ -1194,21 +1194,24 @@ struct AdjFwWindow {
 };
 
 // The finish launch of an attempt: each workgroup runs its block of adj_finish_kernel (the error terms by
-// agent-scope stores), then counts itself in; the last to arrive sums the terms in adjoint_t's order, applies
-// its PI controller (thread 0) and plans the next attempt into LDS, which the whole workgroup then stores.
-// Every workgroup stages the forward-step window and reads the state at its start, so the controller's
-// inputs are on chip when the last one arrives (its only wait is the terms' round trip).
+// agent-scope stores), then counts itself in; the last to arrive sums the terms in adjoint_t's order and
+// thread 0 applies its PI controller.  The next attempt's plan differs from the current one only in its
+// step-dependent fields (the host wrote the rest into both buffers, kan_adjloop.hpp adj_loop_plan): those the
+// workgroup's threads write in parallel, stage s's forward-step search on thread s.  Every workgroup stages
+// the forward-step window and reads the state at its start, so the controller's inputs are on chip when the
+// last one arrives.  The host's mirror is written when the state needs it (a stop, the end) and every 8
+// attempts (the host's queue refill reads the attempt count from it).
 constexpr int kAdjMaxTerms = kMaxGrid + 2;   // 1 + P, P <= G + 1
 __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopArgs la) {
+    using K = Tsit5Tab;
     __shared__ double red[(kAdjFinBlock / kWave) * 6];
     __shared__ double sums[6];
     __shared__ double wts[kAdjWin], wdts[kAdjWin];
     __shared__ void* wsl[kAdjWin];
     __shared__ double terms[kAdjMaxTerms];
     __shared__ unsigned arr;
-    __shared__ AdjLoopPlan lp;
-    __shared__ int go;
-    __shared__ int64_t nit;   // the planned attempt's index (thread 0's state)
+    __shared__ AdjLoopCtl cs;   // the state after the decision
+    __shared__ int64_t fis[6];
     const AdjLoopCtl* cp = la.ctl;
     if (cp->status != 0) return;
     AdjLoopCtl c = *cp;
@@ -1258,23 +1261,58 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
             }
         }
         if (c.status == 0) adj_loop_top(la, c);
-        go = c.status == 0;
-        nit = c.it;
-        if (go) {
-            const AdjFwWindow fw{wts, wdts, wsl, w0, wn, la.fts, la.fdts, la.slots};
-            adj_loop_plan(la, c, lp, fw);
-        }
-        *la.ctl = c;
-        *la.mirror = c;
-        __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cs = c;
     }
     __syncthreads();
-    if (go) {   // the plan, 8 bytes per thread (the next launches read it after this one ends)
-        constexpr int nw = sizeof(AdjLoopPlan) / sizeof(uint64_t);
-        static_assert(sizeof(AdjLoopPlan) % sizeof(uint64_t) == 0, "plan words");
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(&lp);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(la.plan + (nit & 1));
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+    c = cs;
+    const int t = threadIdx.x;
+    if (c.status == 0) {   // the next attempt's step-dependent fields
+        AdjLoopPlan& pl = la.plan[c.it & 1];
+        AdjStepArgs& a = pl.a;
+        const double h = c.h, tau = c.tau;
+        if (t < 6) {
+            const double ts = la.tf - (t == 5 ? tau + h : tau + K::TC[t] * h);
+            const AdjFwWindow fw{wts, wdts, wsl, w0, wn, la.fts, la.fdts, la.slots};
+            const int64_t fi = adj_loop_interval(fw, la.nsteps, ts, c.fi);
+            const double r = (ts - fw.ts(fi)) / fw.dts(fi);
+            const double th = r < 0.0 ? 0.0 : (r > 1.0 ? 1.0 : r);
+            const double* su = static_cast<const double*>(fw.slot(fi));
+            a.su_u[t] = su;
+            for (int m = 0; m < 4; ++m) a.su_q[t][m] = su + (m + 1) * la.n;
+            a.su_c[t][0] = th;
+            a.su_c[t][1] = th * th;
+            a.su_c[t][2] = th * th * th;
+            a.su_c[t][3] = th * th * th * th;
+            fis[t] = fi;
+        } else if (t < 42) {
+            const int ii = (t - 6) / 6, jj = (t - 6) % 6;
+            a.a[ii][jj] = jj <= ii ? h * K::TA[ii][jj] : 0.0;
+        } else if (t < 49) {
+            a.ec[t - 42] = h * K::BT[t - 42];
+        } else if (t == 49) {
+            a.kl[0] = c.fs ? la.kl[6] : la.kl[0];
+            a.kl[6] = c.fs ? la.kl[0] : la.kl[6];
+            a.lam = la.lam[c.lc];
+            a.lam_out = la.lam[c.lc ^ 1];
+            AdjFinish& f = pl.f;
+            f.a0 = h * K::TA[5][0];
+            f.e0 = h * K::BT[0];
+            f.mu = la.mu[c.mc];
+            f.mu_new = la.mu[c.mc ^ 1];
+            f.km1 = c.fs ? la.km[6] : la.km[0];
+            f.km7 = c.fs ? la.km[0] : la.km[6];
+        }
+        __syncthreads();
+        if (t == 0) {
+            a.reload[0] = 1;
+            for (int q = 1; q < 6; ++q) a.reload[q] = fis[q] == fis[q - 1] ? 0 : 1;   // (same slot: same u_i, Q_m)
+            c.fi = fis[5];
+        }
+    }
+    if (t == 0) {
+        *la.ctl = c;
+        if (c.status != 0 || (c.it & 7) == 0) *la.mirror = c;
+        __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1378,7 +1416,7 @@ __device__ __forceinline__ bool fk_loop_decide(const FkLoopArgs& la, int64_t q, 
         FkLoopCtl o = c;
         if (o.status == 0) o.cand[3] = la.slots[o.step + 2];
         *out = o;
-        *la.mirror = o;
+        if (o.status != 0 || (o.it & 7) == 0) *la.mirror = o;   // (the host's queue refill reads it; 1 in 8)
     }
     return c.status == 0;
 }
@@ -1399,6 +1437,29 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     __shared__ double lsum;
     // the table's loads first: under DEV they overlap the state and partials loads of the decision
     for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    // DEV: this wave's first row is loaded before the decision, for the attempt it will most likely take
+    // (the previous one accepted: the next step's u and k_1); a rejection reloads it below
+    const int64_t b0 = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const double* su_spec = nullptr;
+    const double* sk_spec = nullptr;
+    kd2 us0[NP], ks0[NP];
+    if constexpr (DEV) {
+        const FkLoopCtl* sp = la.state + ((lq + 1) & 1);
+        if (sp->status == 0) {
+            const int64_t st0 = sp->step;
+            su_spec = static_cast<const double*>(sp->pending ? sp->cand[2] : sp->cand[1]);
+            sk_spec = sp->pending ? static_cast<const double*>(sp->cand[1]) + 5 * la.n
+                                  : (st0 == 0 ? la.k1_0 : static_cast<const double*>(sp->cand[0]) + 5 * la.n);
+            if (b0 < B) {
+                const int64_t rb = b0 * Nx + 2 * (threadIdx.x & (kWave - 1));
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    us0[k] = ld_fstep(su_spec + rb + 128 * k);
+                    ks0[k] = ld_fstep(sk_spec + rb + 128 * k);
+                }
+            }
+        }
+    }
     if constexpr (DEV) {
         FkLoopCtl c;
         if (!fk_loop_decide(la, lq, c, red, &lsum)) return;   // the solve has ended: a launch queued ahead
@@ -1426,13 +1487,21 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     const bool want_err = err_slab != nullptr;
     const int64_t rstride = (int64_t)gridDim.x * (kBlock / kWave);
     double eacc = 0.0;
-    for (int64_t b = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6); b < B; b += rstride) {
+    for (int64_t b = b0; b < B; b += rstride) {
         const int64_t rb = b * Nx + 2 * lane;
         kd2 uv[NP], kk[7][NP], y[NP];
+        if (DEV && b == b0 && u == su_spec && k1 == sk_spec) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            uv[k] = ld_fstep(u + rb + 128 * k);
-            kk[0][k] = ld_fstep(k1 + rb + 128 * k);
+            for (int k = 0; k < NP; ++k) {
+                uv[k] = us0[k];
+                kk[0][k] = ks0[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                uv[k] = ld_fstep(u + rb + 128 * k);
+                kk[0][k] = ld_fstep(k1 + rb + 128 * k);
+            }
         }
 #pragma unroll
         for (int s = 0; s < 6; ++s) {

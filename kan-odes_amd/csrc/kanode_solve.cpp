@@ -1196,7 +1196,9 @@ kanode_status adjoint_fk_loop(kanode_handle* h, const void* p, kanode_solution* 
         kan::adj_loop_plan(la, c, *hp, hfw);
         std::memcpy((char*)A.hplan + sizeof(kan::AdjLoopPlan), &c, sizeof(c));
         *A.hmir = c;
-        SOLVE_HIP(h, hipMemcpyAsync(A.plan + (c.it & 1), hp, sizeof(kan::AdjLoopPlan), hipMemcpyHostToDevice, st));
+        // both buffers: the device rewrites only a plan's step-dependent fields (adj_finish_loop_kernel)
+        for (int b = 0; b < 2; ++b)
+            SOLVE_HIP(h, hipMemcpyAsync(A.plan + b, hp, sizeof(kan::AdjLoopPlan), hipMemcpyHostToDevice, st));
         SOLVE_HIP(h, hipMemcpyAsync(A.ctl, (char*)A.hplan + sizeof(kan::AdjLoopPlan), sizeof(c), hipMemcpyHostToDevice,
                                     st));
         const int64_t base = c.it;

@@ -7,7 +7,7 @@ O=$R/gpurun_out/r5/lv
 mkdir -p $O
 cd $R && export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_native_solve.py tests/test_gpu_fk_e2e.py > $O/tests.txt 2>&1 || exit 3
+  tests/test_gpu_native_solve.py tests/test_gpu_fk_e2e.py tests/test_gpu_anchors.py > $O/tests.txt 2>&1 || exit 3
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_small -o run -- \
   python3 tools/prof_small.py --reps 10 > $O/kt_small.log 2>&1 || exit 3
 rm -f $O/kt_small/*kernel_trace.csv $O/kt_small/*agent_info.csv
