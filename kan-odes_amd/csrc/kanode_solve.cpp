@@ -116,6 +116,8 @@ struct kanode_solution {
         int64_t saveat_cap = 0;
         double* ts = nullptr;              // [cap] then dts [cap]
         int64_t ts_cap = 0;
+        double* hts = nullptr;             // pinned host staging of ts | dts
+        int64_t hts_cap = 0;
         int64_t* out = nullptr;            // naccept, nreject, nf, status
         void* adj_meta = nullptr;          // adjoint: stops, jump rows and offsets
         size_t adj_meta_bytes = 0;
@@ -203,6 +205,7 @@ struct kanode_solution {
         if (adj) (void)hipFree(adj);
         if (padj) (void)hipFree(padj);
         if (hs_dev) (void)hipFree(hs_dev);
+        if (fused.hts) (void)hipHostFree(fused.hts);
         for (void* q : {(void*)loop.ctl, (void*)loop.parts, (void*)loop.dslots, (void*)loop.ts})
             if (q) (void)hipFree(q);
         for (void* q : {(void*)loop.hmir, (void*)loop.hslots})
@@ -674,7 +677,18 @@ kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, dou
     bool launched = false;
     SOLVE_TRY(kanode_internal_chain_tsit5(h, p, u0, s->batch, &a, st, launched));
     if (!launched) return KANODE_OK;
+    // the counters and the step records in one stream synchronisation (the records through pinned staging,
+    // whole: their length is what the counters say)
+    if (s->record && f.hts_cap < f.cap) {
+        if (f.hts) (void)hipHostFree(f.hts);
+        f.hts = nullptr;
+        f.hts_cap = 0;
+        SOLVE_HIP(h, hipHostMalloc((void**)&f.hts, 2 * (size_t)f.cap * sizeof(double)));
+        f.hts_cap = f.cap;
+    }
     SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (s->record)
+        SOLVE_HIP(h, hipMemcpyAsync(f.hts, f.ts, 2 * (size_t)f.cap * sizeof(double), hipMemcpyDeviceToHost, st));
     SOLVE_HIP(h, hipStreamSynchronize(st));
     int64_t res[4];
     std::memcpy(res, s->hscal, sizeof(res));
@@ -682,12 +696,8 @@ kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, dou
     if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
     const int64_t na = res[0];
     if (s->record) {
-        s->ts.resize(na);
-        s->dts.resize(na);
-        if (na > 0) {
-            SOLVE_HIP(h, hipMemcpy(s->ts.data(), f.ts, (size_t)na * sizeof(double), hipMemcpyDeviceToHost));
-            SOLVE_HIP(h, hipMemcpy(s->dts.data(), f.ts + f.cap, (size_t)na * sizeof(double), hipMemcpyDeviceToHost));
-        }
+        s->ts.assign(f.hts, f.hts + na);
+        s->dts.assign(f.hts + f.cap, f.hts + f.cap + na);
         if (!s->slots_borrowed)
             for (void* q : s->slots) (void)hipFree(q);
         s->slots.resize(f.cap);
