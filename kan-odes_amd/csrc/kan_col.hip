@@ -1316,7 +1316,9 @@ __device__ __forceinline__ T wave_sum_rows(T v) {   // Σ over the wave (all lan
 struct LvWaveShape {
     static constexpr int I = 2, H = 10, O = 2, G = 5, per = G + 1, F1 = I * per, F2 = H * per;
 };
-template <typename T, int NORM>
+// LDSC: the coefficients are read from the LDS parameters at each use instead of held in registers (the
+// stage-parallel adjoint, whose waves have half the register file each)
+template <typename T, int NORM, bool LDSC = false>
 struct LvWaveModel {
     using S = LvWaveShape;
     const Math<T>& M;
@@ -1325,9 +1327,22 @@ struct LvWaveModel {
     bool act;
     int64_t idx, n;
     int lane;
-    T c1r[S::F1];   // lane r < H: C1[r][c], c < F1 (feature c = input c / per, knot c % per)
-    T c1c[S::H];    // lane c < F1: C1[r][c], r < H
-    T c2c[S::O];    // lane c < F2: C2[o][c]
+    const T* ps;                     // the parameters (LDS)
+    T c1r[LDSC ? 1 : S::F1];   // lane r < H: C1[r][c], c < F1 (feature c = input c / per, knot c % per)
+    T c1c[LDSC ? 1 : S::H];    // lane c < F1: C1[r][c], r < H
+    T c2c[LDSC ? 1 : S::O];    // lane c < F2: C2[o][c]
+    __device__ T C1r(int c) const {
+        if constexpr (LDSC) return lane < S::H ? ps[q1(lcl[0], lane, c)] : T(0);
+        else return c1r[c];
+    }
+    __device__ T C1c(int r) const {
+        if constexpr (LDSC) return lane < S::F1 ? ps[q1(lcl[0], r, lane)] : T(0);
+        else return c1c[r];
+    }
+    __device__ T C2c(int o) const {
+        if constexpr (LDSC) return lane < S::F2 ? ps[q2(lcl[1], o, lane)] : T(0);
+        else return c2c[o];
+    }
 
     __device__ static int64_t q1(const LayerConst& L, int r, int c) {
         const int i = c / S::per, g = c % S::per;
@@ -1337,15 +1352,18 @@ struct LvWaveModel {
         const int i = c / S::per, g = c % S::per;
         return g < S::G ? L.p_off + o + S::O * (g + S::G * i) : L.w_off + o + S::O * i;
     }
-    __device__ LvWaveModel(const Math<T>& M_, const LayerConst* lcl_, const T* ps, int P_)
-        : M(M_), lcl(lcl_), P(P_), act((int)threadIdx.x < S::I), idx(threadIdx.x), n(S::I), lane(threadIdx.x) {
-        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+    __device__ LvWaveModel(const Math<T>& M_, const LayerConst* lcl_, const T* ps_, int P_)
+        : M(M_), lcl(lcl_), P(P_), act((int)(threadIdx.x & (kWave - 1)) < S::I), idx(threadIdx.x & (kWave - 1)),
+          n(S::I), lane(threadIdx.x & (kWave - 1)), ps(ps_) {
+        if constexpr (!LDSC) {
+            const LayerConst &L1 = lcl[0], &L2 = lcl[1];
 #pragma unroll
-        for (int c = 0; c < S::F1; ++c) c1r[c] = lane < S::H ? ps[q1(L1, lane, c)] : T(0);
+            for (int c = 0; c < S::F1; ++c) c1r[c] = lane < S::H ? ps[q1(L1, lane, c)] : T(0);
 #pragma unroll
-        for (int r = 0; r < S::H; ++r) c1c[r] = lane < S::F1 ? ps[q1(L1, r, lane)] : T(0);
+            for (int r = 0; r < S::H; ++r) c1c[r] = lane < S::F1 ? ps[q1(L1, r, lane)] : T(0);
 #pragma unroll
-        for (int o = 0; o < S::O; ++o) c2c[o] = lane < S::F2 ? ps[q2(L2, o, lane)] : T(0);
+            for (int o = 0; o < S::O; ++o) c2c[o] = lane < S::F2 ? ps[q2(L2, o, lane)] : T(0);
+        }
     }
     // layer 1: this lane's feature of (x_0, x_1) (lanes < F1) and h_r on lane r < H
     __device__ T layer1(T y, T& f1, T& p1, T& d1) const {
@@ -1354,7 +1372,7 @@ struct LvWaveModel {
         wide_feature<T, NORM>(M, lcl[0], c % S::per, c / S::per == 0 ? x0 : x1, f1, p1, d1);
         T h = T(0);
 #pragma unroll
-        for (int k = 0; k < S::F1; ++k) h = kfma<T>(c1r[k], lane_read(f1, k), h);
+        for (int k = 0; k < S::F1; ++k) h = kfma<T>(C1r(k), lane_read(f1, k), h);
         return h;
     }
     // layer 2: this lane's feature of h_{lane / per} (lanes < F2)
@@ -1368,7 +1386,7 @@ struct LvWaveModel {
         T f1, p1, d1, f2, p2, d2;
         const T h = layer1(y, f1, p1, d1);
         layer2(h, f2, p2, d2);
-        const T y0 = wave_sum_rows(c2c[0] * f2), y1 = wave_sum_rows(c2c[1] * f2);
+        const T y0 = wave_sum_rows(C2c(0) * f2), y1 = wave_sum_rows(C2c(1) * f2);
         return lane == 0 ? y0 : (lane == 1 ? y1 : T(0));
     }
     __device__ T vjp(T y, T ls, T* __restrict__ km) {
@@ -1383,7 +1401,7 @@ struct LvWaveModel {
         if (lane < S::F2) {
             km[q2(L2, 0, lane)] = yb0 * f2;
             km[q2(L2, 1, lane)] = yb1 * f2;
-            const T pb = c2c[0] * yb0 + c2c[1] * yb1;
+            const T pb = C2c(0) * yb0 + C2c(1) * yb1;
             z2 = g2 < S::G ? p2 * pb * (T)L2.invh : p2 * pb;
         }
         // h̄_r = N'(h_r)·Σ_g z̄_(r,g) + z̄_(r,swish) on lane r < H (the group's lanes per·r .. per·r + G)
@@ -1401,7 +1419,7 @@ struct LvWaveModel {
         for (int rr = 0; rr < S::H; ++rr) {
             const T hbr = lane_read(hb, rr);
             if (lane < S::F1) km[q1(L1, rr, lane)] = hbr * f1;
-            pb1 = kfma<T>(c1c[rr], hbr, pb1);
+            pb1 = kfma<T>(C1c(rr), hbr, pb1);
         }
         const T z1 = lane < S::F1 ? (g1 < S::G ? p1 * pb1 * (T)L1.invh : p1 * pb1) : T(0);
         // x̄_i = N'(x_i)·Σ_g z̄_(i,g) + z̄_(i,swish) on lane i < I
@@ -1413,6 +1431,62 @@ struct LvWaveModel {
         const T dx = __shfl(d1, S::per * i, kWave);
         __syncthreads();   // (one wave: km complete before the driver reads it)
         return act ? dx * sx + xsw : T(0);
+    }
+    // vjp at λs = e_0 and e_1 at once (one forward, the two pullbacks interleaved): the rows G_0, G_1 of ∂f/∂p
+    // into g0, g1 (no barrier: the caller's) and J_0, J_1 of ∂f/∂u on lanes < I.  Each product is vjp's with
+    // λs = e_k (its x·1 and + x·0 are exact).
+    __device__ void vjp2(T y, T* __restrict__ g0, T* __restrict__ g1, T& j0, T& j1) const {
+        const LayerConst &L1 = lcl[0], &L2 = lcl[1];
+        T f1, p1, d1, f2, p2, d2;
+        const T h = layer1(y, f1, p1, d1);
+        layer2(h, f2, p2, d2);
+        const int g2 = lane % S::per;
+        T za = T(0), zb = T(0);
+        if (lane < S::F2) {
+            g0[q2(L2, 0, lane)] = f2;
+            g0[q2(L2, 1, lane)] = T(0);
+            g1[q2(L2, 0, lane)] = T(0);
+            g1[q2(L2, 1, lane)] = f2;
+            const T ca = C2c(0), cb = C2c(1);
+            za = g2 < S::G ? p2 * ca * (T)L2.invh : p2 * ca;
+            zb = g2 < S::G ? p2 * cb * (T)L2.invh : p2 * cb;
+        }
+        const int r = lane < S::H ? lane : 0;
+        T sa = T(0), sb = T(0);
+#pragma unroll
+        for (int g = 0; g < S::G; ++g) {
+            sa = sa + __shfl(za, S::per * r + g, kWave);
+            sb = sb + __shfl(zb, S::per * r + g, kWave);
+        }
+        const T swa = __shfl(za, S::per * r + S::G, kWave), swb = __shfl(zb, S::per * r + S::G, kWave);
+        const T dn = __shfl(d2, S::per * r, kWave);
+        const T ha = lane < S::H ? dn * sa + swa : T(0), hb = lane < S::H ? dn * sb + swb : T(0);
+        const int g1i = lane % S::per;
+        T pa = T(0), pb = T(0);
+#pragma unroll
+        for (int rr = 0; rr < S::H; ++rr) {
+            const T hra = lane_read(ha, rr), hrb = lane_read(hb, rr);
+            if (lane < S::F1) {
+                g0[q1(L1, rr, lane)] = hra * f1;
+                g1[q1(L1, rr, lane)] = hrb * f1;
+            }
+            const T cc = C1c(rr);
+            pa = kfma<T>(cc, hra, pa);
+            pb = kfma<T>(cc, hrb, pb);
+        }
+        const T z1a = lane < S::F1 ? (g1i < S::G ? p1 * pa * (T)L1.invh : p1 * pa) : T(0);
+        const T z1b = lane < S::F1 ? (g1i < S::G ? p1 * pb * (T)L1.invh : p1 * pb) : T(0);
+        const int i = lane < S::I ? lane : 0;
+        T xa = T(0), xb = T(0);
+#pragma unroll
+        for (int g = 0; g < S::G; ++g) {
+            xa = xa + __shfl(z1a, S::per * i + g, kWave);
+            xb = xb + __shfl(z1b, S::per * i + g, kWave);
+        }
+        const T xwa = __shfl(z1a, S::per * i + S::G, kWave), xwb = __shfl(z1b, S::per * i + S::G, kWave);
+        const T dx = __shfl(d1, S::per * i, kWave);
+        j0 = act ? dx * xa + xwa : T(0);
+        j1 = act ? dx * xb + xwb : T(0);
     }
 };
 
@@ -1451,6 +1525,267 @@ kd_chain_adjoint_lvwave_kernel(const LayerConst* __restrict__ lcs, const T* __re
     onewg_adjoint<T>(m, a, mu, km, tsl, dtsl, red, recl);
 }
 
+// One Lotka-Volterra trajectory's adjoint with its stage evaluations in parallel (fp64; the idea of
+// kan_small.hip's fk_small_adjoint_sp_kernel).  The pullback is linear in the stage input: kλ = λsᵀJ(u),
+// kμ = λsᵀG(u), with J = ∂f/∂u (2 × 2) and G = ∂f/∂p (2 × 240) at the stage's point u(t) of the forward dense
+// output, which does not depend on λ.  So the rows of J and G at the six stage points of a step are evaluated
+// at once, wave i taking stage i (LvWaveModel::vjp2: both rows, λs = e_0 and e_1), into LDS; the stage
+// recurrence is then two-vector algebra, and lane l keeps the μ entries l, l + 64, .. (no sums over lanes but
+// the error norm's).  Every wave runs the recurrence and the step control on the same LDS values.  FSAL: the
+// accepted step's last point is the next step's first (its rows carry over; after a saveat jump kλ_1 is
+// re-formed from them).  Same step control as onewg_adjoint; rounding-level differences from its order.
+#ifndef KAN_LV_SP
+#define KAN_LV_SP 1
+#endif
+constexpr int kLvSpWaves = 6;
+constexpr int kLvP = LvWaveShape::F1 * LvWaveShape::H + LvWaveShape::F2 * LvWaveShape::O;   // 240
+constexpr int kLvPL = (kLvP + kWave - 1) / kWave;                                               // μ entries per lane
+template <int NORM>
+__global__ void __launch_bounds__(kLvSpWaves * kWave)
+kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* __restrict__ p, ChainAdjointArgs a,
+                             int stage_rec) {
+    using K = Tsit5Tab;
+    constexpr int N = LvWaveShape::I, P = kLvP, RW = P + N;   // a row: G_k (P), then J_k (N)
+    extern __shared__ __attribute__((aligned(16))) unsigned char cv_raw[];
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cv_raw);
+    double* ps = reinterpret_cast<double*>(cv_raw + 2 * sizeof(LayerConst));
+    double* tsl = ps + P;
+    double* dtsl = tsl + a.nsteps;
+    __shared__ double jst[6][N][RW];   // this step's stage points: row k of [G | J] at stage i
+    __shared__ double jfs[2][N][RW];   // the step's first point (FSAL), by parity
+    {
+        const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
+            tsl[i] = a.ts[i];
+            dtsl[i] = a.dts[i];
+        }
+    }
+    KAN_EXP_TABLE_LDS(tab);
+    const Math<double> M{tab};
+    const double* rec = reinterpret_cast<const double*>(a.rec);
+    const double* rk1 = reinterpret_cast<const double*>(a.k1_0);
+    if (stage_rec) {
+        double* recl = dtsl + a.nsteps;
+        onewg_stage_rec<double>(recl, a, N);
+        rec = recl;
+        rk1 = recl + a.nsteps * 7 * N;
+    }
+    LvWaveModel<double, NORM, true> m(M, lcl, ps, P);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const double* dl = reinterpret_cast<const double*>(a.dl_du);
+    const double t0 = a.t0, tf = a.tf, TT = tf - t0;
+    const double ntot = (double)(N + P);
+    int64_t cur = a.nsteps - 1;   // this wave's forward interval
+    auto interp = [&](double tau) -> double {   // u(tf - τ) on lanes < N (onewg_adjoint's adj)
+        const double t = tf - tau;
+        while (cur > 0 && tsl[cur] > t) --cur;
+        while (cur + 1 < a.nsteps && tsl[cur + 1] <= t) ++cur;
+        const double dti = dtsl[cur];
+        const double th = ::fmin(1.0, ::fmax(0.0, (t - tsl[cur]) / dti));
+        const int c = lane < N ? lane : 0;
+        const double* __restrict__ r = rec + cur * 7 * N;
+        const double* __restrict__ k1 = cur == 0 ? rk1 : rec + (cur - 1) * 7 * N + 6 * N;
+        double kv[7];
+        kv[0] = k1[c];
+#pragma unroll
+        for (int q = 1; q < 7; ++q) kv[q] = r[q * N + c];
+        double y = r[c];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            const double b = th * (K::RI[q][0] + th * (K::RI[q][1] + th * (K::RI[q][2] + th * K::RI[q][3])));
+            y = ::fma(b * dti, kv[q], y);
+        }
+        return lane < N ? y : 0.0;
+    };
+    auto rows = [&](double tau, double (*R)[RW]) {   // both rows of [G | J] at τ into R[0], R[1]
+        const double y = interp(tau);
+        double j0, j1;
+        m.vjp2(y, R[0], R[1], j0, j1);
+        if (lane < N) {
+            R[0][P + lane] = j0;
+            R[1][P + lane] = j1;
+        }
+    };
+    auto jump = [&](int gidx, double& l0, double& l1) {   // λ += Σ ∂L/∂u rows (in order)
+        for (int32_t q = a.joff[gidx]; q < a.joff[gidx + 1]; ++q) {
+            l0 = l0 + dl[(int64_t)a.jrows[q] * N];
+            l1 = l1 + dl[(int64_t)a.jrows[q] * N + 1];
+        }
+    };
+    // kλ = λsᵀJ and this lane's kμ entries λsᵀG from rows R[0], R[1]
+    auto kl_of = [&](const double (*R)[RW], double s0, double s1, double& k0, double& k1) {
+        k0 = ::fma(s1, R[1][P], s0 * R[0][P]);
+        k1 = ::fma(s1, R[1][P + 1], s0 * R[0][P + 1]);
+    };
+    auto km_of = [&](const double (*R)[RW], double s0, double s1, int r) -> double {
+        const int q = lane + kWave * r;
+        return q < P ? ::fma(s1, R[1][q], s0 * R[0][q]) : 0.0;
+    };
+    double l0 = 0.0, l1 = 0.0;
+    if (dl) jump(0, l0, l1);
+    int fp = 0;
+    rows(0.0, w == 0 ? jfs[0] : jst[w]);   // (waves > 0: a scratch copy)
+    __syncthreads();
+    double k10, k11;   // kλ_1
+    kl_of(jfs[0], l0, l1, k10, k11);
+    int64_t nf = 1;
+    double mu[kLvPL];
+#pragma unroll
+    for (int r = 0; r < kLvPL; ++r) mu[r] = 0.0;
+    double h = a.dt;
+    if (a.adaptive && !(a.dt > 0)) {   // Hairer-Wanner on [λ; μ] (μ = 0)
+        double sm1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < kLvPL; ++r) {
+            const double v = km_of(jfs[0], l0, l1, r) / a.abstol;
+            sm1 = ::fma(v, v, sm1);
+        }
+        const double sk0 = ::fma(a.reltol, kabs(l0), a.abstol), sk1 = ::fma(a.reltol, kabs(l1), a.abstol);
+        const double d0 = ::sqrt(((l0 / sk0) * (l0 / sk0) + (l1 / sk1) * (l1 / sk1)) / ntot);
+        const double d1 = ::sqrt(((k10 / sk0) * (k10 / sk0) + (k11 / sk1) * (k11 / sk1) + wave_sum(sm1)) / ntot);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = ::fmin(h0, TT);
+        rows(h0, jst[w]);
+        __syncthreads();
+        const double s0 = ::fma(h0, k10, l0), s1 = ::fma(h0, k11, l1);
+        double kh0, kh1;
+        kl_of(jst[0], s0, s1, kh0, kh1);
+        ++nf;
+        double sm2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < kLvPL; ++r) {
+            const double v = (km_of(jst[0], s0, s1, r) - km_of(jfs[0], l0, l1, r)) / a.abstol;
+            sm2 = ::fma(v, v, sm2);
+        }
+        const double e0 = (kh0 - k10) / sk0, e1 = (kh1 - k11) / sk1;
+        const double d2 = ::sqrt((e0 * e0 + e1 * e1 + wave_sum(sm2)) / ntot) / h0;
+        const double mx = ::fmax(d1, d2);
+        const double h1 = mx <= 1e-15 ? ::fmax(1e-6, h0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
+        h = ::fmin(::fmin(100 * h0, h1), TT);
+        __syncthreads();   // jst is rewritten by the first step
+    }
+    double qold = a.qoldinit, tau = 0.0;
+    int64_t si = 0, naccept = 0, nreject = 0, it = 0, status = 0;
+    double wc = 1.0;   // c of this wave's stage (selects: no runtime index into the tableau)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) wc = w == i ? K::TC[i] : wc;
+    for (; it < a.maxiters; ++it) {
+        if (tau >= TT - 1e-14 * ::fmax(1.0, TT)) break;
+        h = ::fmin(h, a.stops[si] - tau);
+        rows(w == 5 ? tau + h : tau + wc * h, jst[w]);
+        __syncthreads();
+        double cA[kLvPL], cE[kLvPL];
+#pragma unroll
+        for (int r = 0; r < kLvPL; ++r) {
+            const double m1 = km_of(jfs[fp], l0, l1, r);
+            cA[r] = (h * K::TA[5][0]) * m1;
+            cE[r] = (h * K::BT[0]) * m1;
+        }
+        double k0[7], k1[7];
+        k0[0] = k10;
+        k1[0] = k11;
+        double s0 = l0, s1 = l1;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            s0 = l0;
+            s1 = l1;
+#pragma unroll
+            for (int q = 0; q <= i; ++q) {
+                s0 = ::fma(h * K::TA[i][q], k0[q], s0);
+                s1 = ::fma(h * K::TA[i][q], k1[q], s1);
+            }
+            kl_of(jst[i], s0, s1, k0[i + 1], k1[i + 1]);
+#pragma unroll
+            for (int r = 0; r < kLvPL; ++r) {
+                const double mm = km_of(jst[i], s0, s1, r);
+                if (i < 5) cA[r] = ::fma(h * K::TA[5][i + 1], mm, cA[r]);
+                cE[r] = ::fma(h * K::BT[i + 1], mm, cE[r]);
+            }
+        }
+        nf += 6;
+        double hnew = h;
+        if (a.adaptive) {
+            double ev0 = 0.0, ev1 = 0.0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                ev0 = ::fma(h * K::BT[r], k0[r], ev0);
+                ev1 = ::fma(h * K::BT[r], k1[r], ev1);
+            }
+            const double e0 = ::fma(h * K::BT[6], k0[6], ev0), e1 = ::fma(h * K::BT[6], k1[6], ev1);
+            const double sk0 = ::fma(a.reltol, ::fmax(kabs(l0), kabs(s0)), a.abstol);
+            const double sk1 = ::fma(a.reltol, ::fmax(kabs(l1), kabs(s1)), a.abstol);
+            double sm = 0.0;
+#pragma unroll
+            for (int r = 0; r < kLvPL; ++r) {
+                const double sk = ::fma(a.reltol, ::fmax(kabs(mu[r]), kabs(mu[r] + cA[r])), a.abstol);
+                sm = ::fma(cE[r] / sk, cE[r] / sk, sm);
+            }
+            const double eest = ::sqrt(((e0 / sk0) * (e0 / sk0) + (e1 / sk1) * (e1 / sk1) + wave_sum(sm)) / ntot);
+            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            if (eest > 1.0 && h > a.dtmin) {
+                ++nreject;
+                h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
+                __syncthreads();   // every wave is done with jst
+                continue;
+            }
+            double q = q11 / ::pow(qold, a.beta2);
+            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
+            if (1.0 <= q && q <= 1.0) q = 1.0;
+            hnew = q > 0 ? h / q : h * a.qmax;
+            qold = ::fmax(eest, a.qoldinit);
+        }
+        // the accepted step's last point becomes the next step's first (wave 5 wrote it)
+        if (w == 5)
+            for (int q = lane; q < RW; q += kWave) {
+                jfs[fp ^ 1][0][q] = jst[5][0][q];
+                jfs[fp ^ 1][1][q] = jst[5][1][q];
+            }
+        __syncthreads();   // every wave is done with jst, and jfs[fp ^ 1] is complete
+        fp ^= 1;
+        tau = tau + h;
+        l0 = s0;
+        l1 = s1;
+#pragma unroll
+        for (int r = 0; r < kLvPL; ++r) mu[r] = mu[r] + cA[r];
+        k10 = k0[6];
+        k11 = k1[6];
+        if (a.hs && threadIdx.x == 0 && naccept < a.hs_cap) a.hs[naccept] = h;
+        ++naccept;
+        if (::fabs(tau - a.stops[si]) <= 1e-12 * ::fmax(1.0, TT)) {
+            tau = a.stops[si];
+            if (si + 1 < a.nstops) {
+                if (dl && a.joff[si + 2] > a.joff[si + 1]) {
+                    jump((int)si + 1, l0, l1);
+                    kl_of(jfs[fp], l0, l1, k10, k11);   // u_modified!: kλ_1 re-formed
+                    ++nf;
+                }
+            }
+            si = si + 1 < a.nstops ? si + 1 : a.nstops - 1;
+        }
+        h = hnew;
+    }
+    if (it == a.maxiters && !(tau >= TT - 1e-14 * ::fmax(1.0, TT))) status = 1;
+    if (dl) jump((int)a.nstops, l0, l1);
+    if (w == 0) {
+        if (a.du0 && lane < N) reinterpret_cast<double*>(a.du0)[lane] = lane == 0 ? l0 : l1;
+        if (a.dp) {
+#pragma unroll
+            for (int r = 0; r < kLvPL; ++r)
+                if (lane + kWave * r < P) reinterpret_cast<double*>(a.dp)[lane + kWave * r] = mu[r];
+        }
+        if (lane == 0) {
+            a.out[0] = naccept;
+            a.out[1] = nreject;
+            a.out[2] = nf;
+            a.out[3] = status;
+        }
+    }
+}
+
 // The one-workgroup adjoint (kd_chain_adjoint_kernel): the small-chain conditions of
 // launch_kd_chain_tsit5 plus nsteps <= kChainAdjointMaxSteps and the LDS budget.
 template <typename T>
@@ -1470,6 +1805,26 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
         const size_t rec = sizeof(T) * ((size_t)a.nsteps * 7 + 1) * LvWaveShape::I;
         const int stage_rec = lds + rec <= 60 * 1024 ? 1 : 0;
         if (stage_rec) lds += rec;
+        if constexpr (std::is_same<T, double>::value) {   // the stage-parallel form (kd_chain_adjoint_lvsp_kernel)
+            const size_t jst = sizeof(double) * 8 * LvWaveShape::I * (kLvP + LvWaveShape::I);
+            size_t lsp = 2 * sizeof(LayerConst) + sizeof(double) * (kLvP + 2 * (size_t)a.nsteps);
+            const int sp_rec = lsp + rec + jst <= 140 * 1024 ? 1 : 0;
+            if (sp_rec) lsp += rec;
+            if (KAN_LV_SP && P == kLvP && lsp + jst <= 140 * 1024) {
+                const void* fn = hlcs[0].norm == NORM_TANH_FAST
+                                     ? reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>)
+                                     : reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>);
+                const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsp);
+                if (e != hipSuccess) return e;
+                if (hlcs[0].norm == NORM_TANH_FAST)
+                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>), dim3(1), dim3(kLvSpWaves * kWave),
+                                       lsp, st, lcs, p, a, sp_rec);
+                else
+                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>), dim3(1), dim3(kLvSpWaves * kWave),
+                                       lsp, st, lcs, p, a, sp_rec);
+                return hipGetLastError();
+            }
+        }
         if (pre % 8 == 0 && lds <= 60 * 1024) {
             if (hlcs[0].norm == NORM_TANH_FAST)
                 hipLaunchKernelGGL((kd_chain_adjoint_lvwave_kernel<T, NORM_TANH_FAST>), dim3(1), dim3(kWave), lds, st,

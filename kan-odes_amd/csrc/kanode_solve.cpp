@@ -121,6 +121,10 @@ struct kanode_solution {
         int64_t* out = nullptr;            // naccept, nreject, nf, status
         void* adj_meta = nullptr;          // adjoint: stops, jump rows and offsets
         size_t adj_meta_bytes = 0;
+        void* hup = nullptr;               // pinned staging of the small uploads (staged_upload)
+        size_t hup_bytes = 0;
+        hipEvent_t hup_ev = nullptr;       // recorded after the last upload from hup
+        bool hup_pending = false;
     } fused;
     double* dscal = nullptr;         // device scalars (norm totals; an adaptive FK adjoint step's 1 + P terms)
     double* hscal = nullptr;         // pinned host mirror (mapped, coherent)
@@ -206,6 +210,11 @@ struct kanode_solution {
         if (padj) (void)hipFree(padj);
         if (hs_dev) (void)hipFree(hs_dev);
         if (fused.hts) (void)hipHostFree(fused.hts);
+        if (fused.hup_ev) {
+            if (fused.hup_pending) (void)hipEventSynchronize(fused.hup_ev);
+            (void)hipEventDestroy(fused.hup_ev);
+        }
+        if (fused.hup) (void)hipHostFree(fused.hup);
         for (void* q : {(void*)loop.ctl, (void*)loop.parts, (void*)loop.dslots, (void*)loop.ts})
             if (q) (void)hipFree(q);
         for (void* q : {(void*)loop.hmir, (void*)loop.hslots})
@@ -597,6 +606,31 @@ kanode_status solve_t(kanode_handle* h, const void* p, const void* u0, double t0
 }
 
 // ---- one-workgroup solve of a small chain (kd_chain_tsit5_kernel) ------------------------
+// A stream-ordered upload of host bytes through the solution's pinned staging: unlike hipMemcpy from pageable
+// memory it does not hold the host until the stream drains.  The staging is rewritten only after the previous
+// upload from it has run (its event).
+kanode_status staged_upload(kanode_handle* h, kanode_solution* s, void* dst, const void* src, size_t bytes,
+                            hipStream_t st) {
+    auto& f = s->fused;
+    if (!f.hup_ev) SOLVE_HIP(h, hipEventCreateWithFlags(&f.hup_ev, hipEventDisableTiming));
+    if (f.hup_pending) {
+        SOLVE_HIP(h, hipEventSynchronize(f.hup_ev));
+        f.hup_pending = false;
+    }
+    if (f.hup_bytes < bytes) {
+        if (f.hup) (void)hipHostFree(f.hup);
+        f.hup = nullptr;
+        f.hup_bytes = 0;
+        SOLVE_HIP(h, hipHostMalloc(&f.hup, bytes));
+        f.hup_bytes = bytes;
+    }
+    std::memcpy(f.hup, src, bytes);
+    SOLVE_HIP(h, hipMemcpyAsync(dst, f.hup, bytes, hipMemcpyHostToDevice, st));
+    SOLVE_HIP(h, hipEventRecord(f.hup_ev, st));
+    f.hup_pending = true;
+    return KANODE_OK;
+}
+
 // The whole forward solve in one launch for a chain of small layers and <= 16 trajectories (the
 // Lotka-Volterra shape).  done = false when the shape is not covered or the dense-output block
 // filled up: the caller then runs the host loop (solve_t) from scratch.
@@ -648,8 +682,7 @@ kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, dou
         f.saveat_cap = n_save;
     }
     if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
-    if (n_save > 0)
-        SOLVE_HIP(h, hipMemcpyAsync(f.saveat, saveat, (size_t)n_save * sizeof(double), hipMemcpyHostToDevice, st));
+    if (n_save > 0) SOLVE_TRY(staged_upload(h, s, f.saveat, saveat, (size_t)n_save * sizeof(double), st));
     kan::ChainSolveArgs a{};
     a.t0 = t0;
     a.tf = tf;
@@ -1608,7 +1641,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
 // groups and stops go to the solution's adj_meta buffer, everything else into a (rec, k1_0, ts, dts and
 // nsteps are the caller's).
 kanode_status one_launch_adj_args(kanode_handle* h, kanode_solution* s, const void* dl_du, void* du0, void* dp,
-                                  const kanode_solver_options& o, kan::ChainAdjointArgs& a) {
+                                  const kanode_solver_options& o, kan::ChainAdjointArgs& a, hipStream_t st) {
     if (!o.adaptive && !(o.dt > 0))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "fixed-step adjoint needs opt->dt > 0");
     const double t0 = s->t0, tf = s->tf, TT = tf - t0;
@@ -1664,7 +1697,7 @@ kanode_status one_launch_adj_args(kanode_handle* h, kanode_solution* s, const vo
     if (!rows.empty())
         std::memcpy(host.data() + ns * sizeof(double) + off.size() * sizeof(int32_t), rows.data(),
                     rows.size() * sizeof(int32_t));
-    SOLVE_HIP(h, hipMemcpy(f.adj_meta, host.data(), bytes, hipMemcpyHostToDevice));
+    SOLVE_TRY(staged_upload(h, s, f.adj_meta, host.data(), bytes, st));
     if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
     a = kan::ChainAdjointArgs{};
     a.t0 = t0;
@@ -1726,7 +1759,7 @@ kanode_status adjoint_fused_t(kanode_handle* h, const void* p, kanode_solution* 
         !kanode_internal_chain_tsit5_ok(h, s->batch))
         return KANODE_OK;
     kan::ChainAdjointArgs a{};
-    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, a));
+    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, a, st));
     auto& f = s->fused;
     a.rec = f.block;
     a.k1_0 = s->k1_0;
@@ -1765,7 +1798,7 @@ kanode_status adjoint_pair_t(kanode_handle* h, const void* p, kanode_solution* s
     const int nwg = kanode_internal_pair_adjoint_workgroups(h, s->batch);
     if (nwg < 1 || nwg > 256) return KANODE_OK;
     kan::PairAdjArgs pa{};
-    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, pa.c));
+    SOLVE_TRY(one_launch_adj_args(h, s, dl_du, du0, dp, o, pa.c, st));
     const size_t tab = (size_t)nsteps * sizeof(double), off_tab = 256, off_ts = off_tab + tab, off_dts = off_ts + tab;
     const size_t off_x = (off_dts + tab + 255) / 256 * 256;
     const size_t need = off_x + (size_t)2 * nwg * kan::kPairAdjXW * sizeof(double);
