@@ -1537,14 +1537,19 @@ kd_chain_adjoint_lvwave_kernel(const LayerConst* __restrict__ lcs, const T* __re
 #ifndef KAN_LV_SP
 #define KAN_LV_SP 1
 #endif
-constexpr int kLvSpWaves = 6;
+constexpr int kLvSpWaves = 6;   // the stage waves; one more takes the controller's qold^β2 during the stage phase
 constexpr int kLvP = LvWaveShape::F1 * LvWaveShape::H + LvWaveShape::F2 * LvWaveShape::O;   // 240
 constexpr int kLvPL = (kLvP + kWave - 1) / kWave;                                               // μ entries per lane
 template <int NORM>
-__global__ void __launch_bounds__(kLvSpWaves * kWave)
+__global__ void __launch_bounds__((kLvSpWaves + 1) * kWave)
 kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* __restrict__ p, ChainAdjointArgs a,
                              int stage_rec) {
     using K = Tsit5Tab;
+#ifdef KAN_LVSP_FASTPOW   // timing experiment only: fp32 fast exp/log for the controller's powers
+#define KAN_LVSP_POW(x, y) (double)__expf((float)(y) * __logf((float)(x)))
+#else
+#define KAN_LVSP_POW(x, y) ::pow(x, y)
+#endif
     constexpr int N = LvWaveShape::I, P = kLvP, RW = P + N;   // a row: G_k (P), then J_k (N)
     extern __shared__ __attribute__((aligned(16))) unsigned char cv_raw[];
     LayerConst* lcl = reinterpret_cast<LayerConst*>(cv_raw);
@@ -1553,6 +1558,7 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
     double* dtsl = tsl + a.nsteps;
     __shared__ double jst[6][N][RW];   // this step's stage points: row k of [G | J] at stage i
     __shared__ double jfs[2][N][RW];   // the step's first point (FSAL), by parity
+    __shared__ double pqs;             // qold^β2 of this step (the last wave)
     {
         const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
@@ -1628,7 +1634,7 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
     double l0 = 0.0, l1 = 0.0;
     if (dl) jump(0, l0, l1);
     int fp = 0;
-    rows(0.0, w == 0 ? jfs[0] : jst[w]);   // (waves > 0: a scratch copy)
+    if (w < kLvSpWaves) rows(0.0, w == 0 ? jfs[0] : jst[w]);   // (waves > 0: a scratch copy)
     __syncthreads();
     double k10, k11;   // kλ_1
     kl_of(jfs[0], l0, l1, k10, k11);
@@ -1649,7 +1655,7 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
         const double d1 = ::sqrt(((k10 / sk0) * (k10 / sk0) + (k11 / sk1) * (k11 / sk1) + wave_sum(sm1)) / ntot);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         h0 = ::fmin(h0, TT);
-        rows(h0, jst[w]);
+        if (w < kLvSpWaves) rows(h0, jst[w]);
         __syncthreads();
         const double s0 = ::fma(h0, k10, l0), s1 = ::fma(h0, k11, l1);
         double kh0, kh1;
@@ -1676,7 +1682,10 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
     for (; it < a.maxiters; ++it) {
         if (tau >= TT - 1e-14 * ::fmax(1.0, TT)) break;
         h = ::fmin(h, a.stops[si] - tau);
-        rows(w == 5 ? tau + h : tau + wc * h, jst[w]);
+#ifndef KAN_LVSP_NOPH1   // timing experiment only: the stage points left at their first values (wrong results)
+        if (w < kLvSpWaves) rows(w == 5 ? tau + h : tau + wc * h, jst[w]);
+#endif
+        if (w == kLvSpWaves && lane == 0 && a.adaptive) pqs = KAN_LVSP_POW(qold, a.beta2);
         __syncthreads();
         double cA[kLvPL], cE[kLvPL];
 #pragma unroll
@@ -1725,14 +1734,14 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
                 sm = ::fma(cE[r] / sk, cE[r] / sk, sm);
             }
             const double eest = ::sqrt(((e0 / sk0) * (e0 / sk0) + (e1 / sk1) * (e1 / sk1) + wave_sum(sm)) / ntot);
-            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            const double q11 = eest > 0 ? KAN_LVSP_POW(eest, a.beta1) : 0.0;
             if (eest > 1.0 && h > a.dtmin) {
                 ++nreject;
                 h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
                 __syncthreads();   // every wave is done with jst
                 continue;
             }
-            double q = q11 / ::pow(qold, a.beta2);
+            double q = q11 / pqs;   // (= pow(qold, β2); read after the stage phase's barrier)
             q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
             if (1.0 <= q && q <= 1.0) q = 1.0;
             hnew = q > 0 ? h / q : h * a.qmax;
@@ -1768,6 +1777,7 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
         }
         h = hnew;
     }
+#undef KAN_LVSP_POW
     if (it == a.maxiters && !(tau >= TT - 1e-14 * ::fmax(1.0, TT))) status = 1;
     if (dl) jump((int)a.nstops, l0, l1);
     if (w == 0) {
@@ -1814,13 +1824,18 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
                 const void* fn = hlcs[0].norm == NORM_TANH_FAST
                                      ? reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>)
                                      : reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>);
-                const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsp);
-                if (e != hipSuccess) return e;
+                static size_t set_lds[2] = {0, 0};   // (the attribute is raised once per instantiation and size)
+                size_t& cap = set_lds[hlcs[0].norm == NORM_TANH_FAST ? 0 : 1];
+                if (lsp > cap) {
+                    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsp);
+                    if (e != hipSuccess) return e;
+                    cap = lsp;
+                }
                 if (hlcs[0].norm == NORM_TANH_FAST)
-                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>), dim3(1), dim3(kLvSpWaves * kWave),
+                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>), dim3(1), dim3((kLvSpWaves + 1) * kWave),
                                        lsp, st, lcs, p, a, sp_rec);
                 else
-                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>), dim3(1), dim3(kLvSpWaves * kWave),
+                    hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>), dim3(1), dim3((kLvSpWaves + 1) * kWave),
                                        lsp, st, lcs, p, a, sp_rec);
                 return hipGetLastError();
             }

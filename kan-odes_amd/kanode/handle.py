@@ -312,7 +312,13 @@ class KanodeHandle:
         self._check_t(u0, None, "u0")
         if u0.numel() != B * self.N or self.N_out != self.N:
             raise ValueError("solve needs u0 of B x N entries and an RHS with N_in == N_out")
-        sv = (C.c_double * max(1, len(saveat)))(*[float(x) for x in saveat])
+        key = tuple(saveat)
+        cache = self.__dict__.setdefault("_saveat_c", {})
+        sv = cache.get(key)
+        if sv is None:   # (the C array of a saveat list, kept: training solves pass the same list every step)
+            if len(cache) >= 16:
+                cache.clear()
+            sv = cache[key] = (C.c_double * max(1, len(saveat)))(*[float(x) for x in saveat])
         u_save = torch.empty((len(saveat),) + tuple(u0.shape), dtype=self.dtype, device=self.device)
         st = L.SolveStatsC()
         dense = None

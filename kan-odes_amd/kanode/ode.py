@@ -27,6 +27,7 @@ from __future__ import annotations
 import ctypes
 import math
 from dataclasses import dataclass, field
+from functools import lru_cache
 
 import torch
 
@@ -73,6 +74,14 @@ def _norm(f, x: torch.Tensor) -> float:
     return math.sqrt(float(red((x * x).sum().reshape(1)).item()) / f.global_count(x.numel()))
 
 
+_OPTS_C: dict = {}
+
+
+@lru_cache(maxsize=64)
+def _ascending(saveat: tuple) -> bool:
+    return all(a <= b for a, b in zip(saveat, saveat[1:]))
+
+
 @dataclass
 class Tsit5Options:
     abstol: float = 1e-6
@@ -97,6 +106,17 @@ class Tsit5Options:
     replay_adjoint_dts: tuple | None = None
 
     def to_c(self):
+        """A kanode_solver_options struct (a copy of one built per field values, which the caller may edit)."""
+        key = (self.abstol, self.reltol, self.dt, self.adaptive, self.maxiters, self.dtmin, self.beta1, self.beta2,
+               self.gamma, self.qmin, self.qmax, self.qoldinit, self.control, self.graph_steps)
+        o = _OPTS_C.get(key)
+        if o is None:
+            if len(_OPTS_C) >= 64:
+                _OPTS_C.clear()
+            o = _OPTS_C[key] = self._to_c()
+        return type(o).from_buffer_copy(o)
+
+    def _to_c(self):
         from . import _lib as L
         o = L.SolverOptsC()
         L.lib().kanode_solver_options_default(ctypes.byref(o))
@@ -192,7 +212,7 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
         raise ValueError(f"unknown sensealg {sensealg!r}")
     grad = torch.is_grad_enabled() and (getattr(p, "requires_grad", False) or u0.requires_grad)
     native = (opt.native and hasattr(f, "hd") and isinstance(p, torch.Tensor) and u0.is_cuda and u0.dim() in (1, 2) and dense_record is None
-              and tf > t0 and all(a <= b for a, b in zip(saveat, saveat[1:])))
+              and tf > t0 and _ascending(tuple(saveat)))
     if native:
         tol = 1e-12 * max(1.0, abs(tf))
         saveat = [s for s in saveat if s <= tf + tol]

@@ -91,7 +91,9 @@ class FusedAdam(Adam):
 
 
 def mse_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    return torch.mean((target - pred) ** 2)
+    """mean((target - pred)²) (the drivers' loss, Fisher-KPP_Source.jl:107-108 mean(abs2, X - pred)): torch's
+    fused mse_loss, one launch forward and one backward instead of a sub / pow / mean chain."""
+    return torch.nn.functional.mse_loss(pred, target)
 
 
 def reg_loss(p: torch.Tensor, act_reg: float = 1.0, entropy_reg: float = 1.0) -> torch.Tensor:
