@@ -1559,6 +1559,12 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
     __shared__ double jst[6][N][RW];   // this step's stage points: row k of [G | J] at stage i
     __shared__ double jfs[2][N][RW];   // the step's first point (FSAL), by parity
     __shared__ double pqs;             // qold^β2 of this step (the last wave)
+    // the tableau in LDS (a_ij [6][6], b̃ [7], the interpolant's r_qm [7][4]): as compile-time literals the 71
+    // fp64 constants were materialised once and held (then spilled) across the step loop; LDS reads of a
+    // uniform address are broadcasts, re-issued after each barrier
+    __shared__ double kt[71];
+    for (int q = threadIdx.x; q < 71; q += blockDim.x)
+        kt[q] = q < 36 ? K::TA[q / 6][q % 6] : (q < 43 ? K::BT[q - 36] : K::RI[(q - 43) / 4][(q - 43) % 4]);
     {
         const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
@@ -1602,12 +1608,18 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
         double y = r[c];
 #pragma unroll
         for (int q = 0; q < 7; ++q) {
-            const double b = th * (K::RI[q][0] + th * (K::RI[q][1] + th * (K::RI[q][2] + th * K::RI[q][3])));
+            const double* ri = kt + 43 + 4 * q;
+            const double b = th * (ri[0] + th * (ri[1] + th * (ri[2] + th * ri[3])));
             y = ::fma(b * dti, kv[q], y);
         }
         return lane < N ? y : 0.0;
     };
     auto rows = [&](double tau, double (*R)[RW]) {   // both rows of [G | J] at τ into R[0], R[1]
+        // (the lane made opaque per call: the model's lane-derived indices are then recomputed here, a few
+        // integer ops, instead of hoisted out of the step loop and spilled)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        m.lane = ln;
         const double y = interp(tau);
         double j0, j1;
         m.vjp2(y, R[0], R[1], j0, j1);
@@ -1691,8 +1703,8 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
 #pragma unroll
         for (int r = 0; r < kLvPL; ++r) {
             const double m1 = km_of(jfs[fp], l0, l1, r);
-            cA[r] = (h * K::TA[5][0]) * m1;
-            cE[r] = (h * K::BT[0]) * m1;
+            cA[r] = (h * kt[30]) * m1;
+            cE[r] = (h * kt[36]) * m1;
         }
         double k0[7], k1[7];
         k0[0] = k10;
@@ -1704,15 +1716,16 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
             s1 = l1;
 #pragma unroll
             for (int q = 0; q <= i; ++q) {
-                s0 = ::fma(h * K::TA[i][q], k0[q], s0);
-                s1 = ::fma(h * K::TA[i][q], k1[q], s1);
+                const double c = h * kt[6 * i + q];
+                s0 = ::fma(c, k0[q], s0);
+                s1 = ::fma(c, k1[q], s1);
             }
             kl_of(jst[i], s0, s1, k0[i + 1], k1[i + 1]);
 #pragma unroll
             for (int r = 0; r < kLvPL; ++r) {
                 const double mm = km_of(jst[i], s0, s1, r);
-                if (i < 5) cA[r] = ::fma(h * K::TA[5][i + 1], mm, cA[r]);
-                cE[r] = ::fma(h * K::BT[i + 1], mm, cE[r]);
+                if (i < 5) cA[r] = ::fma(h * kt[30 + i + 1], mm, cA[r]);
+                cE[r] = ::fma(h * kt[36 + i + 1], mm, cE[r]);
             }
         }
         nf += 6;
@@ -1721,10 +1734,10 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
             double ev0 = 0.0, ev1 = 0.0;
 #pragma unroll
             for (int r = 0; r < 6; ++r) {
-                ev0 = ::fma(h * K::BT[r], k0[r], ev0);
-                ev1 = ::fma(h * K::BT[r], k1[r], ev1);
+                ev0 = ::fma(h * kt[36 + r], k0[r], ev0);
+                ev1 = ::fma(h * kt[36 + r], k1[r], ev1);
             }
-            const double e0 = ::fma(h * K::BT[6], k0[6], ev0), e1 = ::fma(h * K::BT[6], k1[6], ev1);
+            const double e0 = ::fma(h * kt[42], k0[6], ev0), e1 = ::fma(h * kt[42], k1[6], ev1);
             const double sk0 = ::fma(a.reltol, ::fmax(kabs(l0), kabs(s0)), a.abstol);
             const double sk1 = ::fma(a.reltol, ::fmax(kabs(l1), kabs(s1)), a.abstol);
             double sm = 0.0;

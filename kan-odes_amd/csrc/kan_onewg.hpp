@@ -25,6 +25,13 @@
 
 namespace kan {
 
+// the step controller's powers (KAN_ONEWG_EXPLOG: exp2(y·log2 x), an A/B of their cost on one wave)
+#ifdef KAN_ONEWG_EXPLOG
+#define KAN_ONEWG_POW(x, y) ::exp2((y) * ::log2(x))
+#else
+#define KAN_ONEWG_POW(x, y) ::pow(x, y)
+#endif
+
 // Σ over the block of v (inactive entries give 0), the same ordered total in every thread.  red: LDS of
 // blockDim / 64 doubles.
 __device__ __forceinline__ double onewg_bsum(double v, double* red) {
@@ -93,13 +100,13 @@ __device__ __forceinline__ void onewg_tsit5(Mdl& m, const T* __restrict__ u0, co
             const double sk = ::fma(a.reltol, ::fmax(kabs((double)u), kabs((double)y)), a.abstol);
             const double r = e / sk;
             const double eest = ::sqrt(bsum(r * r) / (double)n);
-            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            const double q11 = eest > 0 ? KAN_ONEWG_POW(eest, a.beta1) : 0.0;
             if (eest > 1.0 && dt > a.dtmin) {
                 ++nreject;
                 dt = dt / ::fmin(1.0 / a.qmin, q11 / a.gamma);
                 continue;
             }
-            double q = q11 / ::pow(qold, a.beta2);
+            double q = q11 / KAN_ONEWG_POW(qold, a.beta2);
             q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
             if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
             dtnew = q > 0 ? dt / q : dt * a.qmax;
@@ -314,14 +321,14 @@ __device__ __forceinline__ void onewg_adjoint(Mdl& m, const ChainAdjointArgs& a,
                 s += (e / sk) * (e / sk);
             }
             const double eest = ::sqrt(bsum(s) / (double)ntot);
-            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            const double q11 = eest > 0 ? KAN_ONEWG_POW(eest, a.beta1) : 0.0;
             if (eest > 1.0 && h > a.dtmin) {
                 ++nreject;
                 h = h / ::fmin(1.0 / a.qmin, q11 / a.gamma);
                 __syncthreads();   // mu1 is rewritten by the retry
                 continue;
             }
-            double q = q11 / ::pow(qold, a.beta2);
+            double q = q11 / KAN_ONEWG_POW(qold, a.beta2);
             q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
             if (1.0 <= q && q <= 1.0) q = 1.0;
             hnew = q > 0 ? h / q : h * a.qmax;
