@@ -1545,11 +1545,7 @@ __global__ void __launch_bounds__((kLvSpWaves + 1) * kWave)
 kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* __restrict__ p, ChainAdjointArgs a,
                              int stage_rec) {
     using K = Tsit5Tab;
-#ifdef KAN_LVSP_FASTPOW   // timing experiment only: fp32 fast exp/log for the controller's powers
-#define KAN_LVSP_POW(x, y) (double)__expf((float)(y) * __logf((float)(x)))
-#else
-#define KAN_LVSP_POW(x, y) ::pow(x, y)
-#endif
+#define KAN_LVSP_POW(x, y) KAN_ONEWG_POW(x, y)
     constexpr int N = LvWaveShape::I, P = kLvP, RW = P + N;   // a row: G_k (P), then J_k (N)
     extern __shared__ __attribute__((aligned(16))) unsigned char cv_raw[];
     LayerConst* lcl = reinterpret_cast<LayerConst*>(cv_raw);

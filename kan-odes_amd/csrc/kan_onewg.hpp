@@ -25,11 +25,14 @@
 
 namespace kan {
 
-// the step controller's powers (KAN_ONEWG_EXPLOG: exp2(y·log2 x), an A/B of their cost on one wave)
-#ifdef KAN_ONEWG_EXPLOG
-#define KAN_ONEWG_POW(x, y) ::exp2((y) * ::log2(x))
-#else
+// The step controller's powers EEst^β1 and qold^β2 as exp2(y·log2 x) (x > 0 here): on one wave the full pow
+// sits on each step's dependency chain, and this form took the FK26 forward solve 169 -> 148 us, its adjoint
+// 647 -> 623 us (profiles/r05/small/onewg_pow_ab.txt).  It can differ from pow in the last bits, so a step size
+// can differ from the host loop's at rounding level (the tests' bars allow for that).  KAN_ONEWG_STDPOW: pow.
+#ifdef KAN_ONEWG_STDPOW
 #define KAN_ONEWG_POW(x, y) ::pow(x, y)
+#else
+#define KAN_ONEWG_POW(x, y) ::exp2((y) * ::log2(x))
 #endif
 
 // Σ over the block of v (inactive entries give 0), the same ordered total in every thread.  red: LDS of
