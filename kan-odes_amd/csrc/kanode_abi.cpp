@@ -1513,6 +1513,9 @@ kanode_status kanode_internal_fk_adjoint_step(kanode_handle* h, const void* p, k
         a->fin.km1 = af->km1;
         a->fin.km7 = af->km7;
         a->fin.out = af->out;
+        // the arrival counters re-zeroed on the stream before every fused launch: a wait that timed
+        // out in an earlier launch cannot leave them off by one for this one
+        HIP_TRY(h, hipMemsetAsync(h->fin_ctr, 0, 2 * sizeof(unsigned), st));
     }
     bool fused_fin = false;
     HIP_TRY(h, kan::launch_fk_vjp_step_pp(h->hpc, h->hlc[0], h->dlc, h->dpc, (const double*)p, h->dtable, cd, co,
