@@ -241,6 +241,30 @@ class _NativeAdjointSolve(torch.autograd.Function):
         return None, None, None, None, None, dp, du0
 
 
+def native_mse_gradient(f, u0, tspan, p, saveat, opt: Tsit5Options, target):
+    """(loss, dL/dp, Solution) for L = mse_loss(solve(...).u, target) through the native solve and
+    InterpolatingAdjoint, without the autograd engine: the same two C calls as backward() of
+    solve_native_interpolating_adjoint, with ∂L/∂u formed as mse_loss's backward does ((u - X)·2/numel).
+    For Trainer's plain-MSE step (a handful of launches per iteration, where the engine's own overhead showed)."""
+    hd = f.hd
+    oc = opt.to_c()
+    pc = p.detach().contiguous()
+    u_save, st, dense = hd.solve_tsit5(pc, u0.detach().contiguous(), float(tspan[0]), float(tspan[1]), saveat, oc,
+                                       keep_dense=True)
+    try:
+        stats = dict(st)
+        stats["dts"] = dense.step_sizes()[1].tolist()
+        loss = torch.nn.functional.mse_loss(u_save, target)
+        dl = (u_save - target).mul_(2.0 / u_save.numel())
+        _, dp, ast = hd.adjoint_tsit5(pc, dense, dl, oc, tuple(u0.shape))
+        if hd.get_option("record_adjoint_steps"):
+            ast["dts"] = hd.adjoint_step_sizes().tolist()
+        stats["adjoint"] = ast
+    finally:
+        hd.release_dense(dense)
+    return loss, dp, Solution(list(saveat), u_save, stats)
+
+
 def solve_native_interpolating_adjoint(f, u0, tspan, p, saveat, opt: Tsit5Options) -> Solution:
     stats = {}
     u = _NativeAdjointSolve.apply(f.hd, tspan, list(saveat), opt, stats, p, u0)

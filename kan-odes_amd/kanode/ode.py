@@ -190,6 +190,22 @@ def _step_fused(f, u, p, t, dt, k1, opt: Tsit5Options):
     return unew, ks, eest
 
 
+def _saveat_list(tspan, saveat) -> list:
+    t0, tf = float(tspan[0]), float(tspan[1])
+    if saveat is None:
+        return [t0, tf]
+    if isinstance(saveat, (int, float)):
+        n = int(round((tf - t0) / saveat))
+        return [t0 + i * saveat for i in range(n + 1)]
+    return [float(s) for s in saveat]
+
+
+def native_ok(f, u0: torch.Tensor, tspan, p, saveat: list, opt: Tsit5Options) -> bool:
+    """solve() runs in libkanode (kanode_solve_tsit5 / kanode_adjoint_tsit5) for these arguments."""
+    return (opt.native and hasattr(f, "hd") and isinstance(p, torch.Tensor) and u0.is_cuda and u0.dim() in (1, 2)
+            and float(tspan[1]) > float(tspan[0]) and _ascending(tuple(saveat)))
+
+
 def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Options | None = None,
           sensealg: str = "discrete", dense_record=None) -> Solution:
     """solve(ODEProblem(f, u0, tspan, p), Tsit5(); saveat, abstol, reltol, sensealg) on device tensors.
@@ -202,17 +218,11 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
     dense_record: an adjoint.DenseRecord that receives every accepted step."""
     opt = opt or Tsit5Options()
     t0, tf = float(tspan[0]), float(tspan[1])
-    if saveat is None:
-        saveat = [t0, tf]
-    elif isinstance(saveat, (int, float)):
-        n = int(round((tf - t0) / saveat))
-        saveat = [t0 + i * saveat for i in range(n + 1)]
-    saveat = [float(s) for s in saveat]
+    saveat = _saveat_list(tspan, saveat)
     if sensealg not in ("discrete", "interpolating_adjoint"):
         raise ValueError(f"unknown sensealg {sensealg!r}")
     grad = torch.is_grad_enabled() and (getattr(p, "requires_grad", False) or u0.requires_grad)
-    native = (opt.native and hasattr(f, "hd") and isinstance(p, torch.Tensor) and u0.is_cuda and u0.dim() in (1, 2) and dense_record is None
-              and tf > t0 and _ascending(tuple(saveat)))
+    native = dense_record is None and native_ok(f, u0, tspan, p, saveat, opt)
     if native:
         tol = 1e-12 * max(1.0, abs(tf))
         saveat = [s for s in saveat if s <= tf + tol]
