@@ -595,6 +595,7 @@ def surrogate_dist_bench(dev, rank: int, world: int, backend: str, reps: int = 2
     it = _max_over_ranks((time.perf_counter() - t0) / reps, dev, backend)
     _, _, sol = tr.loss_and_grad()
     out["bu512_tp"] = {"unit": "ms/iteration", "ms_per_iteration": it * 1e3, "ranks": world,
+                       "host": "Python integrator (kanode.tp) over torch.distributed",
                        "grid_shards": tp_size, "data_parallel_groups": n_groups, "ics_per_group": 4,
                        "grid_points_per_rank": tp.n, "sensealg": tr.sensealg,
                        "forward_steps": sol.stats["naccept"],

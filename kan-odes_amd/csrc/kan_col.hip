@@ -1833,12 +1833,9 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
                 const void* fn = hlcs[0].norm == NORM_TANH_FAST
                                      ? reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>)
                                      : reinterpret_cast<const void*>(&kd_chain_adjoint_lvsp_kernel<NORM_SOFTSIGN>);
-                static size_t set_lds[2] = {0, 0};   // (the attribute is raised once per instantiation and size)
-                size_t& cap = set_lds[hlcs[0].norm == NORM_TANH_FAST ? 0 : 1];
-                if (lsp > cap) {
-                    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsp);
+                {
+                    const hipError_t e = ensure_dynamic_lds(fn, lsp);
                     if (e != hipSuccess) return e;
-                    cap = lsp;
                 }
                 if (hlcs[0].norm == NORM_TANH_FAST)
                     hipLaunchKernelGGL((kd_chain_adjoint_lvsp_kernel<NORM_TANH_FAST>), dim3(1), dim3((kLvSpWaves + 1) * kWave),

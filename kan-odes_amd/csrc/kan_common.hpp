@@ -3,11 +3,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "kan_device.hpp"
 
 namespace kan {
+
+// Raise a kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize) on the CURRENT device to
+// at least `lds` bytes.  HIP applies the attribute per device, so the raised sizes are remembered per
+// (kernel, device) under a lock: a second GPU driven from the same process, or two threads, still raise it.
+inline hipError_t ensure_dynamic_lds(const void* fn, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, size_t> raised;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    size_t& cap = raised[{fn, dev}];
+    if (lds <= cap) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess) cap = lds;
+    return e;
+}
 
 constexpr int kBlock = 256;
 constexpr int kWave = 64;

@@ -805,7 +805,7 @@ hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, c
     const void* fn = pa.S == 4    ? reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<4>)
                      : pa.S == 8 ? reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<8>)
                                  : reinterpret_cast<const void*>(&kd_pair_adjoint_kernel<16>);
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = ensure_dynamic_lds(fn, lds);
     if (e != hipSuccess) return e;
     // every workgroup spins on the others at each exchange, so all nwg must be resident at once: launch only
     // when the device's capacity for this kernel (workgroups per CU at this LDS carve x CUs) covers the grid

@@ -201,12 +201,10 @@ hipError_t launch_fk_small_adjoint(const LayerConst& hlc, const PPConst& hpc, co
     const int threads = (int)B * kWave;
 #define KAN_SMALL_ADJ1(NORM, PATH, GT, MAXT)                                                                       \
     do {                                                                                                         \
-        static size_t set_lds_ = 0; /* (the attribute raised once per instantiation and size) */                 \
-        if (lds > set_lds_) {                                                                                    \
+        {                                                                                                        \
             const void* fn = reinterpret_cast<const void*>(&fk_small_adjoint_kernel<NORM, PATH, GT, MAXT>);        \
-            hipError_t e_ = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);       \
+            hipError_t e_ = ensure_dynamic_lds(fn, lds);                                                         \
             if (e_ != hipSuccess) return e_;                                                                     \
-            set_lds_ = lds;                                                                                      \
         }                                                                                                        \
         hipLaunchKernelGGL((fk_small_adjoint_kernel<NORM, PATH, GT, MAXT>), dim3(1), dim3(threads), lds, st, lc, p, \
                            (const double2*)tables, s, B, a, stage_rec);                                          \

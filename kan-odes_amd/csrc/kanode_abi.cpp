@@ -1653,6 +1653,7 @@ kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int6
 }
 void kanode_internal_set_last_adjoint(kanode_handle* h, int path) { h->last_adjoint = path; }
 
+void kanode_internal_clear_adjoint_steps(kanode_handle* h) { h->adj_steps.clear(); }
 std::vector<double>* kanode_internal_adjoint_steps(kanode_handle* h) {
     return h->record_adj_steps ? &h->adj_steps : nullptr;
 }

@@ -119,6 +119,7 @@ int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batc
 // KANODE_OPT_LAST_ADJOINT: record the path kanode_adjoint_tsit5 took (a kanode_adjoint_path value)
 void kanode_internal_set_last_adjoint(kanode_handle* h, int path);
 // KANODE_OPT_RECORD_ADJOINT_STEPS: the handle's record of the accepted adjoint step sizes, or null when off
+void kanode_internal_clear_adjoint_steps(kanode_handle* h);
 std::vector<double>* kanode_internal_adjoint_steps(kanode_handle* h);
 kanode_status kanode_internal_pair_adjoint(kanode_handle* h, const void* p, int64_t batch, kan::PairAdjArgs* a,
                                            void* stream, bool& launched);

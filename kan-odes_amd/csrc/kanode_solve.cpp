@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <string>
 #include <cstdlib>
@@ -360,6 +361,16 @@ struct CtlRange {
     const double* p;
     int n;
 };
+// spin-wait hint for the host polls of mapped control words
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#elif defined(__aarch64__)
+    asm volatile("yield" ::: "memory");
+#else
+    std::atomic_signal_fence(std::memory_order_seq_cst);
+#endif
+}
 kanode_status wait_ctl(kanode_handle* h, hipStream_t st, std::initializer_list<CtlRange> rs) {
     if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "adaptive step control reads the error norm");
     auto ready = [&] {
@@ -377,7 +388,7 @@ kanode_status wait_ctl(kanode_handle* h, hipStream_t st, std::initializer_list<C
             }
             if (q != hipErrorNotReady) SOLVE_HIP(h, q);
         }
-        __builtin_ia32_pause();
+        cpu_relax();
     }
 }
 
@@ -996,21 +1007,45 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
     constexpr int64_t kBatch = 16;
     const size_t sb = s->state_bytes();
     auto& L = s->loop;
-    const int64_t cap = std::min<int64_t>(o.maxiters, (int64_t)1 << 22) + 2 * kBatch + 2;
-    if (L.cap < cap) {
-        SOLVE_HIP(h, hipStreamSynchronize(st));
+    // the slot table and step records grow geometrically with the launches queued (a solve that reaches
+    // maxiters stops on the device's status 2, not on the table size)
+    const int64_t cap_max = o.maxiters + 2 * kBatch + 3;
+    auto grow = [&](int64_t want) -> kanode_status {
+        if (L.cap >= want) return KANODE_OK;
+        int64_t cap = std::max<int64_t>(L.cap, 1024);
+        while (cap < want) cap *= 2;
+        cap = std::max(std::min(cap, cap_max), want);
+        SOLVE_HIP(h, hipStreamSynchronize(st));   // (the queued launches write the old records)
+        void** nslots = nullptr;
+        double* nts = nullptr;
+        void** nh = nullptr;
+        SOLVE_TRY(dev_alloc(h, (void**)&nslots, cap * sizeof(void*), "slot table"));
+        if (kanode_status r = dev_alloc(h, (void**)&nts, 2 * cap * sizeof(double), "step records"); r != KANODE_OK) {
+            (void)hipFree(nslots);
+            return r;
+        }
+        if (hipHostMalloc((void**)&nh, cap * sizeof(void*)) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(nslots);
+            (void)hipFree(nts);
+            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device loop): pinned slot staging");
+        }
+        if (L.cap > 0) {   // keep what is recorded: slots [0, synced), ts | dts (each cap long)
+            SOLVE_HIP(h, hipMemcpy(nslots, L.dslots, L.cap * sizeof(void*), hipMemcpyDeviceToDevice));
+            SOLVE_HIP(h, hipMemcpy(nts, L.ts, L.cap * sizeof(double), hipMemcpyDeviceToDevice));
+            SOLVE_HIP(h, hipMemcpy(nts + cap, L.ts + L.cap, L.cap * sizeof(double), hipMemcpyDeviceToDevice));
+            std::memcpy(nh, L.hslots, L.cap * sizeof(void*));
+        }
         for (void* q : {(void*)L.dslots, (void*)L.ts})
             if (q) (void)hipFree(q);
         if (L.hslots) (void)hipHostFree(L.hslots);
-        L.dslots = nullptr;
-        L.ts = nullptr;
-        L.hslots = nullptr;
-        L.cap = 0;
-        SOLVE_TRY(dev_alloc(h, (void**)&L.dslots, cap * sizeof(void*), "slot table"));
-        SOLVE_TRY(dev_alloc(h, (void**)&L.ts, 2 * cap * sizeof(double), "step records"));
-        SOLVE_HIP(h, hipHostMalloc((void**)&L.hslots, cap * sizeof(void*)));
+        L.dslots = nslots;
+        L.ts = nts;
+        L.hslots = nh;
         L.cap = cap;
-    }
+        return KANODE_OK;
+    };
+    SOLVE_TRY(grow(std::min<int64_t>(cap_max, 4 * kBatch + 3)));
     if (!L.ctl) {
         SOLVE_TRY(dev_alloc(h, (void**)&L.ctl, 2 * sizeof(kan::FkLoopCtl), "loop state"));
         SOLVE_TRY(dev_alloc(h, (void**)&L.parts, 2 * kanode_internal_max_parts() * sizeof(double), "loop partials"));
@@ -1064,8 +1099,14 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
     const volatile kan::FkLoopCtl* mir = L.hmir;
     int64_t queued = 0;
     for (;;) {
-        if (queued + kBatch + 3 > L.cap)
-            return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device loop): step table full");
+        if (queued + kBatch + 3 > L.cap) {
+            if (queued + kBatch + 3 > cap_max)
+                return kanode_internal_fail(h, KANODE_ERR_ALLOC, "Tsit5 (device loop): step table full");
+            SOLVE_TRY(grow(queued + kBatch + 3));
+            la.slots = L.dslots;
+            la.ts = L.ts;
+            la.dts = L.ts + L.cap;
+        }
         // slots for every step the queued launches can reach (each launch advances at most one step; a state
         // names the slots up to its step + 2)
         SOLVE_TRY(ensure_slots(h, s, queued + kBatch + 3, st));
@@ -1087,7 +1128,7 @@ kanode_status solve_fk_loop(kanode_handle* h, const void* p, const void* u0, dou
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) SOLVE_HIP(h, q);
             }
-            __builtin_ia32_pause();
+            cpu_relax();
         }
         if (mir->status != 0) break;
         if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it + 1 < queued - kBatch)
@@ -1255,7 +1296,7 @@ kanode_status adjoint_fk_loop(kanode_handle* h, const void* p, kanode_solution* 
                     if (q == hipSuccess) break;
                     if (q != hipErrorNotReady) SOLVE_HIP(h, q);
                 }
-                __builtin_ia32_pause();
+                cpu_relax();
             }
             if (mir->status != 0) break;
             if (hipStreamQuery(st) == hipSuccess && mir->status == 0 && mir->it < base + queued - kBatch)
@@ -1876,6 +1917,9 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve needs an RHS with N_in == N_out");
     for (int64_t j = 1; j < n_save; ++j)
         if (!(saveat[j] >= saveat[j - 1])) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must ascend");
+    // a stop past tf would never be reached and its rows of u_save would stay unwritten
+    if (n_save > 0 && !(saveat[n_save - 1] <= tf + 1e-12 * std::max(1.0, std::fabs(tf))))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must lie within [t0, tf]");
     hipStream_t st = (hipStream_t)stream;
     const int dtype = kanode_internal_dtype(h);
     const int64_t n = kanode_internal_state_length(h) * batch;
@@ -1981,7 +2025,7 @@ extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, c
     TableHold hold(h);
     bool done = false;
     kanode_internal_set_last_adjoint(h, KANODE_ADJ_NONE);
-    if (std::vector<double>* rec = kanode_internal_adjoint_steps(h)) rec->clear();
+    kanode_internal_clear_adjoint_steps(h);   // recorded or not: no stale sizes from an earlier adjoint
     kanode_status r = s->dtype == KANODE_F64 ? adjoint_fused_t<double>(h, p, s, dl_du, du0, dp, o, stats, st, done)
                                              : adjoint_fused_t<float>(h, p, s, dl_du, du0, dp, o, stats, st, done);
     if (r == KANODE_OK && done) kanode_internal_set_last_adjoint(h, KANODE_ADJ_CHAIN_WG);

@@ -157,6 +157,8 @@ class Trainer:
 
     def loss_and_grad(self):
         sv = _saveat_list(self.tspan, self.saveat)
+        tf = float(self.tspan[1])
+        sv = [s for s in sv if s <= tf + 1e-12 * max(1.0, abs(tf))]     # as solve() filters them
         if (not self.tp and not self.sparse_reg and self.sensealg == "interpolating_adjoint"
                 and tuple(self.target.shape) == (len(sv),) + tuple(self.u0.shape)
                 and native_ok(self.rhs, self.u0, self.tspan, self.p, sv, self.solver)):

@@ -110,3 +110,26 @@ def test_trainer_uses_fused_adam_and_matches_torch_adam():
         assert la == lb
     assert (fused.p - slow.p).abs().max().item() <= 1e-15 * slow.p.abs().max().item()
     assert fused.history[-1] < fused.history[0]
+
+
+def test_trainer_fast_path_filters_saveat_past_tf():
+    """a saveat point past tf is dropped as solve() drops it (not left as unwritten rows of the
+    solution), and kanode_solve_tsit5 itself rejects such a stop."""
+    nx, B = 256, 2
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=1.0 / (nx - 1), D=0.01, device=device())
+    x = np.arange(nx) / (nx - 1)
+    u0 = t(np.stack([(np.tanh((x - c) / 0.02) - np.tanh((x - c - 0.2) / 0.02)) / 2 for c in (0.3, 0.4)]))
+    opt = kanode.Tsit5Options(adaptive=False, dt=5e-4)
+    ptrue = t(np.random.default_rng(2).uniform(-0.5, 0.5, 11))
+    ts = [0.0, 0.05, 0.1]
+    target = kanode.solve(rhs, u0, (0.0, 0.1), ptrue, ts, opt).u
+    p0 = ptrue * 1.1
+    ref = kanode.Trainer(rhs, u0, (0.0, 0.1), ts, target, p0, eta=1e-2, solver=opt)
+    past = kanode.Trainer(rhs, u0, (0.0, 0.1), ts + [0.3], target, p0, eta=1e-2, solver=opt)
+    la, ga, _ = ref.loss_and_grad()
+    lb, gb, _ = past.loss_and_grad()
+    assert float(la) == float(lb)
+    assert torch.equal(ga, gb)
+    with pytest.raises(kanode.KanodeError, match="saveat"):
+        rhs.hd.solve_tsit5(p0, u0, 0.0, 0.1, [0.0, 0.3], opt.to_c())
