@@ -737,6 +737,9 @@ def main() -> None:
                     help="nccl (= RCCL) for one rank per GPU; gloo only to rehearse the multi-rank path")
     ap.add_argument("--no-table", action="store_true",
                     help="per-point basis recurrence instead of the piecewise-polynomial table (kan_pp.hip)")
+    ap.add_argument("--no-shard-ceiling", action="store_true",
+                    help="skip the single-GPU shard_ceiling projection (its smaller-batch launches of the same kernel "
+                         "would mix into a kernel-trace summary of the 1M-trajectory launch)")
     ap.add_argument("--grid-rhs", type=int, default=0,
                     help="tuning: persistent grid of the table RHS kernel (KANODE_OPT_GRID_RHS; 0 = default)")
     args = ap.parse_args()
@@ -840,7 +843,7 @@ def main() -> None:
     total_evals = B * args.steps * world
     value = total_evals / elapsed
     ceiling = None
-    if world == 1 and not weak:
+    if world == 1 and not weak and not args.no_shard_ceiling:
         ceiling = shard_ceiling(rhs, u, du, ps, stream, args.steps, B / (kern_ms * 1e-3))
     alg_bytes = 8.0 * (rhs.P + B * (nx + nx))       # p + u in + du out, per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
