@@ -289,6 +289,74 @@ def lv4096_bench(dev, steps: int = 200):
             "note": f"device time per RHS from a hipGraph of {steps} launches (one fused-chain kernel each)"}
 
 
+def lv_targets(u0: np.ndarray, ts) -> np.ndarray:
+    """The analytic Lotka-Volterra model (LV_driver_KANODE.jl:110-122: α = 1.5, β = 1, γ = 1, δ = 3) from every
+    initial condition of u0 (B, 2), at the times ts: (len(ts), B, 2), one stacked DOP853 solve at 1e-10 / 1e-12."""
+    from scipy.integrate import solve_ivp
+    B = u0.shape[0]
+
+    def f(t, x):
+        a, b = x[:B], x[B:]
+        return np.concatenate([1.5 * a - a * b, a * b - 3.0 * b])
+    y = solve_ivp(f, (0.0, float(ts[-1])), np.concatenate([u0[:, 0], u0[:, 1]]), t_eval=ts, method="DOP853",
+                  rtol=1e-10, atol=1e-12).y            # (2B, len(ts))
+    return np.stack([y[:B].T, y[B:].T], axis=-1)
+
+
+def lv4096_train_bench(dev, with_cpu: bool, reps: int = 10, B: int = 4096, B_cpu: int = 16):
+    """BASELINE configs[1] trained: the LV KAN [2,10,2] G=5 NeuralODE over B = 4096 random initial conditions
+    u0 ~ U[0.5, 2]² (seed 1) as ONE batched ODE (state [2, B], shared adaptive dt and RMS error
+    norm, as a Lux chain on a matrix state in the reference), fp32, tspan (0, 3.5), saveat 0:0.1:3.4 against the
+    analytic LV trajectories of every IC; one LV_driver_KANODE.jl:283-287 iteration = adaptive Tsit5 solve +
+    InterpolatingAdjoint + Adam(5e-4) (Trainer.step).  CPU: the same iteration in C (oracle/cpu_epoch.c, fp64,
+    one core) on the first B_cpu initial conditions (a bounded sample: the step count of a batched ODE depends on
+    its batch), reported per trajectory beside the GPU's."""
+    ts = [0.1 * i for i in range(35)]
+    rng = np.random.default_rng(1)
+    u0n = rng.uniform(0.5, 2.0, (B, 2))
+    target = lv_targets(u0n, ts)
+    chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
+    # a trained network (the round-5 LV anchor run's final parameters, seed 1, 1e5 Adam iterations from [1, 1];
+    # tests/golden/lv_trained_p_seed1.npy): the LV oscillation itself sets the step count, as late in training
+    p0 = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "lv_trained_p_seed1.npy"))
+    rhs = kanode.ChainRHS(chain, dtype=torch.float32, device=dev)
+    u0 = torch.as_tensor(u0n, dtype=torch.float32, device=dev).contiguous()
+    tgt = torch.as_tensor(target, dtype=torch.float32, device=dev).contiguous()
+    tr = kanode.Trainer(rhs, u0, (0.0, 3.5), ts, tgt, torch.as_tensor(p0, dtype=torch.float32, device=dev),
+                        eta=5e-4, sensealg="interpolating_adjoint")
+    tr.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tr.step()
+    torch.cuda.synchronize()
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    _, _, sol = tr.loss_and_grad()
+    out = {"unit": "ms/iteration", "batch": B, "dtype": "f32", "gpu": gpu_ms,
+           "gpu_per_trajectory_us": gpu_ms * 1e3 / B,
+           "forward_steps": sol.stats["naccept"], "adjoint_steps": sol.stats["adjoint"]["naccept"],
+           "adjoint_path": rhs.hd.get_option("last_adjoint"),
+           "what": "configs[1] training iteration: adaptive Tsit5 + InterpolatingAdjoint + Adam(5e-4), LV KAN "
+                   "[2,10,2] G=5, 4096 ICs as one batched ODE, fp32, saveat 0:0.1:3.4 vs the analytic LV model"}
+    if with_cpu:
+        from oracle import oracle as O
+        specs = [O.LayerSpec(2, 10, 5, "tanh_fast"), O.LayerSpec(10, 2, 5, "tanh_fast")]
+        pc = p0.copy()
+        times, st = [], None
+        for r in range(8):
+            t1 = time.perf_counter()
+            _, _, pc, st, _ = O.chain_epoch(specs, pc, u0n[:B_cpu], 3.5, ts, target[:, :B_cpu], eta=5e-4)
+            if r >= 2:
+                times.append(time.perf_counter() - t1)
+        cpu_ms = float(np.median(times)) * 1e3
+        out.update({"cpu": cpu_ms, "cpu_batch": B_cpu, "cpu_cores": 1, "cpu_forward_steps": st["naccept"],
+                    "cpu_per_trajectory_us": cpu_ms * 1e3 / B_cpu,
+                    "cpu_kind": "port (oracle/cpu_epoch.c, fp64, one core; the first 16 ICs as one batched ODE; "
+                                "median of 6 after 2 warm-ups)",
+                    "speedup_per_trajectory": (cpu_ms / B_cpu) / (gpu_ms / B)})
+    return out
+
+
 def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
     """BASELINE configs[0] shape: one LV_driver_KANODE.jl training iteration (KAN [2,10,2] G=5,
     u0 = [1, 1], tspan (0, 3.5), saveat 0:0.1:3.4, adaptive Tsit5 at the default tolerances,
@@ -910,6 +978,7 @@ def main() -> None:
     if rank == 0 and not args.no_vjp:
         out["lv4096"] = lv4096_bench(dev)
         out["lv1_train"] = lv1_train_bench(dev, world == 1 and not args.no_cpu_baseline)
+        out["lv4096_train"] = lv4096_train_bench(dev, world == 1 and not args.no_cpu_baseline)
         out["fk26_train"] = fk26_train_bench(dev, world == 1 and not args.no_cpu_baseline)
         out["surrogates"] = surrogate_bench(dev, world == 1 and not args.no_cpu_baseline)
 
