@@ -361,6 +361,27 @@ kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0
 kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,
                                    const void* dl_du, void* du0, void* dp, const kanode_solver_options* opt,
                                    kanode_solve_stats* stats, void* stream);
+/* Forward sensitivities: SciMLSensitivity 7.69 ForwardDiffSensitivity, the gradient the reference computes for its
+ * small source-term problems (Fisher-KPP_Source.jl:198 and the Allen-Cahn source driver: Zygote.gradient(loss, p)
+ * with no sensealg, length(u0) + length(p) <= 100, so the automatic choice is forward mode over ForwardDiff.Dual
+ * numbers with one partial per parameter).  The solve of u together with S_k = ∂u/∂p_k, the Dual error norm over
+ * value and partials (per entry the scale abstol + reltol·max(‖u_i‖, ‖unew_i‖), ‖x‖² = value² + Σ partials²; the
+ * RMS over n·(1 + P) values), saveat from the same interpolant:
+ *     u_save[n_save, N, B] <- u(saveat[j]);  s_save[n_save, P, N, B] <- ∂u(saveat[j])/∂p   (device, either nullable)
+ * so dL/dp = Σ_j Σ_i ∂L/∂u_i(t_j) · s_save[j, :, i] (the host's contraction, as the Dual pullback's).  Covered: the
+ * pointwise + periodic Laplacian RHS (fp64, rbf, G = 5 or 10, base activation, softsign / tanh_fast) with
+ * nx·batch <= 64, as ONE workgroup (control is ignored); KANODE_ERR_UNSUPPORTED otherwise.  Synchronous (reads the
+ * step counters). */
+kanode_status kanode_forward_sensitivity_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
+                                               double t0, double tf, const double* saveat, int64_t n_save,
+                                               void* u_save, void* s_save, const kanode_solver_options* opt,
+                                               kanode_solve_stats* stats, void* stream);
+/* 1 when kanode_forward_sensitivity_tsit5 covers this handle at `batch` trajectories, else 0 (no GPU work). */
+/* The accepted steps of the handle's last kanode_forward_sensitivity_tsit5 (until the next solve without a dense output
+ * on the handle): ts[i], dts[i] for i < min(count, cap) (host arrays, either NULL); returns the count (the first 4096
+ * steps are recorded), -1 for a NULL handle.  Diagnostics: another solver can replay the same step sequence. */
+int64_t kanode_forward_sensitivity_step_sizes(kanode_handle* h, double* ts, double* dts, int64_t cap);
+int32_t kanode_forward_sensitivity_supported(const kanode_handle* h, int64_t batch);
 /* KANODE_OPT_RECORD_ADJOINT_STEPS: the accepted step sizes of the handle's last kanode_adjoint_tsit5
  * (in backward order), out[i] for i < min(count, cap) (out may be NULL).  Returns the count (0 when not
  * recorded), -1 for NULL. */

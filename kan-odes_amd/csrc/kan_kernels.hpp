@@ -411,6 +411,14 @@ hipError_t launch_fk_small_tsit5(const LayerConst& hlc, const PPConst& hpc, cons
 hipError_t launch_fk_small_adjoint(const LayerConst& hlc, const PPConst& hpc, const LayerConst* lc, const double* p,
                                    const double* tables, const FkSmallArgs& s, int64_t B, const ChainAdjointArgs& a,
                                    hipStream_t st);
+// Forward sensitivities of a small Fisher-KPP field (SciMLSensitivity ForwardDiffSensitivity, kan_small.hip):
+// one workgroup of G + 2 waves (the values and one partial per parameter), Nx·B <= 64 points; u_save [n_save][n],
+// s_save [n_save][P][n].  tab: the PP_PHI / PP_DPHI / PP_SWISH tables (built by the caller) or the reference formula.
+constexpr int kFsensMaxWaves = 16;
+bool fk_small_fsens_supported(const LayerConst& hlc, int Nx, int64_t B);
+hipError_t launch_fk_small_fsens(const LayerConst& hlc, const PPConst& hpc, bool tab, const LayerConst* lc,
+                                 const double* p, const double* tables, const FkSmallArgs& s, const double* u0,
+                                 int64_t B, const ChainSolveArgs& a, double* s_save, hipStream_t st);
 int pair_adjoint_workgroups(const LayerConst* hl, int64_t B, int S);
 hipError_t launch_kd_pair_adjoint(const LayerConst* hl, const LayerConst* dlc, const double* p, int64_t B,
                                   PairAdjArgs pa, hipStream_t st);

@@ -143,6 +143,219 @@ fk_small_adjoint_kernel(const LayerConst* __restrict__ lcp, const double* __rest
     onewg_adjoint<double>(m, a, mu, km, tsl, dtsl, red, recl);
 }
 
+
+// ---- forward sensitivities (SciMLSensitivity 7.69 ForwardDiffSensitivity) ---------------------------------
+// The reference's Fisher-KPP gradient at its own size: Zygote.gradient(x -> loss(x), p) with no sensealg
+// (Fisher-KPP_Source.jl:198; the Allen-Cahn source driver likewise).  With length(u0) + length(p) = 26 + 11
+// <= 100 SciMLSensitivity picks ForwardDiffSensitivity: the solve runs over ForwardDiff.Dual numbers with one
+// partial per parameter (chunk = P = 11), i.e. over the state [u; S_1..S_P], S_k = ∂u/∂p_k, with
+//     S_k' = (D lap) S_k + φ'(u) S_k + ∂φ/∂p_k(u),   ∂φ/∂C_k = B_k(N(u)),  ∂φ/∂W = swish(u)
+// (kdense.jl:116-124), integrated by the same Tsit5 (third-party semantics, restated from the pinned
+// SciMLSensitivity 7.69 / DiffEqBase / OrdinaryDiffEq 6.89; verify where Julia exists).  What the Dual solve
+// changes in the step control: DiffEqBase's ODE_DEFAULT_NORM over Dual numbers counts the partials.  The
+// residual scale of state entry i is abstol + reltol·max(‖u_i‖, ‖unew_i‖) with ‖x‖ = sqrt(value² + Σ_k
+// partial_k²) (calculate_residuals calls the scalar Dual norm), the residual's value and partials are divided by
+// it, and EEst = sqrt(Σ_i (value² + Σ_k partial_k²) / (n·(1 + P))); the Hairer-Wanner initial step takes the same
+// norms; saveat values and partials come from the same interpolant.
+//
+// Layout: wave 0 carries the values, wave 1 + k the partial S_k (k < G: C_k, k = G: W); lane l is point l % Nx
+// of trajectory l / Nx (Nx·B <= 64).  Every wave integrates the values too (the same instructions on the same
+// inputs, so the same bits in every wave): no wave waits on another within a step.  The exchanges are the
+// per-entry Dual norms (one LDS round per step) and the error norm's block sum.  TAB: φ, φ' and swish from the
+// piecewise-polynomial tables (PP_PHI, PP_DPHI, PP_SWISH staged in LDS, the reference formula off the table);
+// otherwise the reference formula throughout (odd Nx, table path off).
+template <int NORM, int GT, bool TAB>
+__global__ void __launch_bounds__((GT + 2) * kWave)
+fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ p,
+                      const double2* __restrict__ tables, FkSmallArgs s, const double* __restrict__ u0, int64_t B,
+                      ChainSolveArgs a, double* __restrict__ s_save) {
+    using K = Tsit5Tab;
+    extern __shared__ double2 tl[];
+    __shared__ double red[kFsensMaxWaves];
+    const int tsz = TAB ? (kPPCoef / 2) * s.ni : 0;
+    if constexpr (TAB) {
+        const int fns[3] = {PP_PHI, PP_DPHI, PP_SWISH};
+        stage_tables(tl, tables, s.ni, fns, 3);
+    }
+    double* __restrict__ xv = reinterpret_cast<double*>(tl + 3 * tsz);   // [waves][64] per-entry exchange
+    KAN_EXP_TABLE_LDS(tab);   // (its barrier also publishes the tables)
+    const Math<double> M{tab};
+    const LayerConst& lc = *lcp;
+    constexpr int P = GT + 1;
+    const int w = threadIdx.x / kWave, l = threadIdx.x & (kWave - 1);
+    const int nw = (int)(blockDim.x / kWave);
+    const int Nx = s.Nx;
+    const int64_t n = (int64_t)Nx * B;
+    const bool act = l < n;
+    const int j = l % Nx, b0 = l - j;
+    const int jm = act ? b0 + (j + Nx - 1) % Nx : l, jp = act ? b0 + (j + 1) % Nx : l;
+    const bool sens = w > 0;   // (wave-uniform)
+    const int kq = w - 1;
+    const double2* tphi = tl;
+    const double2* tdphi = tl + tsz;
+    const double2* tsw = tl + 2 * tsz;
+    auto lap = [&](double v) -> double {
+        const double um = __shfl(v, jm, kWave), up = __shfl(v, jp, kWave);
+        return lap3<double>(um, v, up, j, Nx, s.cd, s.co);
+    };
+    // f(y) = (D lap y) + φ(y)   (FkSmallModel::rhs)
+    auto fu = [&](double y) -> double {
+        const double lp = lap(y);
+        double k = 0.0;
+        bool ok = false;
+        if constexpr (TAB) k = pp_eval(tphi, s.ni, s.inv_w, s.x0, y, ok);
+        if (!ok) {
+            double sc;
+            k = pp_direct<NORM, BASIS_RBF>(M, lc, p, lc.grid, y, sc);
+        }
+        return lp + k;
+    };
+    // partial kq of f at the Dual (y, sv): ((D lap) sv + sv φ'(y)) + ∂φ/∂p_kq(y)
+    auto fs = [&](double y, double sv) -> double {
+        const double lp = lap(sv);
+        double dphi = 0.0, sw = 0.0;
+        bool ok = false;
+        if constexpr (TAB) ok = pp_eval2<true>(tdphi, tsw, s.ni, s.inv_w, s.x0, y, dphi, sw);
+        if (!ok) pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, y, dphi, sw);
+        double dp = sw;
+        if (kq < GT) {
+            const double nn = normalize<NORM, double>(M, lc.norm, y);
+            const double z = (nn - (double)lc.grid[kq]) * (double)lc.invh;
+            double aux;
+            dp = basis_direct<double>(M, BASIS_RBF, z, aux);
+        }
+        return (lp + sv * dphi) + dp;
+    };
+    // Σ over the waves of v at this lane's entry (value first, then the partials in order: the entry's Dual
+    // sse), the same total in every wave
+    auto pt_sum = [&](double v) -> double {
+        xv[w * kWave + l] = v;
+        __syncthreads();
+        double t = xv[l];
+        for (int q = 1; q < nw; ++q) t += xv[q * kWave + l];
+        __syncthreads();
+        return t;
+    };
+    auto bsum = [&](double v) -> double { return onewg_bsum(act ? v : 0.0, red); };
+    double* __restrict__ usave = reinterpret_cast<double*>(a.u_save);
+    auto put = [&](int64_t si, double v) {
+        if (!act) return;
+        if (!sens) {
+            if (usave) usave[si * n + l] = v;
+        } else if (s_save) {
+            s_save[(si * P + kq) * n + l] = v;
+        }
+    };
+    double u = act ? u0[l] : 0.0, S = 0.0;
+    double k[7], kS[7];
+    k[0] = fu(u);
+    kS[0] = sens ? fs(u, S) : 0.0;
+    const double t0 = a.t0, tf = a.tf;
+    const double ntot = (double)n * (double)(P + 1);
+    int64_t si = 0;
+    while (si < a.n_save && a.saveat[si] <= t0 + 1e-14 * ::fmax(1.0, ::fabs(t0))) {
+        put(si, sens ? S : u);
+        ++si;
+    }
+    double nrm = 0.0;   // ‖u_i‖ of this lane's entry (the Dual norm over value and partials)
+    if (a.adaptive) {
+        const double v = sens ? S : u;
+        nrm = ::sqrt(pt_sum(act ? v * v : 0.0));
+    }
+    double dt = a.dt;
+    if (a.adaptive && !(a.dt > 0)) {   // Hairer & Wanner over the Dual state
+        const double sk = ::fma(a.reltol, nrm, a.abstol);
+        const double e0 = (sens ? S : u) / sk, e1 = (sens ? kS[0] : k[0]) / sk;
+        const double d0 = ::sqrt(bsum(e0 * e0) / ntot);
+        const double d1 = ::sqrt(bsum(e1 * e1) / ntot);
+        double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        dt0 = ::fmin(dt0, tf - t0);
+        const double y1 = ::fma(dt0, k[0], u);
+        const double f1 = fu(y1);
+        const double g1 = sens ? fs(y1, ::fma(dt0, kS[0], S)) : 0.0;
+        const double e = ::fma(-1.0, sens ? kS[0] : k[0], sens ? g1 : f1) / sk;
+        const double d2 = ::sqrt(bsum(e * e) / ntot) / dt0;
+        const double mx = ::fmax(d1, d2);
+        const double dt1 = mx <= 1e-15 ? ::fmax(1e-6, dt0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
+        dt = ::fmin(::fmin(100 * dt0, dt1), tf - t0);
+    }
+    double qold = a.qoldinit, t = t0;
+    int64_t naccept = 0, nreject = 0, nf = 0, it = 0, status = 0;
+    for (; it < a.maxiters; ++it) {
+        if (t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf))) break;
+        dt = ::fmin(dt, tf - t);
+        double y = u, ys = S;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            y = u;
+            ys = S;
+#pragma unroll
+            for (int q = 0; q <= i; ++q) {
+                y = ::fma(dt * K::TA[i][q], k[q], y);
+                ys = ::fma(dt * K::TA[i][q], kS[q], ys);
+            }
+            k[i + 1] = fu(y);
+            kS[i + 1] = sens ? fs(y, ys) : 0.0;
+        }
+        nf += 6;
+        double dtnew = dt, nn = nrm;
+        if (a.adaptive) {
+            double ev = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) ev = ::fma(dt * K::BT[q], sens ? kS[q] : k[q], ev);
+            const double e = ::fma(dt * K::BT[6], sens ? kS[6] : k[6], ev);
+            const double yn = sens ? ys : y;
+            nn = ::sqrt(pt_sum(act ? yn * yn : 0.0));
+            const double sk = ::fma(a.reltol, ::fmax(nrm, nn), a.abstol);
+            const double r = e / sk;
+            const double eest = ::sqrt(bsum(r * r) / ntot);
+            const double q11 = eest > 0 ? ::pow(eest, a.beta1) : 0.0;
+            if (eest > 1.0 && dt > a.dtmin) {
+                ++nreject;
+                dt = dt / ::fmin(1.0 / a.qmin, q11 / a.gamma);
+                continue;
+            }
+            double q = q11 / ::pow(qold, a.beta2);
+            q = ::fmax(1.0 / a.qmax, ::fmin(1.0 / a.qmin, q / a.gamma));
+            if (1.0 <= q && q <= 1.0) q = 1.0;   // qsteady_min = qsteady_max = 1
+            dtnew = q > 0 ? dt / q : dt * a.qmax;
+            qold = ::fmax(eest, a.qoldinit);
+        }
+        const double tn = t + dt;
+        while (si < a.n_save && a.saveat[si] <= tn + 1e-12 * ::fmax(1.0, ::fabs(tn))) {
+            const double tsv = a.saveat[si];
+            double v = sens ? ys : y;
+            if (!(::fabs(tsv - tn) <= 1e-12 * ::fmax(1.0, ::fabs(tn)))) {
+                double wt[7];
+                tsit5_interp_weights((tsv - t) / dt, wt);
+                v = sens ? S : u;
+#pragma unroll
+                for (int q = 0; q < 7; ++q) v = ::fma(wt[q] * dt, sens ? kS[q] : k[q], v);
+            }
+            put(si, v);
+            ++si;
+        }
+        if (a.ts && threadIdx.x == 0 && naccept < a.cap) {   // the accepted steps (diagnostics: step-size replay)
+            a.ts[naccept] = t;
+            a.dts[naccept] = dt;
+        }
+        u = y;   // commit (value and partials), FSAL
+        S = ys;
+        k[0] = k[6];
+        kS[0] = kS[6];
+        nrm = nn;
+        t = tn;
+        ++naccept;
+        dt = dtnew;
+    }
+    if (it == a.maxiters && !(t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf)))) status = 1;
+    if (threadIdx.x == 0) {
+        a.out[0] = naccept;
+        a.out[1] = nreject;
+        a.out[2] = nf + 1;
+        a.out[3] = status;
+    }
+}
 }  // namespace
 
 bool fk_small_supported(const LayerConst& hlc, const PPConst& hpc, int Nx, int64_t B) {
@@ -220,5 +433,41 @@ hipError_t launch_fk_small_adjoint(const LayerConst& hlc, const PPConst& hpc, co
     return hipGetLastError();
 }
 #undef KAN_SMALL_GO
+
+bool fk_small_fsens_supported(const LayerConst& hlc, int Nx, int64_t B) {
+    const int P = hlc.G + 1;
+    return Nx >= 3 && B >= 1 && (int64_t)Nx * B <= kWave && P + 1 <= kFsensMaxWaves && hlc.basis == BASIS_RBF &&
+           hlc.use_base && (hlc.G == 10 || hlc.G == 5) && (hlc.norm == NORM_SOFTSIGN || hlc.norm == NORM_TANH_FAST);
+}
+
+hipError_t launch_fk_small_fsens(const LayerConst& hlc, const PPConst& hpc, bool tab, const LayerConst* lc,
+                                 const double* p, const double* tables, const FkSmallArgs& s, const double* u0,
+                                 int64_t B, const ChainSolveArgs& a, double* s_save, hipStream_t st) {
+    if (!fk_small_fsens_supported(hlc, s.Nx, B) || (tab && (!hpc.enabled || s.ni != hpc.ni || !tables)))
+        return hipErrorNotSupported;
+    const int threads = (hlc.G + 2) * kWave;
+    const size_t lds = (tab ? 3 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni : 0) +
+                       sizeof(double) * (size_t)kFsensMaxWaves * kWave;
+#define KAN_FSENS1(NORM, GT, TAB)                                                                                  \
+    do {                                                                                                         \
+        const void* fn = reinterpret_cast<const void*>(&fk_small_fsens_kernel<NORM, GT, TAB>);                   \
+        hipError_t e_ = ensure_dynamic_lds(fn, lds);                                                             \
+        if (e_ != hipSuccess) return e_;                                                                         \
+        hipLaunchKernelGGL((fk_small_fsens_kernel<NORM, GT, TAB>), dim3(1), dim3(threads), lds, st, lc, p,         \
+                           (const double2*)tables, s, u0, B, a, s_save);                                         \
+    } while (0)
+#define KAN_FSENS(NORM, GT)                                                                                        \
+    do {                                                                                                         \
+        if (tab) KAN_FSENS1(NORM, GT, true);                                                                     \
+        else KAN_FSENS1(NORM, GT, false);                                                                        \
+    } while (0)
+    if (hlc.G == 10 && hlc.norm == NORM_SOFTSIGN) KAN_FSENS(NORM_SOFTSIGN, 10);
+    else if (hlc.G == 10) KAN_FSENS(NORM_TANH_FAST, 10);
+    else if (hlc.norm == NORM_SOFTSIGN) KAN_FSENS(NORM_SOFTSIGN, 5);
+    else KAN_FSENS(NORM_TANH_FAST, 5);
+#undef KAN_FSENS
+#undef KAN_FSENS1
+    return hipGetLastError();
+}
 
 }  // namespace kan

@@ -1667,6 +1667,27 @@ extern "C" int64_t kanode_adjoint_step_sizes(const kanode_handle* h, double* out
 int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batch) {
     return kan::pair_adjoint_workgroups(h->hlc, batch, h->pair_persist_s);
 }
+// forward sensitivities of a small Fisher-KPP field (kan_small.hip fk_small_fsens_kernel)
+bool kanode_internal_fsens_ok(const kanode_handle* h, int64_t batch) {
+    return h->spec.rhs_kind == KANODE_RHS_POINTWISE_PERIODIC_LAPLACIAN && h->spec.dtype == KANODE_F64 &&
+           kan::fk_small_fsens_supported(h->hlc[0], (int)h->spec.nx, batch);
+}
+kanode_status kanode_internal_fk_fsens(kanode_handle* h, const void* p, const void* u0, int64_t batch,
+                                       const kan::ChainSolveArgs* a, void* s_save, void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const bool tab = h->pp_on && h->hpc.enabled;
+    if (tab) {
+        const int fns[3] = {kan::PP_PHI, kan::PP_DPHI, kan::PP_SWISH};
+        HIP_TRY(h, kan::launch_fk_pp_build(h->hpc, h->dlc, h->dpc, (const double*)p, h->dtable, fns, 3, st));
+    }
+    const hipError_t e = kan::launch_fk_small_fsens(h->hlc[0], h->hpc, tab, h->dlc, (const double*)p,
+                                                    tab ? h->dtable : nullptr, fk_small_args(h), (const double*)u0,
+                                                    batch, *a, (double*)s_save, st);
+    if (e == hipErrorNotSupported)
+        return fail(h, KANODE_ERR_UNSUPPORTED, "forward sensitivities: shape not covered by the one-workgroup kernel");
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_fk_small_fsens: ") + hipGetErrorString(e));
+    return KANODE_OK;
+}
 kanode_status kanode_internal_chain_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch,
                                           const kan::ChainSolveArgs* a, void* stream, bool& launched) {
     launched = false;

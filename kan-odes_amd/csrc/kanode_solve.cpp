@@ -1902,31 +1902,11 @@ kanode_status check_opts(kanode_handle* h, const kanode_solver_options& o) {
     return KANODE_OK;
 }
 
-}  // namespace
-
-extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch, double t0,
-                                            double tf, const double* saveat, int64_t n_save, void* u_save,
-                                            const kanode_solver_options* opt, kanode_solution** dense,
-                                            kanode_solve_stats* stats, void* stream) {
-    SOLVE_TRY(kanode_internal_check(h));
-    const kanode_solver_options o = resolved(opt);
-    SOLVE_TRY(check_opts(h, o));
-    if (!p || !u0 || batch < 1 || !(tf > t0) || n_save < 0 || (n_save > 0 && (!saveat || !u_save)))
-        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve: null pointer, batch < 1 or tf <= t0");
-    if (!kanode_internal_square(h))
-        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve needs an RHS with N_in == N_out");
-    for (int64_t j = 1; j < n_save; ++j)
-        if (!(saveat[j] >= saveat[j - 1])) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must ascend");
-    // a stop past tf would never be reached and its rows of u_save would stay unwritten
-    if (n_save > 0 && !(saveat[n_save - 1] <= tf + 1e-12 * std::max(1.0, std::fabs(tf))))
-        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must lie within [t0, tf]");
-    hipStream_t st = (hipStream_t)stream;
-    const int dtype = kanode_internal_dtype(h);
-    const int64_t n = kanode_internal_state_length(h) * batch;
-    // without a dense output the handle keeps the solve's storage (and any cached graph) for the next call
-    const bool record = dense != nullptr;
-    kanode_solution** slot = record ? dense : (kanode_solution**)kanode_internal_solution_cache(h);
-    kanode_solution* s = *slot;
+// The solution object in *slot for a state of n entries (reused when its shape matches, else made anew): its
+// k1_0, control scalars (mapped pinned where the platform allows) and error-partials staging.
+kanode_status acquire_solution(kanode_handle* h, kanode_solution** slot, int64_t n, int dtype, bool record,
+                               hipStream_t st, kanode_solution*& s) {
+    s = *slot;
     if (s && (s->h != h || s->n != n || s->dtype != dtype || s->record != record)) {
         // storage of another shape: start over
         if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "dense output of another shape");
@@ -1965,6 +1945,36 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         if (!s->hparts) s->mparts = nullptr;   // the final-reduction launch then sums them
         else arm_ctl(s->hparts, kanode_internal_max_parts());
     }
+    *slot = s;
+    return KANODE_OK;
+}
+
+}  // namespace
+
+extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, const void* u0, int64_t batch, double t0,
+                                            double tf, const double* saveat, int64_t n_save, void* u_save,
+                                            const kanode_solver_options* opt, kanode_solution** dense,
+                                            kanode_solve_stats* stats, void* stream) {
+    SOLVE_TRY(kanode_internal_check(h));
+    const kanode_solver_options o = resolved(opt);
+    SOLVE_TRY(check_opts(h, o));
+    if (!p || !u0 || batch < 1 || !(tf > t0) || n_save < 0 || (n_save > 0 && (!saveat || !u_save)))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve: null pointer, batch < 1 or tf <= t0");
+    if (!kanode_internal_square(h))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "solve needs an RHS with N_in == N_out");
+    for (int64_t j = 1; j < n_save; ++j)
+        if (!(saveat[j] >= saveat[j - 1])) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must ascend");
+    // a stop past tf would never be reached and its rows of u_save would stay unwritten
+    if (n_save > 0 && !(saveat[n_save - 1] <= tf + 1e-12 * std::max(1.0, std::fabs(tf))))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must lie within [t0, tf]");
+    hipStream_t st = (hipStream_t)stream;
+    const int dtype = kanode_internal_dtype(h);
+    const int64_t n = kanode_internal_state_length(h) * batch;
+    // without a dense output the handle keeps the solve's storage (and any cached graph) for the next call
+    const bool record = dense != nullptr;
+    kanode_solution** slot = record ? dense : (kanode_solution**)kanode_internal_solution_cache(h);
+    kanode_solution* s = nullptr;
+    SOLVE_TRY(acquire_solution(h, slot, n, dtype, record, st, s));
     s->batch = batch;
     s->t0 = t0;
     s->tf = tf;
@@ -2008,6 +2018,120 @@ extern "C" kanode_status kanode_solve_tsit5(kanode_handle* h, const void* p, con
         *slot = nullptr;
     }
     return r;
+}
+
+extern "C" int64_t kanode_forward_sensitivity_step_sizes(kanode_handle* h, double* ts, double* dts, int64_t cap) {
+    if (!h) return -1;
+    const kanode_solution* s = *(kanode_solution**)kanode_internal_solution_cache(h);
+    if (!s) return 0;
+    const int64_t n = (int64_t)s->ts.size();
+    const int64_t m = std::min(n, cap);
+    if (ts && m > 0) std::memcpy(ts, s->ts.data(), (size_t)m * sizeof(double));
+    if (dts && m > 0) std::memcpy(dts, s->dts.data(), (size_t)m * sizeof(double));
+    return n;
+}
+
+extern "C" int32_t kanode_forward_sensitivity_supported(const kanode_handle* h, int64_t batch) {
+    return h && batch >= 1 && kanode_internal_fsens_ok(h, batch) ? 1 : 0;
+}
+
+extern "C" kanode_status kanode_forward_sensitivity_tsit5(kanode_handle* h, const void* p, const void* u0,
+                                                           int64_t batch, double t0, double tf, const double* saveat,
+                                                           int64_t n_save, void* u_save, void* s_save,
+                                                           const kanode_solver_options* opt, kanode_solve_stats* stats,
+                                                           void* stream) {
+    SOLVE_TRY(kanode_internal_check(h));
+    const kanode_solver_options o = resolved(opt);
+    SOLVE_TRY(check_opts(h, o));
+    if (!p || !u0 || batch < 1 || !(tf > t0) || n_save < 0 || (n_save > 0 && !saveat))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "forward sensitivities: null pointer, batch < 1 or tf <= t0");
+    if (!kanode_internal_square(h))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "forward sensitivities need an RHS with N_in == N_out");
+    for (int64_t j = 1; j < n_save; ++j)
+        if (!(saveat[j] >= saveat[j - 1])) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must ascend");
+    if (n_save > 0 && !(saveat[n_save - 1] <= tf + 1e-12 * std::max(1.0, std::fabs(tf))))
+        return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "saveat must lie within [t0, tf]");
+    if (!kanode_internal_fsens_ok(h, batch))
+        return kanode_internal_fail(h, KANODE_ERR_UNSUPPORTED,
+                                    "forward sensitivities: a Fisher-KPP (pointwise + periodic Laplacian) fp64 RHS with "
+                                    "nx * batch <= 64, rbf basis, G = 5 or 10, base activation, softsign / tanh_fast");
+    hipStream_t st = (hipStream_t)stream;
+    if (capturing(st)) return kanode_internal_fail(h, KANODE_ERR_CAPTURE, "forward sensitivities read their counters");
+    const int64_t n = kanode_internal_state_length(h) * batch;
+    kanode_solution** slot = (kanode_solution**)kanode_internal_solution_cache(h);
+    kanode_solution* s = nullptr;
+    SOLVE_TRY(acquire_solution(h, slot, n, KANODE_F64, false, st, s));
+    SOLVE_TRY(ctl_begin(h, s, st));
+    auto& f = s->fused;
+    if (f.saveat_cap < n_save) {
+        if (f.saveat) (void)hipFree(f.saveat);
+        f.saveat = nullptr;
+        f.saveat_cap = 0;
+        SOLVE_HIP(h, hipMalloc((void**)&f.saveat, (size_t)n_save * sizeof(double)));
+        f.saveat_cap = n_save;
+    }
+    if (!f.out) SOLVE_HIP(h, hipMalloc((void**)&f.out, 4 * sizeof(int64_t)));
+    if (n_save > 0) SOLVE_TRY(staged_upload(h, s, f.saveat, saveat, (size_t)n_save * sizeof(double), st));
+    // the accepted step times / sizes (up to kFsensSteps), read back with the counters
+    constexpr int64_t kFsensSteps = 4096;
+    if (f.ts_cap < kFsensSteps) {
+        if (f.ts) (void)hipFree(f.ts);
+        f.ts = nullptr;
+        f.ts_cap = 0;
+        SOLVE_HIP(h, hipMalloc((void**)&f.ts, 2 * (size_t)kFsensSteps * sizeof(double)));
+        f.ts_cap = kFsensSteps;
+    }
+    if (f.hts_cap < f.ts_cap) {
+        if (f.hts) (void)hipHostFree(f.hts);
+        f.hts = nullptr;
+        f.hts_cap = 0;
+        SOLVE_HIP(h, hipHostMalloc((void**)&f.hts, 2 * (size_t)f.ts_cap * sizeof(double)));
+        f.hts_cap = f.ts_cap;
+    }
+    kan::ChainSolveArgs a{};
+    a.cap = f.ts_cap;
+    a.ts = f.ts;
+    a.dts = f.ts + f.ts_cap;
+    a.t0 = t0;
+    a.tf = tf;
+    a.dt = o.dt;
+    a.abstol = o.abstol;
+    a.reltol = o.reltol;
+    a.dtmin = o.dtmin;
+    a.beta1 = o.beta1;
+    a.beta2 = o.beta2;
+    a.gamma = o.gamma;
+    a.qmin = o.qmin;
+    a.qmax = o.qmax;
+    a.qoldinit = o.qoldinit;
+    a.adaptive = o.adaptive ? 1 : 0;
+    a.maxiters = o.maxiters;
+    a.n_save = n_save;
+    a.saveat = f.saveat;
+    a.u_save = n_save > 0 ? u_save : nullptr;
+    a.out = f.out;
+    kanode_status r = kanode_internal_fk_fsens(h, p, u0, batch, &a, n_save > 0 ? s_save : nullptr, st);
+    if (r != KANODE_OK) {
+        s->ctl_dirty = true;
+        return r;
+    }
+    SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipMemcpyAsync(f.hts, f.ts, 2 * (size_t)f.ts_cap * sizeof(double), hipMemcpyDeviceToHost, st));
+    SOLVE_HIP(h, hipStreamSynchronize(st));
+    int64_t res[4];
+    std::memcpy(res, s->hscal, sizeof(res));
+    if (res[3] == 1) return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "Tsit5: maxiters reached");
+    const int64_t nrec = std::min<int64_t>(res[0], f.ts_cap);
+    s->t0 = t0;
+    s->tf = tf;
+    s->ts.assign(f.hts, f.hts + nrec);
+    s->dts.assign(f.hts + f.ts_cap, f.hts + f.ts_cap + nrec);
+    if (stats) {
+        stats->naccept = res[0];
+        stats->nreject = res[1];
+        stats->nf = res[2];
+    }
+    return KANODE_OK;
 }
 
 extern "C" kanode_status kanode_adjoint_tsit5(kanode_handle* h, const void* p, const kanode_solution* dense,

@@ -312,13 +312,7 @@ class KanodeHandle:
         self._check_t(u0, None, "u0")
         if u0.numel() != B * self.N or self.N_out != self.N:
             raise ValueError("solve needs u0 of B x N entries and an RHS with N_in == N_out")
-        key = tuple(saveat)
-        cache = self.__dict__.setdefault("_saveat_c", {})
-        sv = cache.get(key)
-        if sv is None:   # (the C array of a saveat list, kept: training solves pass the same list every step)
-            if len(cache) >= 16:
-                cache.clear()
-            sv = cache[key] = (C.c_double * max(1, len(saveat)))(*[float(x) for x in saveat])
+        sv = self._saveat_c(saveat)
         u_save = torch.empty((len(saveat),) + tuple(u0.shape), dtype=self.dtype, device=self.device)
         st = L.SolveStatsC()
         dense = None
@@ -330,6 +324,47 @@ class KanodeHandle:
                                            _ptr(u_save), C.byref(opts), dptr, C.byref(st), _stream(self.device)),
                 self._h, "kanode_solve_tsit5")
         return u_save, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf), dense
+
+    def _saveat_c(self, saveat):
+        key = tuple(saveat)
+        cache = self.__dict__.setdefault("_saveat_cache", {})
+        sv = cache.get(key)
+        if sv is None:   # (the C array of a saveat list, kept: training solves pass the same list every step)
+            if len(cache) >= 16:
+                cache.clear()
+            sv = cache[key] = (C.c_double * max(1, len(saveat)))(*[float(x) for x in saveat])
+        return sv
+
+    def forward_sensitivity_supported(self, batch: int) -> bool:
+        """kanode_forward_sensitivity_supported: the one-workgroup forward-sensitivity solve covers this batch."""
+        return bool(L.lib().kanode_forward_sensitivity_supported(self._h, int(batch)))
+
+    def forward_sensitivity_step_sizes(self):
+        """(t_n, dt_n) of the accepted steps of the last forward_sensitivity_tsit5 (float64 numpy arrays)."""
+        n = int(L.lib().kanode_forward_sensitivity_step_sizes(self._h, None, None, 0))
+        ts, dts = np.zeros(max(n, 0)), np.zeros(max(n, 0))
+        if n > 0:
+            L.lib().kanode_forward_sensitivity_step_sizes(self._h, ts.ctypes.data, dts.ctypes.data, n)
+        return ts, dts
+
+    def forward_sensitivity_tsit5(self, p: torch.Tensor, u0: torch.Tensor, t0: float, tf: float, saveat,
+                                  opts: "L.SolverOptsC"):
+        """ForwardDiffSensitivity's solve (kanode_forward_sensitivity_tsit5): (u_save (n_save, *u0.shape),
+        s_save (n_save, P, *u0.shape) = ∂u(saveat)/∂p, stats dict)."""
+        B = u0.shape[0] if u0.dim() == 2 else 1
+        self._check_t(p, (self.P,), "p")
+        self._check_t(u0, None, "u0")
+        if u0.numel() != B * self.N:
+            raise ValueError("forward sensitivities need u0 of B x N entries")
+        sv = self._saveat_c(saveat)
+        u_save = torch.empty((len(saveat),) + tuple(u0.shape), dtype=self.dtype, device=self.device)
+        s_save = torch.empty((len(saveat), self.P) + tuple(u0.shape), dtype=self.dtype, device=self.device)
+        st = L.SolveStatsC()
+        L.check(L.lib().kanode_forward_sensitivity_tsit5(self._h, _ptr(p), _ptr(u0), B, float(t0), float(tf), sv,
+                                                         len(saveat), _ptr(u_save), _ptr(s_save), C.byref(opts),
+                                                         C.byref(st), _stream(self.device)),
+                self._h, "kanode_forward_sensitivity_tsit5")
+        return u_save, s_save, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf)
 
     def adjoint_tsit5(self, p: torch.Tensor, dense: "DenseOutput", dl_du: torch.Tensor, opts: "L.SolverOptsC",
                       u_shape):

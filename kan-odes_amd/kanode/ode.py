@@ -214,18 +214,33 @@ def solve(f, u0: torch.Tensor, tspan, p: torch.Tensor, saveat=None, opt: Tsit5Op
     Differentiable w.r.t. u0 and p when f is (kanode RHS objects are):
       sensealg="discrete"              reverse mode through every stage (discrete adjoint);
       sensealg="interpolating_adjoint" SciMLSensitivity's InterpolatingAdjoint, the reference's
-                                       default (kanode.adjoint; f needs `vjp_stage`).
+                                       default (kanode.adjoint; f needs `vjp_stage`);
+      sensealg="forward"               ForwardDiffSensitivity (gradient w.r.t. p; the native one-workgroup
+                                       forward-sensitivity solve of a small Fisher-KPP field);
+      sensealg="auto"                  SciMLSensitivity's automatic choice for a hand-written ODEProblem:
+                                       "forward" where length(u0) + length(p) <= 100 and covered, else
+                                       "interpolating_adjoint".
     dense_record: an adjoint.DenseRecord that receives every accepted step."""
     opt = opt or Tsit5Options()
     t0, tf = float(tspan[0]), float(tspan[1])
     saveat = _saveat_list(tspan, saveat)
-    if sensealg not in ("discrete", "interpolating_adjoint"):
+    if sensealg not in ("discrete", "interpolating_adjoint", "forward", "auto"):
         raise ValueError(f"unknown sensealg {sensealg!r}")
     grad = torch.is_grad_enabled() and (getattr(p, "requires_grad", False) or u0.requires_grad)
     native = dense_record is None and native_ok(f, u0, tspan, p, saveat, opt)
     if native:
         tol = 1e-12 * max(1.0, abs(tf))
         saveat = [s for s in saveat if s <= tf + tol]
+    if sensealg == "auto":   # SciMLSensitivity's automatic choice for a hand-written ODEProblem (adjoint.forward_ok)
+        from .adjoint import forward_ok
+        sensealg = "forward" if native and forward_ok(f, u0, p) else "interpolating_adjoint"
+    if sensealg == "forward" and grad:
+        from .adjoint import forward_ok, solve_forward_sensitivity
+        hd = getattr(f, "hd", None)
+        if not native or hd is None or not hd.forward_sensitivity_supported(u0.shape[0] if u0.dim() == 2 else 1):
+            raise ValueError("sensealg='forward' needs the native forward-sensitivity solve (a small Fisher-KPP field, "
+                             "kanode_forward_sensitivity_supported)")
+        return solve_forward_sensitivity(f, u0, tspan, p, saveat, opt)
     if sensealg == "interpolating_adjoint" and grad:
         if native:
             from .adjoint import solve_native_interpolating_adjoint

@@ -133,7 +133,13 @@ def fisher_kpp_laplacian(nx: int, dx: float) -> np.ndarray:
 
 
 class FisherKPPRHS:
-    """rc_kanode: du = D * lap * u + KDense(1,1,G).(u) pointwise, u (B, Nx) [Julia u[Nx, B]]."""
+    """rc_kanode: du = D * lap * u + KDense(1,1,G).(u) pointwise, u (B, Nx) [Julia u[Nx, B]].
+
+    A hand-written ODEProblem in the reference (no NeuralODE, no sensealg given: Fisher-KPP_Source.jl:102-103,198),
+    so its gradient is SciMLSensitivity's automatic choice (auto_sensealg): ForwardDiffSensitivity for small
+    problems, else the InterpolatingAdjoint."""
+
+    auto_sensealg = True
 
     def __init__(self, kan1, nx: int, dx: float, D: float = 0.01, dtype=torch.float64, device=None,
                  table: bool | None = None):

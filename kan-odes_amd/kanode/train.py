@@ -10,6 +10,9 @@
     Trainer     — one iteration = forward Tsit5 solve, loss, the gradient by the
                   InterpolatingAdjoint (the reference's NeuralODE default sensealg; native
                   kanode_adjoint_tsit5 on the GPU) wherever the RHS provides the adjoint stage,
+                  ForwardDiffSensitivity for a small hand-written ODEProblem (the Fisher-KPP /
+                  Allen-Cahn source drivers at their own sizes: SciMLSensitivity's automatic
+                  choice; native kanode_forward_sensitivity_tsit5),
                   else the discrete adjoint (reverse mode through the stages), ONE all-reduce
                   of [∂L/∂p ; L] across the trajectory shards (RCCL over xGMI with backend
                   "nccl"; gloo on CPU), then the identical Adam step on every rank.
@@ -18,7 +21,7 @@ from __future__ import annotations
 
 import torch
 
-from .adjoint import native_mse_gradient
+from .adjoint import forward_ok, native_mse_gradient, native_mse_gradient_forward
 from .ode import Solution, Tsit5Options, _saveat_list, native_ok, solve
 
 
@@ -148,9 +151,14 @@ class Trainer:
         self.sparse_reg = sparse_reg
         self.group = group
         self.history = []
-        # the reference's default (NeuralODE: InterpolatingAdjoint(autojacvec = ZygoteVJP())) where the
-        # RHS provides the adjoint stage, else reverse mode through the solver steps
-        self.sensealg = sensealg or ("interpolating_adjoint" if hasattr(rhs, "vjp_stage") else "discrete")
+        # the reference's default: NeuralODE passes InterpolatingAdjoint(autojacvec = ZygoteVJP()); a hand-written
+        # ODEProblem (rhs.auto_sensealg: Fisher-KPP / Allen-Cahn source) gets SciMLSensitivity's automatic choice,
+        # ForwardDiffSensitivity where length(u0) + length(p) <= 100 (resolved per step: "auto"); reverse mode
+        # through the solver steps for an RHS without an adjoint stage
+        if sensealg is None:
+            sensealg = ("auto" if getattr(rhs, "auto_sensealg", False) else "interpolating_adjoint") \
+                if hasattr(rhs, "vjp_stage") else "discrete"
+        self.sensealg = sensealg
 
     def predict(self, p) -> Solution:
         return solve(self.rhs, self.u0, self.tspan, p, self.saveat, self.solver, sensealg=self.sensealg)
@@ -159,9 +167,17 @@ class Trainer:
         sv = _saveat_list(self.tspan, self.saveat)
         tf = float(self.tspan[1])
         sv = [s for s in sv if s <= tf + 1e-12 * max(1.0, abs(tf))]     # as solve() filters them
-        if (not self.tp and not self.sparse_reg and self.sensealg == "interpolating_adjoint"
-                and tuple(self.target.shape) == (len(sv),) + tuple(self.u0.shape)
-                and native_ok(self.rhs, self.u0, self.tspan, self.p, sv, self.solver)):
+        sa = self.sensealg
+        fast = (not self.tp and not self.sparse_reg and tuple(self.target.shape) == (len(sv),) + tuple(self.u0.shape)
+                and native_ok(self.rhs, self.u0, self.tspan, self.p, sv, self.solver))
+        if sa == "auto":
+            sa = "forward" if fast and forward_ok(self.rhs, self.u0, self.p) else "interpolating_adjoint"
+        if fast and sa == "forward":
+            # ForwardDiffSensitivity: one native call carrying ∂u/∂p (adjoint.native_mse_gradient_forward)
+            loss, g, sol = native_mse_gradient_forward(self.rhs, self.u0, self.tspan, self.p, sv, self.solver,
+                                                       self.target)
+            return loss.detach(), g, sol
+        if fast and sa == "interpolating_adjoint":
             # the plain-MSE step through the two native calls directly (adjoint.native_mse_gradient)
             loss, g, sol = native_mse_gradient(self.rhs, self.u0, self.tspan, self.p, sv, self.solver, self.target)
             return loss.detach(), g, sol

@@ -476,3 +476,215 @@ int kref_chain_solve_f64(int32_t nl, const kref_layer* Ls, const double* p, cons
     *seconds = now_s() - t_start;
     return rc;
 }
+
+/* ---- ForwardDiffSensitivity (SciMLSensitivity 7.69's automatic sensealg for the small source-term drivers:
+ * Fisher-KPP_Source.jl:198 Zygote.gradient(loss, p), length(u0) + length(p) <= 100; third-party semantics
+ * restated, the same statement as kan-odes_amd/csrc/kan_small.hip fk_small_fsens_kernel and
+ * tests/test_gpu_fsens.py dual_tsit5).  The Dual-number solve over z = [u; S_1; ...; S_P] (rows of n entries),
+ * S_k = ∂u/∂p_k:  S_k' = (D lap) S_k + φ'(u) S_k + ∂φ/∂p_k(u), φ' and ∂φ/∂p from the oracle's pullback of
+ * one KDense(1,1,G) point with ȳ = 1.  DiffEqBase's Dual norm: entry i's residual scale is
+ * abstol + reltol·max(‖z_i‖, ‖znew_i‖), ‖z_i‖² = Σ_r z[r][i]², and the RMS runs over all (1 + P)·n values. */
+static void fk_fsens_rhs(epoch_ctx* c, const double* z, double* dz, double* g /* [P] scratch */) {
+    const int64_t n = c->n, P = c->P, Nx = c->Nx;
+    c->rhs(c, z, dz);                                    /* the values */
+    for (int64_t k = 0; k < P; ++k) {                    /* (D*lap) S_k, dense gemv 'N' */
+        for (int64_t b = 0; b < c->B; ++b) {
+            const double* sb = z + (1 + k) * n + Nx * b;
+            double* db = dz + (1 + k) * n + Nx * b;
+            memset(db, 0, sizeof(double) * (size_t)Nx);
+            for (int64_t j = 0; j < Nx; ++j) {
+                const double sj = sb[j];
+                const double* Aj = c->A + Nx * j;
+                for (int64_t i = 0; i < Nx; ++i) db[i] += Aj[i] * sj;
+            }
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) {                    /* + φ'(u_i) S_k,i + ∂φ/∂p_k(u_i) */
+        const double one = 1.0;
+        double dphi = 0.0;
+        memset(g, 0, sizeof(double) * (size_t)P);
+        kref_layer_vjp_f64(c->L, c->p, z + i, &one, 1, &dphi, g);
+        for (int64_t k = 0; k < P; ++k) {
+            double* d = dz + (1 + k) * n + i;
+            *d = (*d + z[(1 + k) * n + i] * dphi) + g[k];
+        }
+    }
+}
+
+/* Σ over all (1 + P)·n values of (x / sk_entry)² with the per-entry scales sk[n] */
+static double dual_sumsq(const double* x, const double* sk, int64_t n, int64_t rows) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t r = 0; r < rows; ++r) { const double v = x[r * n + i] / sk[i]; s += v * v; }
+    return s;
+}
+static double dual_nrm(const double* z, int64_t i, int64_t n, int64_t rows) {
+    double s = 0.0;
+    for (int64_t r = 0; r < rows; ++r) s += z[r * n + i] * z[r * n + i];
+    return sqrt(s);
+}
+
+/* The Dual solve from t = 0 to T: zsave [n_save][(1 + P)·n] (values then the P sensitivities), stats[2]. */
+static int fsens_forward(epoch_ctx* c, const double* u0, double T, const double* saveat, int32_t n_save, double abstol,
+                         double reltol, double* zsave, int64_t* stats) {
+    const int64_t n = c->n, P = c->P, rows = 1 + P, m = rows * n;
+    double* buf = malloc(sizeof(double) * (m * 12 + n + P));
+    if (!buf) return -1;
+    double *z = buf, *znew = buf + m, *y = buf + 2 * m, *e = buf + 3 * m;
+    double* ks[7];
+    for (int i = 0; i < 7; ++i) ks[i] = buf + (4 + i) * m;
+    double* sk = buf + 11 * m;
+    double* g = sk + n;
+    const double beta1 = 7.0 / 50.0, beta2 = 2.0 / 25.0, gamma = 0.9, qmin = 0.2, qmax = 10.0, qoldinit = 1e-4;
+    memset(z, 0, sizeof(double) * m);
+    memcpy(z, u0, sizeof(double) * n);
+    int32_t si = 0;
+    while (si < n_save && saveat[si] <= 1e-14) { memcpy(zsave + si * m, z, sizeof(double) * m); ++si; }
+    double t = 0.0;
+    fk_fsens_rhs(c, z, ks[0], g);
+    for (int64_t i = 0; i < n; ++i) sk[i] = abstol + dual_nrm(z, i, n, rows) * reltol;   /* _initdt */
+    const double d0 = sqrt(dual_sumsq(z, sk, n, rows) / m), d1 = sqrt(dual_sumsq(ks[0], sk, n, rows) / m);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+    if (dt0 > T) dt0 = T;
+    for (int64_t q = 0; q < m; ++q) y[q] = z[q] + dt0 * ks[0][q];
+    fk_fsens_rhs(c, y, ks[1], g);
+    for (int64_t q = 0; q < m; ++q) e[q] = ks[1][q] - ks[0][q];
+    const double d2 = sqrt(dual_sumsq(e, sk, n, rows) / m) / dt0;
+    const double mx = d1 > d2 ? d1 : d2;
+    const double dt1 = mx <= 1e-15 ? fmax(1e-6, dt0 * 1e-3) : pow(0.01 / mx, 1.0 / 5.0);
+    double dt = fmin(fmin(100 * dt0, dt1), T);
+    double qold = qoldinit;
+    int64_t nacc = 0, nrej = 0;
+    while (t < T - 1e-14 * fmax(1.0, T)) {
+        if (dt > T - t) dt = T - t;
+        for (int s = 0; s < 6; ++s) {
+            for (int64_t q = 0; q < m; ++q) {
+                double acc = z[q];
+                for (int j = 0; j <= s; ++j) acc = acc + (dt * TA[s][j]) * ks[j][q];
+                y[q] = acc;
+            }
+            if (s == 5) memcpy(znew, y, sizeof(double) * m);
+            fk_fsens_rhs(c, y, ks[s + 1], g);
+        }
+        for (int64_t q = 0; q < m; ++q) {
+            double acc = 0.0;
+            for (int j = 0; j < 7; ++j) acc += TB[j] * ks[j][q];
+            e[q] = dt * acc;
+        }
+        for (int64_t i = 0; i < n; ++i) sk[i] = abstol + fmax(dual_nrm(z, i, n, rows), dual_nrm(znew, i, n, rows)) * reltol;
+        const double EEst = sqrt(dual_sumsq(e, sk, n, rows) / m);
+        const double q11 = EEst > 0 ? pow(EEst, beta1) : 0.0;
+        if (EEst > 1.0) { ++nrej; dt = dt / fmin(1.0 / qmin, q11 / gamma); continue; }
+        double q = q11 / pow(qold, beta2);
+        q = fmax(1.0 / qmax, fmin(1.0 / qmin, q / gamma));
+        const double dtnew = q > 0 ? dt / q : dt * qmax;
+        qold = fmax(EEst, qoldinit);
+        const double tn = t + dt;
+        while (si < n_save && saveat[si] <= tn + 1e-12 * fmax(1.0, fabs(tn))) {
+            const double ts = saveat[si];
+            if (fabs(ts - tn) <= 1e-12 * fmax(1.0, fabs(tn))) {
+                memcpy(zsave + si * m, znew, sizeof(double) * m);
+            } else {
+                double w[7];
+                interp_w((ts - t) / dt, w);
+                for (int64_t q = 0; q < m; ++q) {
+                    double acc = 0.0;
+                    for (int j = 0; j < 7; ++j) acc += (dt * w[j]) * ks[j][q];
+                    zsave[si * m + q] = z[q] + acc;
+                }
+            }
+            ++si;
+        }
+        t = tn;
+        memcpy(z, znew, sizeof(double) * m);
+        memcpy(ks[0], ks[6], sizeof(double) * m);
+        ++nacc;
+        dt = dtnew;
+        if (nacc + nrej > 100000) { free(buf); return -3; }   /* maxiters */
+    }
+    stats[0] = nacc;
+    stats[1] = nrej;
+    free(buf);
+    return 0;
+}
+
+static epoch_ctx fk_ctx(const kref_layer* L, const double* p, double D, double dx, int64_t Nx, int64_t B) {
+    epoch_ctx c = {0};
+    c.rhs = fk_rhs;
+    c.vjp = fk_vjp;
+    c.p = p;
+    c.B = B;
+    c.n = Nx * B;
+    c.P = kref_layer_param_length(L);
+    c.L = L;
+    c.Nx = Nx;
+    c.D = D;
+    c.dx = dx;
+    c.A = calloc((size_t)(Nx * Nx), sizeof(double));
+    c.tmp = malloc(sizeof(double) * Nx);
+    const double dx2 = dx * dx, cd = D * (-2.0 / dx2), co = D * (1.0 / dx2);
+    for (int64_t i = 0; i < Nx; ++i) {
+        c.A[i + Nx * i] = cd;
+        if (i + 1 < Nx) { c.A[i + Nx * (i + 1)] = co; c.A[(i + 1) + Nx * i] = co; }
+    }
+    c.A[0 + Nx * (Nx - 1)] = co;
+    c.A[(Nx - 1) + Nx * 0] = co;
+    return c;
+}
+
+/* The Dual solve alone: usave [n_save][n], ssave [n_save][P][n], stats [2] (accepted, rejected). */
+int kref_fk_fsens_solve_f64(const kref_layer* L, const double* p, double D, double dx, int64_t Nx, const double* u0,
+                            int64_t B, double T, const double* saveat, int32_t n_save, double abstol, double reltol,
+                            double* usave, double* ssave, int64_t* stats, double* seconds) {
+    const double t_start = now_s();
+    epoch_ctx c = fk_ctx(L, p, D, dx, Nx, B);
+    const int64_t n = c.n, m = (1 + c.P) * n;
+    double* zs = malloc(sizeof(double) * (size_t)(m * (n_save > 0 ? n_save : 1)));
+    int rc = zs ? fsens_forward(&c, u0, T, saveat, n_save, abstol, reltol, zs, stats) : -1;
+    if (rc == 0)
+        for (int32_t j = 0; j < n_save; ++j) {
+            memcpy(usave + j * n, zs + j * m, sizeof(double) * n);
+            memcpy(ssave + j * c.P * n, zs + j * m + n, sizeof(double) * c.P * n);
+        }
+    free(zs);
+    free(c.A);
+    free(c.tmp);
+    *seconds = now_s() - t_start;
+    return rc;
+}
+
+/* One Fisher-KPP training epoch with the reference's ForwardDiffSensitivity gradient: the Dual solve, the MSE loss,
+ * dL/dp_k = Σ_j Σ_i 2 (pred - X)/numel · S_k, one Adam step (first step of a fresh optimiser); stats [2]. */
+int kref_fk_fsens_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0,
+                            int64_t B, double T, const double* saveat, int32_t n_save, const double* target,
+                            double abstol, double reltol, double eta, double* loss_out, double* grad, int64_t* stats,
+                            double* seconds) {
+    const double t_start = now_s();
+    if (n_save < 1) return -2;
+    epoch_ctx c = fk_ctx(L, p, D, dx, Nx, B);
+    const int64_t n = c.n, P = c.P, m = (1 + P) * n;
+    double* zs = malloc(sizeof(double) * (size_t)(m * n_save));
+    int rc = zs ? fsens_forward(&c, u0, T, saveat, n_save, abstol, reltol, zs, stats) : -1;
+    if (rc == 0) {
+        const double numel = (double)n * n_save;
+        double loss = 0.0;
+        memset(grad, 0, sizeof(double) * (size_t)P);
+        for (int32_t j = 0; j < n_save; ++j)
+            for (int64_t i = 0; i < n; ++i) {
+                const double r = zs[j * m + i] - target[j * n + i];
+                loss += r * r;
+                const double dl = 2.0 * r / numel;
+                for (int64_t k = 0; k < P; ++k) grad[k] += dl * zs[j * m + (1 + k) * n + i];
+            }
+        *loss_out = loss / numel;
+        for (int64_t q = 0; q < P; ++q) {   /* Flux Adam, first step */
+            const double mm = 0.1 * grad[q], v = 0.001 * grad[q] * grad[q];
+            p[q] -= mm / (1 - 0.9) / (sqrt(v / (1 - 0.999)) + 1e-8) * eta;
+        }
+    }
+    free(zs);
+    free(c.A);
+    free(c.tmp);
+    *seconds = now_s() - t_start;
+    return rc;
+}

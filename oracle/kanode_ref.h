@@ -97,6 +97,16 @@ int kref_fk_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64
                       double reltol, int32_t adaptive, double dt_fixed, double eta, double* loss_out, double* grad,
                       int64_t* stats, double* seconds);
 
+/* ForwardDiffSensitivity (the reference's automatic sensealg at Fisher-KPP_Source.jl:198): the Dual solve alone
+ * (usave [n_save][Nx, B], ssave [n_save][P][Nx, B], stats [2]) and one training epoch with that gradient. */
+int kref_fk_fsens_solve_f64(const kref_layer* L, const double* p, double D, double dx, int64_t Nx, const double* u0,
+                            int64_t B, double T, const double* saveat, int32_t n_save, double abstol, double reltol,
+                            double* usave, double* ssave, int64_t* stats, double* seconds);
+int kref_fk_fsens_epoch_f64(const kref_layer* L, double* p, double D, double dx, int64_t Nx, const double* u0,
+                            int64_t B, double T, const double* saveat, int32_t n_save, const double* target,
+                            double abstol, double reltol, double eta, double* loss_out, double* grad, int64_t* stats,
+                            double* seconds);
+
 /* The same epoch for a Lux.Chain NeuralODE RHS (LV_driver_KANODE.jl:180-219,279-287), u0 [N, B] with
  * N = Ls[0].in_dims = Ls[nl-1].out_dims; and the forward solve alone from t = 0 to T at the adaptive
  * tolerances (the driver's loss_train / loss_test solves, :290-291), pred [n_save][N, B], stats [2]. */

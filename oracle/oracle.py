@@ -106,6 +106,12 @@ def lib() -> C.CDLL:
         L.kref_chain_epoch_f64.restype = C.c_int
         L.kref_chain_epoch_f64.argtypes = [C.c_int32, LP, P, P, C.c_int64, C.c_double, P, C.c_int32, P, C.c_double,
                                            C.c_double, C.c_int32, C.c_double, C.c_double, P, P, P, P]
+        L.kref_fk_fsens_solve_f64.restype = C.c_int
+        L.kref_fk_fsens_solve_f64.argtypes = [LP, P, C.c_double, C.c_double, C.c_int64, P, C.c_int64, C.c_double, P,
+                                              C.c_int32, C.c_double, C.c_double, P, P, P, P]
+        L.kref_fk_fsens_epoch_f64.restype = C.c_int
+        L.kref_fk_fsens_epoch_f64.argtypes = [LP, P, C.c_double, C.c_double, C.c_int64, P, C.c_int64, C.c_double, P,
+                                              C.c_int32, P, C.c_double, C.c_double, C.c_double, P, P, P, P]
         L.kref_chain_solve_f64.restype = C.c_int
         L.kref_chain_solve_f64.argtypes = [C.c_int32, LP, P, P, C.c_int64, C.c_double, P, C.c_int32, C.c_double,
                                            C.c_double, P, P, P]
@@ -262,6 +268,47 @@ def fk_epoch(spec: LayerSpec, p: np.ndarray, D: float, dx: float, u0: np.ndarray
         raise RuntimeError(f"kref_fk_epoch_f64 failed ({rc})")
     stats = dict(naccept=int(st[0]), nreject=int(st[1]), adjoint_naccept=int(st[2]), adjoint_nreject=int(st[3]))
     return loss.value, grad, pn, stats, secs.value
+
+
+def fk_fsens_solve(spec: LayerSpec, p: np.ndarray, D: float, dx: float, u0: np.ndarray, T: float, saveat,
+                   abstol=1e-6, reltol=1e-3):
+    """The ForwardDiffSensitivity Dual solve in C (oracle/cpu_epoch.c kref_fk_fsens_solve_f64): u0 (B, Nx);
+    returns (u_save (n_save, B, Nx), S (n_save, P, B, Nx), stats dict, seconds)."""
+    u0 = np.ascontiguousarray(u0, dtype=np.float64)
+    B, Nx = u0.shape
+    sv = np.ascontiguousarray(saveat, dtype=np.float64)
+    P = spec.in_dims * spec.grid_len * spec.out_dims + spec.in_dims * spec.out_dims
+    us = np.zeros((sv.size, B, Nx))
+    ss = np.zeros((sv.size, P, B, Nx))
+    st = np.zeros(2, np.int64)
+    secs = C.c_double()
+    rc = lib().kref_fk_fsens_solve_f64(C.byref(spec.to_c()), _ptr(np.ascontiguousarray(p, dtype=np.float64)), D, dx,
+                                       Nx, _ptr(u0), B, T, _ptr(sv), sv.size, abstol, reltol, _ptr(us), _ptr(ss),
+                                       _ptr(st), C.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"kref_fk_fsens_solve_f64 failed ({rc})")
+    return us, ss, dict(naccept=int(st[0]), nreject=int(st[1])), secs.value
+
+
+def fk_fsens_epoch(spec: LayerSpec, p: np.ndarray, D: float, dx: float, u0: np.ndarray, T: float, saveat, target,
+                   abstol=1e-6, reltol=1e-3, eta=1e-2):
+    """One Fisher-KPP training epoch with the ForwardDiffSensitivity gradient in C on one core
+    (kref_fk_fsens_epoch_f64).  Returns (loss, grad, p_new, stats dict, seconds)."""
+    u0 = np.ascontiguousarray(u0, dtype=np.float64)
+    B, Nx = u0.shape
+    sv = np.ascontiguousarray(saveat, dtype=np.float64)
+    tg = np.ascontiguousarray(target, dtype=np.float64)
+    assert tg.shape == (sv.size, B, Nx)
+    pn = np.ascontiguousarray(p, dtype=np.float64).copy()
+    grad = np.zeros_like(pn)
+    loss, secs = C.c_double(), C.c_double()
+    st = np.zeros(2, np.int64)
+    rc = lib().kref_fk_fsens_epoch_f64(C.byref(spec.to_c()), _ptr(pn), D, dx, Nx, _ptr(u0), B, T, _ptr(sv), sv.size,
+                                       _ptr(tg), abstol, reltol, eta, C.byref(loss), _ptr(grad), _ptr(st),
+                                       C.byref(secs))
+    if rc != 0:
+        raise RuntimeError(f"kref_fk_fsens_epoch_f64 failed ({rc})")
+    return loss.value, grad, pn, dict(naccept=int(st[0]), nreject=int(st[1])), secs.value
 
 
 def chain_epoch(specs, p: np.ndarray, u0: np.ndarray, T: float, saveat, target, abstol=1e-6, reltol=1e-3,

@@ -117,7 +117,8 @@ def _progress(msg: str) -> None:
 
 
 def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: int = 100, dev="cuda:0",
-               loss_every: int = 0, out_path: str | None = None, max_seconds: float = 0.0) -> dict:
+               loss_every: int = 0, out_path: str | None = None, max_seconds: float = 0.0,
+               sensealg: str | None = None) -> dict:
     dev = torch.device(dev)
     pr = source_problem(which)
     iters = int(iters or pr["iters"])
@@ -127,7 +128,7 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
     rhs = kanode.FisherKPPRHS(chain, nx=pr["nx"], dx=pr["dx"], D=pr["D"], dtype=torch.float64, device=dev)
     p0 = torch.as_tensor(chain.setup(np.random.default_rng(seed))[0].astype(np.float64), device=dev)
     u0 = torch.as_tensor(pr["u0"], dtype=torch.float64, device=dev).reshape(1, -1)
-    tr = kanode.Trainer(rhs, u0, pr["tspan"], pr["saveat"], Xn, p0, eta=pr["eta"])
+    tr = kanode.Trainer(rhs, u0, pr["tspan"], pr["saveat"], Xn, p0, eta=pr["eta"], sensealg=sensealg)
     ev = kanode.ChainRHS(chain, device=dev)                       # kan1_.(ρgrid) through the C-ABI
     rho = torch.as_tensor(pr["rho"], dtype=torch.float64, device=dev).reshape(-1, 1)
 
@@ -169,15 +170,18 @@ def run_source(which: str, iters: int | None = None, seed: int = 0, log_every: i
         "seed": seed,
         "nx": pr["nx"], "dx": pr["dx"], "D": pr["D"], "tspan": list(pr["tspan"]), "n_saveat": len(pr["saveat"]),
         "wall_s": wall, "ms_per_iteration": wall / max(done, 1) * 1e3,
-        "what": "Trainer.step per iteration (native Tsit5 + InterpolatingAdjoint + FusedAdam); wall_s includes the "
-                "logged loss, a forward solve after the update every log_every iterations",
+        "what": "Trainer.step per iteration (native Tsit5 + the reference's automatic sensealg: ForwardDiffSensitivity "
+                "at these sizes, else InterpolatingAdjoint; FusedAdam); wall_s includes the logged loss, a forward "
+                "solve after the update every log_every iterations",
+        "sensealg": sol.stats.get("sensealg", "interpolating_adjoint"),
         "log_every": log_every,
         "loss_initial": curve[0][1], "loss_final": curve[-1][1], "loss_min": min(l for _, l in curve),
         "loss_curve": curve,
         "dev_curve": dev_curve,
         "first_iter_within_0.01": next((i for i, d in dev_curve if d <= 0.01), None),
         "first_iter_within_0.005": next((i for i, d in dev_curve if d <= 0.005), None),
-        "forward_steps": sol.stats["naccept"], "adjoint_steps": sol.stats["adjoint"]["naccept"],
+        "forward_steps": sol.stats["naccept"],
+        "adjoint_steps": sol.stats["adjoint"]["naccept"] if "adjoint" in sol.stats else None,
         "rho": pr["rho"].tolist(), "learned_source": lr.tolist(),
         "recorded_fit": pr["fitted_text"], "recorded_fit_values": fit.tolist(),
         "max_abs_dev_from_recorded_fit": float(np.max(np.abs(lr - fit))),
@@ -249,6 +253,7 @@ def main() -> None:
     ap.add_argument("--log-every", type=int, default=100)
     ap.add_argument("--out", default="gpurun_out/anchors")
     ap.add_argument("--max-seconds", type=float, default=0.0, help="stop at the first log point past this")
+    ap.add_argument("--sensealg", default=None, help="source problems: None = the reference's automatic choice")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     path = os.path.join(a.out, f"{a.problem}_seed{a.seed}.json")
@@ -257,7 +262,8 @@ def main() -> None:
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_train_final",
                                             "loss_train_min", "loss_test_final", "recorded_converged_loss")}))
     else:
-        o = run_source(a.problem, a.iters or None, a.seed, a.log_every, out_path=path, max_seconds=a.max_seconds)
+        o = run_source(a.problem, a.iters or None, a.seed, a.log_every, out_path=path, max_seconds=a.max_seconds,
+                       sensealg=a.sensealg)
         print(json.dumps({k: o[k] for k in ("anchor", "iters", "ms_per_iteration", "loss_final",
                                             "max_abs_dev_from_recorded_fit", "max_abs_dev_from_true_source",
                                             "first_iter_within_0.01", "first_iter_within_0.005")}))
