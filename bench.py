@@ -385,10 +385,12 @@ def lv1_train_bench(dev, with_cpu: bool, reps: int = 10):
 
     def iteration():
         tr.step()
+        # loss_train(p) after update! (:289): Trainer.eval_loss keeps this forward solve (dense output) for the
+        # next iteration's gradient -- the same problem at the same p -- instead of solving it twice
+        l_tr = tr.eval_loss()
         with torch.no_grad():
-            l_tr = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 3.5), tr.p, ts).u, tr.target)
             l_te = kanode.mse_loss(kanode.solve(rhs, u0, (0.0, 14.0), tr.p, ts_test).u, tgt_test)
-        return float(l_tr), float(l_te)
+        return l_tr, float(l_te)
 
     iteration()
     torch.cuda.synchronize()

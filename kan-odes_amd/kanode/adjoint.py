@@ -241,16 +241,24 @@ class _NativeAdjointSolve(torch.autograd.Function):
         return None, None, None, None, None, dp, du0
 
 
-def native_mse_gradient(f, u0, tspan, p, saveat, opt: Tsit5Options, target):
+def native_forward_dense(f, u0, tspan, p, saveat, opt: Tsit5Options):
+    """The forward half of native_mse_gradient: (u_save, stats, DenseOutput) with the dense output kept."""
+    return f.hd.solve_tsit5(p.detach().contiguous(), u0.detach().contiguous(), float(tspan[0]), float(tspan[1]),
+                            saveat, opt.to_c(), keep_dense=True)
+
+
+def native_mse_gradient(f, u0, tspan, p, saveat, opt: Tsit5Options, target, pre=None):
     """(loss, dL/dp, Solution) for L = mse_loss(solve(...).u, target) through the native solve and
     InterpolatingAdjoint, without the autograd engine: the same two C calls as backward() of
     solve_native_interpolating_adjoint, with ∂L/∂u formed as mse_loss's backward does ((u - X)·2/numel).
-    For Trainer's plain-MSE step (a handful of launches per iteration, where the engine's own overhead showed)."""
+    For Trainer's plain-MSE step (a handful of launches per iteration, where the engine's own overhead showed).
+    pre: an earlier native_forward_dense of the same problem at the same p (its dense output is consumed)."""
     hd = f.hd
     oc = opt.to_c()
     pc = p.detach().contiguous()
-    u_save, st, dense = hd.solve_tsit5(pc, u0.detach().contiguous(), float(tspan[0]), float(tspan[1]), saveat, oc,
-                                       keep_dense=True)
+    if pre is None:
+        pre = native_forward_dense(f, u0, tspan, p, saveat, opt)
+    u_save, st, dense = pre
     try:
         stats = dict(st)
         stats["dts"] = dense.step_sizes()[1].tolist()
@@ -319,11 +327,17 @@ def solve_forward_sensitivity(f, u0, tspan, p, saveat, opt: Tsit5Options) -> Sol
     return Solution(list(saveat), u, stats)
 
 
-def native_mse_gradient_forward(f, u0, tspan, p, saveat, opt: Tsit5Options, target):
+def native_forward_sens(f, u0, tspan, p, saveat, opt: Tsit5Options):
+    """The solve of native_mse_gradient_forward: (u_save, S, stats)."""
+    return f.hd.forward_sensitivity_tsit5(p.detach().contiguous(), u0.detach().contiguous(), float(tspan[0]),
+                                          float(tspan[1]), saveat, opt.to_c())
+
+
+def native_mse_gradient_forward(f, u0, tspan, p, saveat, opt: Tsit5Options, target, pre=None):
     """(loss, dL/dp, Solution) for L = mse_loss(solve(...).u, target) by ForwardDiffSensitivity: one native call
-    (the solve with the sensitivities), then ∂L/∂u = (u - X)·2/numel contracted with them."""
-    u_save, S, st = f.hd.forward_sensitivity_tsit5(p.detach().contiguous(), u0.detach().contiguous(),
-                                                   float(tspan[0]), float(tspan[1]), saveat, opt.to_c())
+    (the solve with the sensitivities), then ∂L/∂u = (u - X)·2/numel contracted with them.  pre: an earlier
+    native_forward_sens of the same problem at the same p."""
+    u_save, S, st = pre if pre is not None else native_forward_sens(f, u0, tspan, p, saveat, opt)
     loss = torch.nn.functional.mse_loss(u_save, target)
     dl = (u_save - target).mul_(2.0 / u_save.numel())
     stats = dict(st)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import torch
 
-from .adjoint import forward_ok, native_mse_gradient, native_mse_gradient_forward
+from .adjoint import forward_ok, native_forward_dense, native_mse_gradient, native_mse_gradient_forward
 from .ode import Solution, Tsit5Options, _saveat_list, native_ok, solve
 
 
@@ -159,11 +159,14 @@ class Trainer:
             sensealg = ("auto" if getattr(rhs, "auto_sensealg", False) else "interpolating_adjoint") \
                 if hasattr(rhs, "vjp_stage") else "discrete"
         self.sensealg = sensealg
+        self._pver = 0        # bumped by every optimiser update (keys the cached forward of eval_loss)
+        self._pre = None      # (pver, path, forward payload) from eval_loss, consumed by the next step
 
     def predict(self, p) -> Solution:
         return solve(self.rhs, self.u0, self.tspan, p, self.saveat, self.solver, sensealg=self.sensealg)
 
-    def loss_and_grad(self):
+    def _fast_path(self):
+        """(saveat list, path) with path "forward" / "interpolating_adjoint" for the native plain-MSE step, or None."""
         sv = _saveat_list(self.tspan, self.saveat)
         tf = float(self.tspan[1])
         sv = [s for s in sv if s <= tf + 1e-12 * max(1.0, abs(tf))]     # as solve() filters them
@@ -172,14 +175,50 @@ class Trainer:
                 and native_ok(self.rhs, self.u0, self.tspan, self.p, sv, self.solver))
         if sa == "auto":
             sa = "forward" if fast and forward_ok(self.rhs, self.u0, self.p) else "interpolating_adjoint"
-        if fast and sa == "forward":
+        return sv, (sa if fast and sa in ("forward", "interpolating_adjoint") else None)
+
+    def _drop_pre(self):
+        if self._pre is not None and self._pre[1] == "interpolating_adjoint":
+            self.rhs.hd.release_dense(self._pre[2][2])
+        self._pre = None
+
+    def eval_loss(self) -> float:
+        """loss(p) at the current parameters, as the drivers log it after update! (LV_driver_KANODE.jl:289-290
+        loss_train(p); Fisher-KPP_Source.jl:204).  On the native plain-MSE path this forward solve is exactly the
+        next iteration's InterpolatingAdjoint forward (same p, u0, tspan, saveat), so its dense output is kept and
+        the next step() takes its gradient from it instead of solving again.  The cache is keyed
+        on the Trainer's own updates: change self.p only through step() (or call eval_loss again)."""
+        self._drop_pre()
+        sv, path = self._fast_path()
+        if path == "interpolating_adjoint":
+            pre = native_forward_dense(self.rhs, self.u0, self.tspan, self.p, sv, self.solver)
+        else:
+            # (in forward mode the next gradient is a Dual solve, whose error norm counts the partials: its steps
+            # and values are not the logged plain solve's, so nothing is kept)
+            with torch.no_grad():
+                return float(mse_loss(solve(self.rhs, self.u0, self.tspan, self.p.detach(), self.saveat,
+                                            self.solver).u, self.target))
+        self._pre = (self._pver, path, pre)
+        return float(mse_loss(pre[0], self.target))
+
+    def loss_and_grad(self):
+        sv, path = self._fast_path()
+        pre = None
+        if self._pre is not None:
+            if self._pre[0] == self._pver and self._pre[1] == path:
+                pre = self._pre[2]
+                self._pre = None
+            else:
+                self._drop_pre()
+        if path == "forward":
             # ForwardDiffSensitivity: one native call carrying ∂u/∂p (adjoint.native_mse_gradient_forward)
             loss, g, sol = native_mse_gradient_forward(self.rhs, self.u0, self.tspan, self.p, sv, self.solver,
-                                                       self.target)
+                                                       self.target, pre=pre)
             return loss.detach(), g, sol
-        if fast and sa == "interpolating_adjoint":
+        if path == "interpolating_adjoint":
             # the plain-MSE step through the two native calls directly (adjoint.native_mse_gradient)
-            loss, g, sol = native_mse_gradient(self.rhs, self.u0, self.tspan, self.p, sv, self.solver, self.target)
+            loss, g, sol = native_mse_gradient(self.rhs, self.u0, self.tspan, self.p, sv, self.solver, self.target,
+                                               pre=pre)
             return loss.detach(), g, sol
         p = self.p.detach().requires_grad_(True)
         sol = self.predict(p)
@@ -208,6 +247,7 @@ class Trainer:
             self.opt.update(self.p, g.contiguous(), scale)      # the mean is formed inside the launch
         else:
             self.opt.update(self.p, g * scale if scale != 1.0 else g)
+        self._pver += 1
         lv = float(loss)
         self.history.append(lv)
         return lv

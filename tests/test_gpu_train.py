@@ -133,3 +133,46 @@ def test_trainer_fast_path_filters_saveat_past_tf():
     assert torch.equal(ga, gb)
     with pytest.raises(kanode.KanodeError, match="saveat"):
         rhs.hd.solve_tsit5(p0, u0, 0.0, 0.1, [0.0, 0.3], opt.to_c())
+
+
+@pytest.mark.parametrize("case", ["lv1", "fk26"])
+def test_eval_loss_forward_is_reused_by_the_next_step_bitwise(case):
+    """the driver's loss_train(p) after update! (LV_driver_KANODE.jl:289) solves exactly the next
+    iteration's InterpolatingAdjoint forward problem.  Trainer.eval_loss keeps that solve's dense output and the next
+    step takes its gradient from it: the parameter trajectory and the logged losses are bitwise those of the trainer
+    that solves again.  (FK26 takes forward mode, whose Dual solve is not the logged plain solve: nothing is kept,
+    and the logged loss is the plain solve's.)"""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    dev = device()
+    if case == "lv1":
+        chain = kanode.Chain(kanode.KDense(2, 10, 5), kanode.KDense(10, 2, 5))
+        rhs = kanode.ChainRHS(chain, device=dev)
+        p0 = t(chain.setup(np.random.default_rng(0))[0].astype(np.float64) / 1e4)
+        u0 = t(np.array([[1.0, 1.0]]))
+        ts = [0.1 * i for i in range(35)]
+        X = t(np.random.default_rng(1).uniform(0.5, 2.0, (35, 1, 2)))
+        tspan, eta = (0.0, 3.5), 5e-4
+    else:
+        import anchors
+        pr = anchors.source_problem("fk")
+        kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
+        rhs = kanode.FisherKPPRHS(kan1, nx=pr["nx"], dx=pr["dx"], D=pr["D"], device=dev)
+        p0 = t(kan1.setup(np.random.default_rng(1))[0].astype(np.float64))
+        u0 = t(pr["u0"][None, :])
+        ts, tspan, eta = pr["saveat"], pr["tspan"], 1e-2
+        X = t(anchors.source_truth(pr))
+    a = kanode.Trainer(rhs, u0, tspan, ts, X, p0, eta=eta)
+    b = kanode.Trainer(rhs, u0, tspan, ts, X, p0, eta=eta)
+    la, lb = [], []
+    for _ in range(4):
+        a.step()
+        la.append(a.eval_loss())           # cached for a's next step
+        b.step()
+        with torch.no_grad():
+            lb.append(float(kanode.mse_loss(kanode.solve(rhs, u0, tspan, b.p, ts,
+                                                         sensealg="discrete").u, X)))
+    assert torch.equal(a.p, b.p)
+    assert a.history == b.history
+    assert la == lb
