@@ -454,12 +454,27 @@ def fk26_train_bench(dev, with_cpu: bool, reps: int = 20):
     torch.cuda.synchronize()
     gpu = (time.perf_counter() - t0) / reps * 1e3
     _, _, sol = tr.loss_and_grad()
-    out = {"unit": "ms/iteration", "batch": 1, "nx": nx, "dtype": "f64", "gpu": gpu,
-           "forward_steps": sol.stats["naccept"], "adjoint_steps": sol.stats["adjoint"]["naccept"],
-           "gpu_path": "one-workgroup solve + one-workgroup adjoint" if rhs.hd.get_option("last_adjoint") == 2
-           else "host loop",
+    sensealg = sol.stats.get("sensealg", "interpolating_adjoint")
+    out = {"unit": "ms/iteration", "batch": 1, "nx": nx, "dtype": "f64", "gpu": gpu, "sensealg": sensealg,
+           "forward_steps": sol.stats["naccept"],
+           "adjoint_steps": sol.stats["adjoint"]["naccept"] if "adjoint" in sol.stats else None,
+           "gpu_path": ("one-workgroup forward-sensitivity solve (kanode_forward_sensitivity_tsit5)"
+                        if sensealg == "forward" else
+                        "one-workgroup solve + one-workgroup adjoint" if rhs.hd.get_option("last_adjoint") == 2
+                        else "host loop"),
            "what": "one Fisher-KPP_Source.jl training iteration: adaptive Tsit5 (T = 5, saveat 0.5, default "
-                   "tolerances) + InterpolatingAdjoint + Adam(1e-2), 26 points, one IC"}
+                   "tolerances), the gradient the reference takes at this size (SciMLSensitivity's automatic choice: "
+                   "ForwardDiffSensitivity), Adam(1e-2), 26 points, one IC"}
+    # the InterpolatingAdjoint iteration beside it (the product's path for larger fields)
+    tra = kanode.Trainer(rhs, u0, (0.0, T), saveat, torch.as_tensor(truth, device=dev), torch.as_tensor(p0, device=dev),
+                         eta=1e-2, solver=kanode.Tsit5Options(), sensealg="interpolating_adjoint")
+    tra.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tra.step()
+    torch.cuda.synchronize()
+    out["gpu_interpolating_adjoint"] = (time.perf_counter() - t0) / reps * 1e3
     if with_cpu:
         from oracle import oracle as O
         spec = O.LayerSpec(1, 1, 10, "softsign")
@@ -467,14 +482,23 @@ def fk26_train_bench(dev, with_cpu: bool, reps: int = 20):
         times = []
         for r in range(23):
             t0 = time.perf_counter()
-            _, _, pc, st, _ = O.fk_epoch(spec, pc, D, dx, rho0[None, :], T, saveat, truth, eta=1e-2)
+            _, _, pc, st, _ = O.fk_fsens_epoch(spec, pc, D, dx, rho0[None, :], T, saveat, truth, eta=1e-2)
             if r >= 3:
                 times.append(time.perf_counter() - t0)
+        pa = p0.copy()
+        times_a = []
+        for r in range(13):
+            t0 = time.perf_counter()
+            _, _, pa, _, _ = O.fk_epoch(spec, pa, D, dx, rho0[None, :], T, saveat, truth, eta=1e-2)
+            if r >= 3:
+                times_a.append(time.perf_counter() - t0)
         out.update({"cpu": float(np.median(times)) * 1e3, "cpu_cores": 1,
-                    "cpu_steps": [st.get("naccept"), st.get("adjoint_naccept")],
-                    "cpu_kind": "port (oracle/cpu_epoch.c: C Tsit5 + InterpolatingAdjoint + Adam over the dense-"
-                                "Laplacian oracle RHS, one core; median of 20 after 3 warm-ups)",
-                    "speedup": float(np.median(times)) * 1e3 / gpu})
+                    "cpu_steps": [st.get("naccept"), st.get("nreject")],
+                    "cpu_kind": "port (oracle/cpu_epoch.c kref_fk_fsens_epoch_f64: the C Dual-number Tsit5 solve "
+                                "(ForwardDiffSensitivity) + Adam over the dense-Laplacian oracle RHS, one core; median "
+                                "of 20 after 3 warm-ups)",
+                    "speedup": float(np.median(times)) * 1e3 / gpu,
+                    "cpu_interpolating_adjoint": float(np.median(times_a)) * 1e3})
     return out
 
 

@@ -374,6 +374,62 @@ function ChainRulesCore.rrule(::typeof(solve_tsit5), h::Handle, u0::AbstractVecO
     return sol, solve_tsit5_pullback
 end
 
+# --- ForwardDiffSensitivity (kanode_forward_sensitivity_tsit5): the gradient SciMLSensitivity 7.69 picks for the
+# source-term drivers at their own sizes (Fisher-KPP_Source.jl:198, Zygote.gradient(loss, p) with no sensealg and
+# length(u0) + length(p) <= 100): the Dual-number solve, one partial per parameter, on the device in one workgroup.
+function fsens!(h::Handle, p::Ptr{Cvoid}, u0::Ptr{Cvoid}, B::Integer, tspan, saveat::Vector{Float64},
+                usave::Ptr{Cvoid}, ssave::Ptr{Cvoid}; opt::SolverOptions = default_options(),
+                stream::Ptr{Cvoid} = C_NULL)
+    st = Ref{SolveStats}()
+    check(h, ccall(sym(:kanode_forward_sensitivity_tsit5), Cint,
+        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Float64, Float64, Ptr{Float64}, Int64, Ptr{Cvoid}, Ptr{Cvoid},
+         Ref{SolverOptions}, Ref{SolveStats}, Ptr{Cvoid}),
+        h.ptr, p, u0, B, tspan[1], tspan[2], saveat, length(saveat), usave, ssave, opt, st, stream))
+    return st[]
+end
+fsens_supported(h::Handle, B::Integer) = ccall(sym(:kanode_forward_sensitivity_supported), Int32,
+                                               (Ptr{Cvoid}, Int64), h.ptr, B) == 1
+
+"""solve_tsit5_fwd(h, u0, tspan, p, saveat; abstol, reltol) -> Array(sol), like solve_tsit5, but differentiable in p
+by forward sensitivities (ForwardDiffSensitivity, the reference's automatic choice for its small source-term
+problems): the rrule's pullback contracts the cotangent with ∂u(saveat)/∂p, computed in the same solve."""
+function solve_tsit5_fwd(h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector, saveat::AbstractVector; kw...)
+    sol, _ = fwd_impl(h, u0, tspan, p, saveat, options(; kw...))
+    return sol
+end
+function fwd_impl(h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector, saveat::AbstractVector,
+                  opt::SolverOptions)
+    checkp(h, p)
+    checku(h, u0, h.nin, "u0")
+    T = h.T
+    ts = Vector{Float64}(saveat)
+    issorted(ts) || throw(ArgumentError("saveat must be ascending"))
+    B = size(u0, 2)
+    fsens_supported(h, B) || throw(ArgumentError("forward sensitivities: not covered for this handle / batch"))
+    pd, ud = upload(tohost(T, p)), upload(tohost(T, u0))
+    out = Array{T}(undef, h.nin, B, length(ts))
+    S = Array{T}(undef, h.nin, B, h.P, length(ts))          # s_save [n_save, P, N, B] in column-major order
+    od, sd = DevBuf(sizeof(out)), DevBuf(sizeof(S))
+    fsens!(h, pd.ptr, ud.ptr, B, tspan, ts, od.ptr, sd.ptr; opt)
+    download!(out, od)
+    download!(S, sd)
+    sol = u0 isa AbstractVector ? reshape(out, h.nin, length(ts)) : out
+    return sol, S
+end
+function ChainRulesCore.rrule(::typeof(solve_tsit5_fwd), h::Handle, u0::AbstractVecOrMat, tspan, p::AbstractVector,
+                              saveat::AbstractVector; kw...)
+    sol, S = fwd_impl(h, u0, tspan, p, saveat, options(; kw...))
+    function solve_tsit5_fwd_pullback(Δ)
+        ū = unthunk(Δ)
+        ū isa AbstractZero && return (NoTangent(), NoTangent(), NoTangent(), NoTangent(), ZeroTangent(), NoTangent())
+        ub = reshape(ū, h.nin * size(u0, 2), 1, length(saveat))
+        Sm = reshape(S, h.nin * size(u0, 2), h.P, length(saveat))
+        dp = vec(sum(sum(Sm .* ub; dims = 1); dims = 3))       # Σ_j Σ_i ū_i(t_j) ∂u_i(t_j)/∂p
+        return (NoTangent(), NoTangent(), NoTangent(), NoTangent(), ptangent(p, dp), NoTangent())
+    end
+    return sol, solve_tsit5_fwd_pullback
+end
+
 # --- data-parallel training across GPUs (kanode_comm_*): one process per GPU, each with its trajectory
 # shard; after the adjoint, the flat [dp; L] (device) is SUM all-reduced over RCCL and the mean applied by
 # kanode_adam_step(scale = 1/nranks).  Rank 0 calls comm_unique_id() and the host distributes the bytes
