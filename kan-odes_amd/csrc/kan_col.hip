@@ -687,6 +687,121 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
     }
 }
 
+// (the generic shapes' stage loop is not unrolled; only the fixed LV shape needs it to be)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
+// The six adjoint stages of one InterpolatingAdjoint step in one launch (ChainAdjStep, kan_kernels.hpp): per
+// column, stage s forms the forward dense output and λs exactly as kd_chain_vjp_stage_kernel does from the
+// integrator's stage arrays, but kλ_1..kλ_6 stay in registers; the stage's parameter cotangents go to the group's
+// LDS row of that stage and the block's per-stage sums to slab region s.  Only λ_new and kλ_7 are written.
+template <typename T, int NORM, int PATH, class S>
+__global__ void __launch_bounds__(kChainVjpBlock)
+kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P, int64_t K,
+                         ChainAdjStep<T> a, T* __restrict__ slab, int64_t region, double* __restrict__ err_slab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char cs_raw[];
+    constexpr int NG = kChainVjpBlock / kChainDim;
+    LayerConst* lcl = reinterpret_cast<LayerConst*>(cs_raw);
+    T* ps = reinterpret_cast<T*>(cs_raw + nl * sizeof(LayerConst));
+    T* rows = ps + P;                                 // [6][NG][P] gradient rows
+    {
+        const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
+        const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
+        int32_t* dst = reinterpret_cast<int32_t*>(cs_raw);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        for (int i = threadIdx.x; i < 6 * NG * P; i += blockDim.x) rows[i] = T(0);
+    }
+    KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps, rows)
+    const Math<T> M{tab};
+    const int N0 = lcl[0].I;
+    const int j = threadIdx.x & (kChainDim - 1);
+    const int g = threadIdx.x / kChainDim;
+    double eacc = 0.0;
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kChainDim;
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kChainDim; k < K; k += stride) {
+        const int64_t idx = (int64_t)N0 * k + j;
+        const bool live = j < N0;
+        T kl[7];
+        const T l0 = live ? a.lam[idx] : T(0);
+        kl[0] = live ? a.kl1[idx] : T(0);
+        T ls = l0;
+        double ev = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            T yj = T(0);
+            if (live) {
+                T kv[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) kv[q] = a.su_k[s][q][idx];   // (all loads first)
+                yj = a.su_u[s][idx];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) yj = kfma<T>((T)a.su_c[s][q], kv[q], yj);
+                ls = l0;
+#pragma unroll
+                for (int q = 0; q <= s; ++q) {
+                    ls = kfma<T>((T)a.a[s][q], kl[q], ls);
+                    if (s == 5) ev = ::fma(a.ec[q], (double)kl[q], ev);
+                }
+            }
+            kl[s + 1] = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, rows + ((size_t)s * NG + g) * P, j, yj, ls);
+        }
+        if (live) {
+            a.lam_out[idx] = ls;
+            a.kl7[idx] = kl[6];
+            if (a.want_error) {
+                const double e = ::fma(a.ec[6], (double)kl[6], ev);
+                const double sk = ::fma(a.reltol, fmax(kabs((double)l0), kabs((double)ls)), a.abstol);
+                const double r = e / sk;
+                eacc = ::fma(r, r, eacc);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 6 * P; i += blockDim.x) {   // each stage's block sums, the stage kernel's order
+        const int s = i / P, q = i - s * P;
+        const T* r0 = rows + (size_t)s * NG * P;
+        T v = r0[q];
+#pragma unroll
+        for (int gg = 1; gg < NG; ++gg) v = v + r0[gg * P + q];
+        slab[s * region + (int64_t)blockIdx.x * P + q] = v;
+    }
+    if (a.want_error) {
+        __shared__ double red[kChainVjpBlock / kWave];
+        const double v[1] = {eacc};
+        block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+    }
+}
+
+#pragma clang diagnostic pop
+
+// km_out[s][q] = Σ_b slab[s·region + b·P + q] (block (q, s), q < P) and err_out[0] = Σ_b err_slab[b] (block (P, 0)):
+// chain_vjp_finish_kernel's sums for the six stages of a step in one launch
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+chain_vjp_step_finish_kernel(const T* __restrict__ slab, int64_t region, int64_t nblk, int64_t P, ChainKmOut<T> km,
+                             const double* __restrict__ err_slab, double* __restrict__ err_out) {
+    __shared__ double red[kBlock / kWave];
+    const int64_t q = blockIdx.x;
+    const int s = blockIdx.y;
+    if (q == P && (s != 0 || !err_out)) return;
+    double acc = 0.0;
+    if (q < P) {
+        acc = strided_rows_sum(slab + s * region + q, nblk, P, acc);
+    } else {
+        acc = strided_rows_sum(err_slab, nblk, 1, acc);
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+        for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+        T* const out = s == 0 ? km.k[0] : s == 1 ? km.k[1] : s == 2 ? km.k[2] : s == 3 ? km.k[3] : s == 4 ? km.k[4] : km.k[5];
+        if (q < P) out[q] = (T)t;
+        else err_out[0] = t;
+    }
+}
+
 // dp[q] (= or +=) Σ_b slab[b·P + q] (block q < P) and err_out[0] = Σ_b err_slab[b] (block P)
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
@@ -1964,6 +2079,53 @@ hipError_t launch_kd_chain_step(const LayerConst* hlcs, int nl, const LayerConst
 // The fused adjoint stage of a small chain (kd_chain_vjp_stage_kernel) when every layer is
 // small (I, O <= 16), the layers share the normalizer/path specialisation, nl <= 4 and the
 // parameter vector plus the gradient rows fit in LDS; hipErrorNotSupported otherwise.
+size_t chain_vjp_step_slab_bytes(int64_t P, int64_t K, size_t esize, int grid_cap) {
+    const int grid = grid_for(K, kChainVjpBlock / kChainDim, grid_cap);
+    return 6 * (((size_t)grid * P * esize + 255) & ~(size_t)255) + (size_t)grid * sizeof(double) + 256;
+}
+
+template <typename T>
+hipError_t launch_kd_chain_vjp_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                    int64_t K, const ChainAdjStep<T>& a, int grid_cap, void* slab, size_t slab_bytes,
+                                    T* const* km_out, double* err_out, hipStream_t st) {
+    if (nl < 1 || nl > kChainMaxLayers || K < 1 || grid_cap < 1) return hipErrorNotSupported;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
+            return hipErrorNotSupported;
+        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
+    }
+    if (hlcs[nl - 1].O != hlcs[0].I) return hipErrorNotSupported;
+    const int ng = kChainVjpBlock / kChainDim;
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + 6 * ng);
+    if (lds > 64 * 1024) return hipErrorNotSupported;
+    // the stage kernel's grid (grid_cap: its slab's row capacity, <= 1024): the same blocks sum the same columns,
+    // so the per-block sums and the reduction order are the stage kernel's
+    const int grid = grid_for(K, ng, grid_cap);
+    if (chain_vjp_step_slab_bytes(P, K, sizeof(T), grid_cap) > slab_bytes) return hipErrorNotSupported;
+    const int64_t region = (int64_t)((((size_t)grid * P * sizeof(T) + 255) & ~(size_t)255) / sizeof(T));
+    T* tslab = (T*)slab;
+    double* eslab = (double*)((char*)slab + 6 * region * sizeof(T));
+    const LayerConst& h = hlcs[0];
+#define KAN_CVSTEP(NORM, PATH, S)                                                                                 \
+    hipLaunchKernelGGL((kd_chain_vjp_step_kernel<T, NORM, PATH, S>), dim3(grid), dim3(kChainVjpBlock), lds, st,  \
+                       lcs, nl, p, (int)P, K, a, tslab, region, eslab)
+    if (h.norm == NORM_TANH_FAST && h.path == PATH_REC && chain_is_lv(hlcs, nl))
+        KAN_CVSTEP(NORM_TANH_FAST, PATH_REC, ChainShapeLV);
+    else if (h.norm == NORM_TANH_FAST && h.path == PATH_REC) KAN_CVSTEP(NORM_TANH_FAST, PATH_REC, ChainShapeAny);
+    else if (h.path == PATH_REC_CORR) KAN_CVSTEP(NORM_RUNTIME, PATH_REC_CORR, ChainShapeAny);
+    else if (h.path == PATH_REC) KAN_CVSTEP(NORM_RUNTIME, PATH_REC, ChainShapeAny);
+    else KAN_CVSTEP(NORM_RUNTIME, PATH_DIRECT, ChainShapeAny);
+#undef KAN_CVSTEP
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    ChainKmOut<T> km{};
+    for (int s = 0; s < 6; ++s) km.k[s] = km_out[s];
+    hipLaunchKernelGGL((chain_vjp_step_finish_kernel<T>), dim3((unsigned)P + 1, 6), dim3(kBlock), 0, st, tslab, region,
+                       (int64_t)grid, (int64_t)P, km, eslab, a.want_error ? err_out : nullptr);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
                                      const T* u, const StageArgs<T>& su, const T* lam, const StageArgs<T>& sl,
@@ -2008,6 +2170,10 @@ hipError_t launch_kd_chain_vjp_stage(const LayerConst* hlcs, int nl, const Layer
 }
 
 #define KAN_COL_INST(T)                                                                                          \
+    template hipError_t launch_kd_chain_vjp_step<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t,  \
+                                                    int64_t, const ChainAdjStep<T>&, int, void*, size_t,        \
+                                                    T* const*,                                                  \
+                                                    double*, hipStream_t);                                        \
     template hipError_t launch_kd_chain_vjp_stage<T>(const LayerConst*, int, const LayerConst*, const T*, int64_t, \
                                                      const T*, const StageArgs<T>&, const T*, const StageArgs<T>&, \
                                                      T*, T*, T*, bool, double*, void*, size_t, int64_t,          \

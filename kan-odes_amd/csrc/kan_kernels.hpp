@@ -426,6 +426,37 @@ constexpr int kChainAdjointMaxSteps = 1024;   // forward steps held in LDS
 template <typename T>
 hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
                                    int64_t B, const ChainAdjointArgs& a, hipStream_t st, bool wide);
+// A whole InterpolatingAdjoint step of a small chain per trajectory column (kd_chain_vjp_step_kernel, kan_col.hip):
+// the six adjoint stages of kanode_solve.cpp adjoint_t in one launch, λ and kλ_1..kλ_7 of a column in registers.
+// Stage s reads the forward dense output u_i + Σ_q su_c[s][q] k_{i,q} (K form, the forward step holding stage s)
+// and the adjoint stage input λ + Σ_{q<=s} a[s][q] kλ_q; its kμ rows go to slab region s ([grid][P] of T, the
+// stage kernel's per-block sums), the λ error partials (with want_error) after the six regions ([grid] doubles).
+// chain_vjp_step_finish reduces the regions into km_out[0..5] (= kμ_2..kμ_7) and the error total, each in the
+// order chain_vjp_finish_kernel uses: the step is bitwise the six kd_chain_vjp_stage_kernel launches.
+template <typename T>
+struct ChainKmOut {
+    T* k[6];
+};
+template <typename T>
+struct ChainAdjStep {
+    const T* su_u[6];
+    const T* su_k[6][7];
+    double su_c[6][7];
+    double a[6][6];   // h·a_sj
+    double ec[7];     // h·btilde_j (the λ error of stage 6)
+    double abstol, reltol;
+    const T* lam;
+    T* lam_out;       // λ_new (stage 6's input)
+    const T* kl1;     // kλ_1 (FSAL)
+    T* kl7;           // kλ_7
+    int32_t want_error, pad;
+};
+template <typename T>
+hipError_t launch_kd_chain_vjp_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
+                                    int64_t K, const ChainAdjStep<T>& a, int grid_cap, void* slab, size_t slab_bytes,
+                                    T* const* km_out, double* err_out, hipStream_t st);
+// slab bytes launch_kd_chain_vjp_step needs for K columns over at most grid_cap blocks
+size_t chain_vjp_step_slab_bytes(int64_t P, int64_t K, size_t esize, int grid_cap);
 // One Tsit5 step of a small chain per trajectory column (kd_chain_step_kernel, kan_col.hip)
 struct ChainStepArgs {
     double a[6][6];   // dt·a_sj

@@ -95,6 +95,8 @@ struct kanode_handle {
     bool built_phi = false, built_vjp = false;
     // adjoint stages whose dp / error reductions wait for kanode_internal_vjp_flush (one launch)
     void* defer_slab = nullptr;
+    void* cstep_slab = nullptr;       // the fused small-chain adjoint step's six stage regions (grown on demand)
+    size_t cstep_bytes = 0;
     void* step_slab = nullptr;        // fused adjoint step: six stages' moment rows + error partials
     kan::FinishJobs jobs{};
     int njobs = 0;
@@ -1009,6 +1011,7 @@ void kanode_destroy(kanode_handle* h) {
     if (h->stage_ws) (void)hipFree(h->stage_ws);
     if (h->dtable) (void)hipFree(h->dtable);
     if (h->defer_slab) (void)hipFree(h->defer_slab);
+    if (h->cstep_slab) (void)hipFree(h->cstep_slab);
     if (h->step_slab) (void)hipFree(h->step_slab);
     if (h->fin_ctr) (void)hipFree(h->fin_ctr);
     if (h->solve_cache) kanode_solution_free(h->solve_cache);
@@ -1458,6 +1461,48 @@ kanode_status kanode_internal_chain_step(kanode_handle* h, const void* p, const 
     if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_step: ") + hipGetErrorString(e));
     launched = true;
     return KANODE_OK;
+}
+// a whole InterpolatingAdjoint step of a small chain (kd_chain_vjp_step_kernel + its finish): km_out[0..5] <- kμ_2..kμ_7,
+// *err_out <- the λ error total (with want_error); launched = false where the kernel does not cover the chain
+template <typename T>
+static kanode_status chain_adjoint_step_t(kanode_handle* h, const T* p, const kan::ChainAdjStep<T>& a,
+                                          void* const* km_out, double* err_out, int64_t batch, hipStream_t st,
+                                          bool& launched) {
+    const size_t row = (size_t)h->P * sizeof(T) + sizeof(double);
+    int64_t cap = (int64_t)(h->slab_bytes / row) - 1;   // the stage kernel's grid cap (launch_kd_chain_vjp_stage)
+    if (cap > 1024) cap = 1024;
+    if (cap < 1) return KANODE_OK;
+    const size_t need = kan::chain_vjp_step_slab_bytes(h->P, batch, sizeof(T), (int)cap);
+    if (h->cstep_bytes < need) {
+        if (is_capturing(st)) return fail(h, KANODE_ERR_CAPTURE, "chain adjoint step slab grows during capture");
+        HIP_TRY(h, hipStreamSynchronize(st));
+        if (h->cstep_slab) HIP_TRY(h, hipFree(h->cstep_slab));
+        h->cstep_slab = nullptr;
+        h->cstep_bytes = 0;
+        HIP_TRY(h, hipMalloc(&h->cstep_slab, need));
+        h->cstep_bytes = need;
+    }
+    T* km[6];
+    for (int s = 0; s < 6; ++s) km[s] = (T*)km_out[s];
+    const hipError_t e = kan::launch_kd_chain_vjp_step<T>(h->hlc, h->n_layers, h->dlc, p, h->P, batch, a, (int)cap,
+                                                          h->cstep_slab, h->cstep_bytes, km, err_out, st);
+    if (e == hipErrorNotSupported) return KANODE_OK;
+    if (e != hipSuccess) return fail(h, KANODE_ERR_HIP, std::string("launch_kd_chain_vjp_step: ") + hipGetErrorString(e));
+    launched = true;
+    return KANODE_OK;
+}
+kanode_status kanode_internal_chain_adjoint_step(kanode_handle* h, const void* p, const void* args, void* const* km_out,
+                                                 double* err_out, int64_t batch, void* stream, bool& launched) {
+    launched = false;
+    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || !h->fused_step) return KANODE_OK;
+    for (int l = 0; l < h->n_layers; ++l)
+        if (h->kind[l] != KIND_COL) return KANODE_OK;
+    const hipStream_t st = (hipStream_t)stream;
+    return h->spec.dtype == KANODE_F64
+               ? chain_adjoint_step_t<double>(h, (const double*)p, *(const kan::ChainAdjStep<double>*)args, km_out,
+                                              err_out, batch, st, launched)
+               : chain_adjoint_step_t<float>(h, (const float*)p, *(const kan::ChainAdjStep<float>*)args, km_out,
+                                             err_out, batch, st, launched);
 }
 kanode_status kanode_internal_fk_adjoint_loop_geometry(kanode_handle* h, int64_t batch, void* stream, bool& ok,
                                                       double** slab, int64_t* grid) {

@@ -119,6 +119,10 @@ int kanode_internal_pair_adjoint_workgroups(const kanode_handle* h, int64_t batc
 // KANODE_OPT_LAST_ADJOINT: record the path kanode_adjoint_tsit5 took (a kanode_adjoint_path value)
 void kanode_internal_set_last_adjoint(kanode_handle* h, int path);
 // KANODE_OPT_RECORD_ADJOINT_STEPS: the handle's record of the accepted adjoint step sizes, or null when off
+// a whole InterpolatingAdjoint step of a small chain in one launch (+ its reduction): args = kan::ChainAdjStep<T>
+// of the handle's dtype; km_out[0..5] <- kμ_2..kμ_7; launched = false where not covered
+kanode_status kanode_internal_chain_adjoint_step(kanode_handle* h, const void* p, const void* args, void* const* km_out,
+                                                 double* err_out, int64_t batch, void* stream, bool& launched);
 // forward sensitivities of a small Fisher-KPP field in one workgroup (kanode_forward_sensitivity_tsit5)
 bool kanode_internal_fsens_ok(const kanode_handle* h, int64_t batch);
 kanode_status kanode_internal_fk_fsens(kanode_handle* h, const void* p, const void* u0, int64_t batch,

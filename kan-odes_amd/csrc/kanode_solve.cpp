@@ -1578,6 +1578,36 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             SOLVE_TRY(kanode_internal_fk_adjoint_step(h, p, &a, kms, o.adaptive ? ctl(s) + 0 : nullptr, s->batch,
                                                       st, fused_step, &combined, &mup,
                                                       o.adaptive && P <= KANODE_MAX_GRID + 1 ? &af : nullptr));
+        } else {
+            // a small chain: the six stages in one launch (kd_chain_vjp_step_kernel), kμ_2..kμ_7 into km[1..6] and
+            // the λ error into slot 0 by its reduction launch: the same values as the six adj_rhs calls below
+            kan::ChainAdjStep<T> ca{};
+            for (int i = 0; i < 6; ++i) {
+                for (int j = 0; j < 6; ++j) ca.a[i][j] = j <= i ? hstep * TA[i][j] : 0.0;
+                const double t = tf - (i == 5 ? tau + hstep : tau + TC[i] * hstep);
+                int64_t fi = (int64_t)(std::upper_bound(s->ts.begin(), s->ts.end(), t) - s->ts.begin()) - 1;
+                fi = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, fi));
+                const double dti = s->dts[fi];
+                const double th = std::min(1.0, std::max(0.0, (t - s->ts[fi]) / dti));
+                double c[7];
+                interp_weights(th, c);
+                ca.su_u[i] = (const T*)s->u(fi);
+                for (int q = 0; q < 7; ++q) {
+                    ca.su_k[i][q] = (const T*)s->k(fi, q + 1);
+                    ca.su_c[i][q] = c[q] * dti;
+                }
+            }
+            for (int j = 0; j < 7; ++j) ca.ec[j] = hstep * BT[j];
+            ca.abstol = o.abstol;
+            ca.reltol = o.reltol;
+            ca.lam = (const T*)lam[lcur];
+            ca.lam_out = (T*)lam[lcur ^ 1];
+            ca.kl1 = (const T*)kl[0];
+            ca.kl7 = (T*)kl[6];
+            ca.want_error = o.adaptive ? 1 : 0;
+            void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
+            SOLVE_TRY(kanode_internal_chain_adjoint_step(h, p, &ca, kms, o.adaptive ? ctl(s) + 0 : nullptr, s->batch, st,
+                                                         fused_step));
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];

@@ -43,7 +43,7 @@ for path in cc:
             ns = dur[key]
         if not ns:
             continue
-        short = name.split("(")[0].replace("void ", "").replace("kan::", "")
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("kan::", "")
         per[short].append((ns, float(r["Counter_Value"]) / 8.0 / ns))
 for k, v in sorted(per.items(), key=lambda kv: -sum(x[0] for x in kv[1])):
     ghz = sorted(x[1] for x in v)

@@ -21,7 +21,7 @@ for r in csv.DictReader(open(a.trace)):
     name = r["Kernel_Name"]
     if a.grep and a.grep not in name:
         continue
-    short = name.split("(")[0].replace("void ", "").replace("kan::", "")
+    short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("kan::", "")
     grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
     wg = int(r.get("Workgroup_Size") or r.get("Workgroup_Size_X") or 0)
     rows[(short, grid, wg)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
