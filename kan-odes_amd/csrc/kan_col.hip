@@ -763,7 +763,7 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
         T v = r0[q];
 #pragma unroll
         for (int gg = 1; gg < NG; ++gg) v = v + r0[gg * P + q];
-        slab[s * region + (int64_t)blockIdx.x * P + q] = v;
+        slab[s * region + (int64_t)q * gridDim.x + blockIdx.x] = v;   // parameter-major: the finish reads rows
     }
     if (a.want_error) {
         __shared__ double red[kChainVjpBlock / kWave];
@@ -774,7 +774,7 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
 
 #pragma clang diagnostic pop
 
-// km_out[s][q] = Σ_b slab[s·region + b·P + q] (block (q, s), q < P) and err_out[0] = Σ_b err_slab[b] (block (P, 0)):
+// km_out[s][q] = Σ_b slab[s·region + q·nblk + b] (block (q, s), q < P) and err_out[0] = Σ_b err_slab[b] (block (P, 0)):
 // chain_vjp_finish_kernel's sums for the six stages of a step in one launch
 template <typename T>
 __global__ void __launch_bounds__(kBlock)
@@ -786,7 +786,7 @@ chain_vjp_step_finish_kernel(const T* __restrict__ slab, int64_t region, int64_t
     if (q == P && (s != 0 || !err_out)) return;
     double acc = 0.0;
     if (q < P) {
-        acc = strided_rows_sum(slab + s * region + q, nblk, P, acc);
+        acc = strided_rows_sum(slab + s * region + q * nblk, nblk, 1, acc);   // (the same order as a stride-P walk)
     } else {
         acc = strided_rows_sum(err_slab, nblk, 1, acc);
     }

@@ -429,7 +429,7 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
 // A whole InterpolatingAdjoint step of a small chain per trajectory column (kd_chain_vjp_step_kernel, kan_col.hip):
 // the six adjoint stages of kanode_solve.cpp adjoint_t in one launch, λ and kλ_1..kλ_7 of a column in registers.
 // Stage s reads the forward dense output u_i + Σ_q su_c[s][q] k_{i,q} (K form, the forward step holding stage s)
-// and the adjoint stage input λ + Σ_{q<=s} a[s][q] kλ_q; its kμ rows go to slab region s ([grid][P] of T, the
+// and the adjoint stage input λ + Σ_{q<=s} a[s][q] kλ_q; its kμ rows go to slab region s ([P][grid] of T: the
 // stage kernel's per-block sums), the λ error partials (with want_error) after the six regions ([grid] doubles).
 // chain_vjp_step_finish reduces the regions into km_out[0..5] (= kμ_2..kμ_7) and the error total, each in the
 // order chain_vjp_finish_kernel uses: the step is bitwise the six kd_chain_vjp_stage_kernel launches.
