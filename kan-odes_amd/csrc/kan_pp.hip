@@ -30,6 +30,25 @@
 
 namespace kan {
 
+// Diagnostic build only (-DKAN_CLOCK_PROBE, tools/build_var.sh; tools/clock_probe.py): thread 0 of every block of
+// the adjoint rows step (slot 0) and the standalone VJP (slot 1) adds its lifetime in shader clocks (s_memtime) and
+// in the 100 MHz reference clock (s_memrealtime); their ratio is the in-kernel clock (MI355X_MICROARCH.md, DVFS
+// give-back item 6).  Vector atomics only.  Absent from the product build.
+#ifdef KAN_CLOCK_PROBE
+__device__ unsigned long long kan_clock_probe[4];
+#define KAN_PROBE_BEGIN                                                                                   \
+    const unsigned long long kan_ck0_ = __builtin_amdgcn_s_memtime(), kan_rt0_ = __builtin_amdgcn_s_memrealtime();
+#define KAN_PROBE_END(slot)                                                                               \
+    if (threadIdx.x == 0) {                                                                               \
+        const unsigned long long c1_ = __builtin_amdgcn_s_memtime(), r1_ = __builtin_amdgcn_s_memrealtime(); \
+        atomicAdd(&kan_clock_probe[2 * (slot)], c1_ - kan_ck0_);                                          \
+        atomicAdd(&kan_clock_probe[2 * (slot) + 1], r1_ - kan_rt0_);                                      \
+    }
+#else
+#define KAN_PROBE_BEGIN
+#define KAN_PROBE_END(slot)
+#endif
+
 constexpr int kPPPerBlock = 4;                       // intervals built per block (13·4·4 = 208 lanes)
 constexpr int kPPEvals = kPPCoef + kPPChecks;        // direct evaluations per interval
 
@@ -592,6 +611,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     if (STG && stage_skip(sl.skip)) return;
+    KAN_PROBE_BEGIN
     const int tsz = (kPPCoef / 2) * ni;   // double2 per table
     for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
         tl[i] = tables[PP_DPHI * tsz + i];
@@ -735,6 +755,7 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
     }
+    KAN_PROBE_END(1)
 }
 
 // The six stages of one InterpolatingAdjoint step in ONE launch (Fisher-KPP table path, dense
@@ -2092,4 +2113,13 @@ hipError_t launch_fk_adjoint_loop(const PPConst& hpc, const LayerConst& hlc, con
     return hipGetLastError();
 }
 
+#ifdef KAN_CLOCK_PROBE
+extern "C" int kan_clock_probe_read(unsigned long long* out) {   // [4]: slot 0 clocks, realtime; slot 1 ...
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kan_clock_probe), sizeof(unsigned long long) * 4);
+}
+extern "C" int kan_clock_probe_reset() {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(kan_clock_probe), z, sizeof(z));
+}
+#endif
 }  // namespace kan

@@ -1,16 +1,21 @@
-"""The reference's recorded Fisher-KPP training outcome.
+"""The reference's recorded training outcomes, held as properties of three
+initialisations rather than one trajectory's prefix.
 
-The full runs (2e4 iterations, three initialisations; Lotka-Volterra 1e5, three seeds; Allen-Cahn) are
-`tools/anchors.py`, their JSONs under `profiles/r05/anchors/` (and `profiles/r04/anchors/`).  This test keeps
-the product training path on that trajectory: Fisher-KPP_Source.jl:33-109,163-213 (Nx = 26, KAN [1, 1] G = 10
-softsign rbf, native Tsit5 + InterpolatingAdjoint + FusedAdam, ADAM(1e-2)) from a fixed initialisation for
-18,000 iterations: `profiles/r05/anchors/fk_seed1.json`'s run first sits within 0.01 of the recorded fit on
-all of ρ ∈ 0:0.05:1 at iteration 17,500 (0.0100) and is at 0.0068 at 18,000 (0.0047 at 2e4).  The GPU path is
-deterministic (fixed-order reductions, the one-workgroup solve and adjoint), so this is that run's prefix.
-
-Bars: the loss falls from 10.1 below 1e-5 (recorded run: 2.2e-6 here), and the learned source kan1_(ρ) on
-ρ ∈ 0:0.05:1 (Fisher-KPP_Source.jl:237) is within 0.01 of the reference's recorded symbolic fit
-x*(1.0024477071121443-x)*0.9953110353893396 (:234) EVERYWHERE on the grid."""
+The full runs are `tools/anchors.py` (`tools/gpu/r6_anchors.sh`), their JSONs under `profiles/r06/anchors/`.
+Round 6, on the product path as it trains by default (Fisher-KPP: the reference's ForwardDiffSensitivity gradient;
+Lotka-Volterra: the InterpolatingAdjoint):
+  * Fisher-KPP source (Fisher-KPP_Source.jl:33-109,163-213; Nx = 26, KAN [1, 1] G = 10 softsign rbf, ADAM(1e-2),
+    2e4 iterations): the learned kan1_(ρ) on ρ ∈ 0:0.05:1 (:237) against the recorded symbolic fit
+    x*(1.0024477071121443-x)*0.9953110353893396 (:234): max deviation 0.050 (seed 0), 0.0048 (seed 1), 0.0067
+    (seed 2); final loss 9.1e-5, 1.4e-7, 5.3e-7 from 2087, 10.1, 0.20.  Seed 0's initial W = 1.09 makes the first
+    solve's source strongly positive (loss 2087); ADAM(1e-2) leaves that region with loss spikes (3.8e-2 at 10,000)
+    and converges late: 0.087 at 18,000, 0.050 at 20,000.
+  * Lotka-Volterra (LV_driver_KANODE.jl:110-305; [2, 10, 2] G = 5, Adam(5e-4)): loss_train at 2e4 iterations
+    4.9e-4, 3.3e-4, 4.4e-5 (seeds 0, 1, 2); at 1e5 the median over the last 2e4 iterations' log points is 1.3e-6,
+    2.9e-6, 1.5e-6 against the recorded converged 8.3e-7 (trend_plotter.py:7-8).
+The bars below hold every seed to a large drop of its loss and a bounded deviation, and the MEDIAN seed to the
+recorded outcome, each with a margin of 1.5x or more over the recorded run: a rounding-level change of the path
+moves these chaotic trajectories, so no single trajectory's prefix is pinned."""
 import os
 import sys
 
@@ -22,22 +27,49 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
+_FK, _LV = {}, {}
 
-def test_fisher_kpp_source_training_follows_recorded_fit():
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_fisher_kpp_source_training_seed(seed):
     import anchors
-    out = anchors.run_source("fk", iters=18000, seed=1, log_every=1000)
-    print({k: out[k] for k in ("loss_initial", "loss_final", "max_abs_dev_from_recorded_fit",
-                               "ms_per_iteration", "forward_steps", "adjoint_steps")})
-    print("learned", np.round(out["learned_source"], 4).tolist())
-    print("recorded", np.round(out["recorded_fit_values"], 4).tolist())
-    assert out["iters"] == 18000
-    assert out["loss_initial"] > 1.0
-    assert out["loss_final"] < 1e-5
-    lr = np.asarray(out["learned_source"])
-    fit = np.asarray(out["recorded_fit_values"])
-    assert np.all(np.isfinite(lr))
-    assert np.abs(lr - fit).max() <= 0.01
-    assert out["max_abs_dev_from_recorded_fit"] <= 0.01
+    out = anchors.run_source("fk", iters=20000, seed=seed, log_every=2000)
+    _FK[seed] = out
+    print(seed, {k: out[k] for k in ("loss_initial", "loss_final", "max_abs_dev_from_recorded_fit",
+                                     "ms_per_iteration", "sensealg")})
+    assert out["iters"] == 20000 and out["sensealg"] == "forward"
+    assert np.all(np.isfinite(out["learned_source"]))
+    assert out["loss_final"] <= 1e-4 * out["loss_initial"]
+    assert out["max_abs_dev_from_recorded_fit"] <= 0.1
+
+
+def test_fisher_kpp_source_training_median_seed_follows_recorded_fit():
+    if len(_FK) < 3:
+        pytest.skip("needs the three seed runs above")
+    devs = sorted(o["max_abs_dev_from_recorded_fit"] for o in _FK.values())
+    losses = sorted(o["loss_final"] for o in _FK.values())
+    print("deviations", devs, "final losses", losses)
+    assert devs[1] <= 0.01          # the median seed: within 0.01 of the recorded fit everywhere on ρ ∈ 0:0.05:1
+    assert losses[1] <= 1e-5
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_lotka_volterra_training_seed(seed):
+    import anchors
+    out = anchors.run_lv(iters=20000, seed=seed, log_every=5000)
+    _LV[seed] = out
+    print(seed, {k: out[k] for k in ("loss_train_initial", "loss_train_final", "ms_per_iteration")})
+    assert out["loss_train_final"] <= 2e-3                      # recorded: <= 4.9e-4 at 2e4 (4x margin)
+    assert out["loss_train_final"] <= 1e-3 * out["loss_train_initial"]
+
+
+def test_lotka_volterra_training_best_seed():
+    if len(_LV) < 3:
+        pytest.skip("needs the three seed runs above")
+    finals = sorted(o["loss_train_final"] for o in _LV.values())
+    print("loss_train at 2e4", finals)
+    assert finals[0] <= 1e-4                                   # recorded 4.4e-5 (seed 2)
+    assert finals[1] <= 8e-4                                   # recorded median 3.3e-4
 
 
 @pytest.mark.parametrize("tol", [1e-3, 1e-7])
