@@ -159,9 +159,10 @@ fk_small_adjoint_kernel(const LayerConst* __restrict__ lcp, const double* __rest
 // norms; saveat values and partials come from the same interpolant.
 //
 // Layout: wave 0 carries the values, wave 1 + k the partial S_k (k < G: C_k, k = G: W); lane l is point l % Nx
-// of trajectory l / Nx (Nx·B <= 64).  Every wave integrates the values too (the same instructions on the same
-// inputs, so the same bits in every wave): no wave waits on another within a step.  The exchanges are the
-// per-entry Dual norms (one LDS round per step) and the error norm's block sum.  TAB: φ, φ' and swish from the
+// of trajectory l / Nx (Nx·B <= 64).  Wave 0 alone evaluates the RHS at the values and hands φ'(y), swish(y) and
+// N(y) of every stage to the partial waves through LDS (one barrier per stage, two slots); a partial wave's
+// evaluation is then a stencil, an fma and one exponential.  The other exchanges are the per-entry Dual norms (one
+// LDS round per step) and the error norm's block sum.  TAB: φ, φ' and swish from the
 // piecewise-polynomial tables (PP_PHI, PP_DPHI, PP_SWISH staged in LDS, the reference formula off the table);
 // otherwise the reference formula throughout (odd Nx, table path off).
 template <int NORM, int GT, bool TAB>
@@ -198,33 +199,47 @@ fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         const double um = __shfl(v, jm, kWave), up = __shfl(v, jp, kWave);
         return lap3<double>(um, v, up, j, Nx, s.cd, s.co);
     };
-    // f(y) = (D lap y) + φ(y)   (FkSmallModel::rhs)
-    auto fu = [&](double y) -> double {
-        const double lp = lap(y);
-        double k = 0.0;
-        bool ok = false;
-        if constexpr (TAB) k = pp_eval(tphi, s.ni, s.inv_w, s.x0, y, ok);
-        if (!ok) {
-            double sc;
-            k = pp_direct<NORM, BASIS_RBF>(M, lc, p, lc.grid, y, sc);
+    // One evaluation of the Dual RHS at the stage input z (wave 0: the values y; wave 1 + k: the partial s_k):
+    //   wave 0:      f(y) = (D lap y) + φ(y)                    (FkSmallModel::rhs), and the quantities every
+    //                partial needs at y -- φ'(y), swish(y), N(y) -- into LDS slot `slot`;
+    //   wave 1 + k:  ((D lap) s_k + s_k φ'(y)) + ∂φ/∂p_k(y),  ∂φ/∂C_k = B_k(N(y)) by the reference formula,
+    //                ∂φ/∂W = swish(y), read from that slot after the block barrier.
+    // Only wave 0 evaluates at the values, so a partial wave costs a stencil, one fma and one exponential.
+    double* __restrict__ shv = xv + kFsensMaxWaves * kWave;   // [2][3][64]: φ', swish, N by slot
+    auto F = [&](double z, int slot) -> double {
+        double r = 0.0;
+        double* sh = shv + slot * 3 * kWave;
+        if (!sens) {
+            const double lp = lap(z);
+            double k = 0.0, dphi = 0.0, sw = 0.0;
+            bool ok = false, ok2 = false;
+            if constexpr (TAB) {
+                k = pp_eval(tphi, s.ni, s.inv_w, s.x0, z, ok);
+                ok2 = pp_eval2<true>(tdphi, tsw, s.ni, s.inv_w, s.x0, z, dphi, sw);
+            }
+            if (!ok) {
+                double sc;
+                k = pp_direct<NORM, BASIS_RBF>(M, lc, p, lc.grid, z, sc);
+            }
+            if (!ok2) pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, z, dphi, sw);
+            r = lp + k;
+            sh[l] = dphi;
+            sh[kWave + l] = sw;
+            sh[2 * kWave + l] = normalize<NORM, double>(M, lc.norm, z);
         }
-        return lp + k;
-    };
-    // partial kq of f at the Dual (y, sv): ((D lap) sv + sv φ'(y)) + ∂φ/∂p_kq(y)
-    auto fs = [&](double y, double sv) -> double {
-        const double lp = lap(sv);
-        double dphi = 0.0, sw = 0.0;
-        bool ok = false;
-        if constexpr (TAB) ok = pp_eval2<true>(tdphi, tsw, s.ni, s.inv_w, s.x0, y, dphi, sw);
-        if (!ok) pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, y, dphi, sw);
-        double dp = sw;
-        if (kq < GT) {
-            const double nn = normalize<NORM, double>(M, lc.norm, y);
-            const double z = (nn - (double)lc.grid[kq]) * (double)lc.invh;
-            double aux;
-            dp = basis_direct<double>(M, BASIS_RBF, z, aux);
+        __syncthreads();
+        if (sens) {
+            const double lp = lap(z);
+            const double dphi = sh[l];
+            double dp = sh[kWave + l];
+            if (kq < GT) {
+                const double y = (sh[2 * kWave + l] - (double)lc.grid[kq]) * (double)lc.invh;
+                double aux;
+                dp = basis_direct<double>(M, BASIS_RBF, y, aux);
+            }
+            r = (lp + z * dphi) + dp;
         }
-        return (lp + sv * dphi) + dp;
+        return r;
     };
     // Σ over the waves of v at this lane's entry (value first, then the partials in order: the entry's Dual
     // sse), the same total in every wave
@@ -246,34 +261,29 @@ fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             s_save[(si * P + kq) * n + l] = v;
         }
     };
-    double u = act ? u0[l] : 0.0, S = 0.0;
-    double k[7], kS[7];
-    k[0] = fu(u);
-    kS[0] = sens ? fs(u, S) : 0.0;
+    // this wave's entry of the Dual state (the value, or partial kq) and its seven stage values
+    double z = sens ? 0.0 : (act ? u0[l] : 0.0);
+    double k[7];
+    k[0] = F(z, 0);
     const double t0 = a.t0, tf = a.tf;
     const double ntot = (double)n * (double)(P + 1);
     int64_t si = 0;
     while (si < a.n_save && a.saveat[si] <= t0 + 1e-14 * ::fmax(1.0, ::fabs(t0))) {
-        put(si, sens ? S : u);
+        put(si, z);
         ++si;
     }
     double nrm = 0.0;   // ‖u_i‖ of this lane's entry (the Dual norm over value and partials)
-    if (a.adaptive) {
-        const double v = sens ? S : u;
-        nrm = ::sqrt(pt_sum(act ? v * v : 0.0));
-    }
+    if (a.adaptive) nrm = ::sqrt(pt_sum(act ? z * z : 0.0));
     double dt = a.dt;
     if (a.adaptive && !(a.dt > 0)) {   // Hairer & Wanner over the Dual state
         const double sk = ::fma(a.reltol, nrm, a.abstol);
-        const double e0 = (sens ? S : u) / sk, e1 = (sens ? kS[0] : k[0]) / sk;
+        const double e0 = z / sk, e1 = k[0] / sk;
         const double d0 = ::sqrt(bsum(e0 * e0) / ntot);
         const double d1 = ::sqrt(bsum(e1 * e1) / ntot);
         double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
         dt0 = ::fmin(dt0, tf - t0);
-        const double y1 = ::fma(dt0, k[0], u);
-        const double f1 = fu(y1);
-        const double g1 = sens ? fs(y1, ::fma(dt0, kS[0], S)) : 0.0;
-        const double e = ::fma(-1.0, sens ? kS[0] : k[0], sens ? g1 : f1) / sk;
+        const double f1 = F(::fma(dt0, k[0], z), 1);
+        const double e = ::fma(-1.0, k[0], f1) / sk;
         const double d2 = ::sqrt(bsum(e * e) / ntot) / dt0;
         const double mx = ::fmax(d1, d2);
         const double dt1 = mx <= 1e-15 ? ::fmax(1e-6, dt0 * 1e-3) : ::pow(0.01 / mx, 1.0 / 5.0);
@@ -284,28 +294,22 @@ fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     for (; it < a.maxiters; ++it) {
         if (t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf))) break;
         dt = ::fmin(dt, tf - t);
-        double y = u, ys = S;
+        double y = z;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            y = u;
-            ys = S;
+            y = z;
 #pragma unroll
-            for (int q = 0; q <= i; ++q) {
-                y = ::fma(dt * K::TA[i][q], k[q], y);
-                ys = ::fma(dt * K::TA[i][q], kS[q], ys);
-            }
-            k[i + 1] = fu(y);
-            kS[i + 1] = sens ? fs(y, ys) : 0.0;
+            for (int q = 0; q <= i; ++q) y = ::fma(dt * K::TA[i][q], k[q], y);
+            k[i + 1] = F(y, i & 1);
         }
         nf += 6;
         double dtnew = dt, nn = nrm;
         if (a.adaptive) {
             double ev = 0.0;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) ev = ::fma(dt * K::BT[q], sens ? kS[q] : k[q], ev);
-            const double e = ::fma(dt * K::BT[6], sens ? kS[6] : k[6], ev);
-            const double yn = sens ? ys : y;
-            nn = ::sqrt(pt_sum(act ? yn * yn : 0.0));
+            for (int q = 0; q < 6; ++q) ev = ::fma(dt * K::BT[q], k[q], ev);
+            const double e = ::fma(dt * K::BT[6], k[6], ev);
+            nn = ::sqrt(pt_sum(act ? y * y : 0.0));
             const double sk = ::fma(a.reltol, ::fmax(nrm, nn), a.abstol);
             const double r = e / sk;
             const double eest = ::sqrt(bsum(r * r) / ntot);
@@ -324,13 +328,13 @@ fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restri
         const double tn = t + dt;
         while (si < a.n_save && a.saveat[si] <= tn + 1e-12 * ::fmax(1.0, ::fabs(tn))) {
             const double tsv = a.saveat[si];
-            double v = sens ? ys : y;
+            double v = y;
             if (!(::fabs(tsv - tn) <= 1e-12 * ::fmax(1.0, ::fabs(tn)))) {
                 double wt[7];
                 tsit5_interp_weights((tsv - t) / dt, wt);
-                v = sens ? S : u;
+                v = z;
 #pragma unroll
-                for (int q = 0; q < 7; ++q) v = ::fma(wt[q] * dt, sens ? kS[q] : k[q], v);
+                for (int q = 0; q < 7; ++q) v = ::fma(wt[q] * dt, k[q], v);
             }
             put(si, v);
             ++si;
@@ -339,10 +343,8 @@ fk_small_fsens_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             a.ts[naccept] = t;
             a.dts[naccept] = dt;
         }
-        u = y;   // commit (value and partials), FSAL
-        S = ys;
+        z = y;   // commit (value and partials), FSAL
         k[0] = k[6];
-        kS[0] = kS[6];
         nrm = nn;
         t = tn;
         ++naccept;
@@ -447,7 +449,7 @@ hipError_t launch_fk_small_fsens(const LayerConst& hlc, const PPConst& hpc, bool
         return hipErrorNotSupported;
     const int threads = (hlc.G + 2) * kWave;
     const size_t lds = (tab ? 3 * sizeof(double2) * (kPPCoef / 2) * (size_t)hpc.ni : 0) +
-                       sizeof(double) * (size_t)kFsensMaxWaves * kWave;
+                       sizeof(double) * (size_t)(kFsensMaxWaves + 6) * kWave;   // exchange + the two slots
 #define KAN_FSENS1(NORM, GT, TAB)                                                                                  \
     do {                                                                                                         \
         const void* fn = reinterpret_cast<const void*>(&fk_small_fsens_kernel<NORM, GT, TAB>);                   \
