@@ -702,14 +702,15 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
     constexpr int NG = kChainVjpBlock / kChainDim;
     LayerConst* lcl = reinterpret_cast<LayerConst*>(cs_raw);
     T* ps = reinterpret_cast<T*>(cs_raw + nl * sizeof(LayerConst));
-    T* rows = ps + P;                                 // [6][NG][P] gradient rows
+    T* rows = ps + P;                                 // [6 (+1 with fsal)][NG][P] gradient rows
+    const int nreg = a.fsal ? 7 : 6;
     {
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cs_raw);
         for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
         for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
-        for (int i = threadIdx.x; i < 6 * NG * P; i += blockDim.x) rows[i] = T(0);
+        for (int i = threadIdx.x; i < nreg * NG * P; i += blockDim.x) rows[i] = T(0);
     }
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps, rows)
     const Math<T> M{tab};
@@ -722,8 +723,22 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
         const int64_t idx = (int64_t)N0 * k + j;
         const bool live = j < N0;
         T kl[7];
-        const T l0 = live ? a.lam[idx] : T(0);
-        kl[0] = live ? a.kl1[idx] : T(0);
+        T l0 = live ? a.lam[idx] : T(0);
+        if (a.fsal) {   // the stop's jump and FSAL re-evaluation (the stage kernel's arithmetic for that call)
+            T yj = T(0);
+            if (live) {
+                T kv[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) kv[q] = a.j_k[q][idx];
+                yj = a.j_u[idx];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) yj = kfma<T>((T)a.j_c[q], kv[q], yj);
+                for (int r = 0; r < a.njump; ++r) l0 = kfma<T>(T(1), a.jump[r][idx], l0);
+            }
+            kl[0] = chain_pullback<T, NORM, PATH, S>(M, lcl, nl, ps, rows + ((size_t)6 * NG + g) * P, j, yj, l0);
+        } else {
+            kl[0] = live ? a.kl1[idx] : T(0);
+        }
         T ls = l0;
         double ev = 0.0;
 #pragma unroll
@@ -757,7 +772,7 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 6 * P; i += blockDim.x) {   // each stage's block sums, the stage kernel's order
+    for (int i = threadIdx.x; i < nreg * P; i += blockDim.x) {   // each stage's block sums, the stage kernel's order
         const int s = i / P, q = i - s * P;
         const T* r0 = rows + (size_t)s * NG * P;
         T v = r0[q];
@@ -796,7 +811,8 @@ chain_vjp_step_finish_kernel(const T* __restrict__ slab, int64_t region, int64_t
     if (threadIdx.x == 0) {
         double t = red[0];
         for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
-        T* const out = s == 0 ? km.k[0] : s == 1 ? km.k[1] : s == 2 ? km.k[2] : s == 3 ? km.k[3] : s == 4 ? km.k[4] : km.k[5];
+        T* const out = s == 0 ? km.k[0] : s == 1 ? km.k[1] : s == 2 ? km.k[2] : s == 3 ? km.k[3] : s == 4 ? km.k[4]
+                     : s == 5 ? km.k[5] : km.k[6];
         if (q < P) out[q] = (T)t;
         else err_out[0] = t;
     }
@@ -2081,31 +2097,34 @@ hipError_t launch_kd_chain_step(const LayerConst* hlcs, int nl, const LayerConst
 // parameter vector plus the gradient rows fit in LDS; hipErrorNotSupported otherwise.
 size_t chain_vjp_step_slab_bytes(int64_t P, int64_t K, size_t esize, int grid_cap) {
     const int grid = grid_for(K, kChainVjpBlock / kChainDim, grid_cap);
-    return 6 * (((size_t)grid * P * esize + 255) & ~(size_t)255) + (size_t)grid * sizeof(double) + 256;
+    return 7 * (((size_t)grid * P * esize + 255) & ~(size_t)255) + (size_t)grid * sizeof(double) + 256;
+}
+bool chain_vjp_step_supported(const LayerConst* hlcs, int nl, int64_t P, size_t esize) {
+    if (nl < 1 || nl > kChainMaxLayers) return false;
+    for (int l = 0; l < nl; ++l) {
+        const LayerConst& h = hlcs[l];
+        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm) return false;
+        if (l > 0 && h.I != hlcs[l - 1].O) return false;
+    }
+    if (hlcs[nl - 1].O != hlcs[0].I) return false;
+    return nl * sizeof(LayerConst) + (size_t)P * esize * (1 + 7 * (kChainVjpBlock / kChainDim)) <= 64 * 1024;
 }
 
 template <typename T>
 hipError_t launch_kd_chain_vjp_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
                                     int64_t K, const ChainAdjStep<T>& a, int grid_cap, void* slab, size_t slab_bytes,
                                     T* const* km_out, double* err_out, hipStream_t st) {
-    if (nl < 1 || nl > kChainMaxLayers || K < 1 || grid_cap < 1) return hipErrorNotSupported;
-    for (int l = 0; l < nl; ++l) {
-        const LayerConst& h = hlcs[l];
-        if (h.I > kChainDim || h.O > kChainDim || h.path != hlcs[0].path || h.norm != hlcs[0].norm)
-            return hipErrorNotSupported;
-        if (l > 0 && h.I != hlcs[l - 1].O) return hipErrorNotSupported;
-    }
-    if (hlcs[nl - 1].O != hlcs[0].I) return hipErrorNotSupported;
+    if (K < 1 || grid_cap < 1 || !chain_vjp_step_supported(hlcs, nl, P, sizeof(T)) || a.njump > 8)
+        return hipErrorNotSupported;
     const int ng = kChainVjpBlock / kChainDim;
-    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + 6 * ng);
-    if (lds > 64 * 1024) return hipErrorNotSupported;
+    const size_t lds = nl * sizeof(LayerConst) + (size_t)P * sizeof(T) * (1 + (a.fsal ? 7 : 6) * ng);
     // the stage kernel's grid (grid_cap: its slab's row capacity, <= 1024): the same blocks sum the same columns,
     // so the per-block sums and the reduction order are the stage kernel's
     const int grid = grid_for(K, ng, grid_cap);
     if (chain_vjp_step_slab_bytes(P, K, sizeof(T), grid_cap) > slab_bytes) return hipErrorNotSupported;
     const int64_t region = (int64_t)((((size_t)grid * P * sizeof(T) + 255) & ~(size_t)255) / sizeof(T));
     T* tslab = (T*)slab;
-    double* eslab = (double*)((char*)slab + 6 * region * sizeof(T));
+    double* eslab = (double*)((char*)slab + 7 * region * sizeof(T));
     const LayerConst& h = hlcs[0];
 #define KAN_CVSTEP(NORM, PATH, S)                                                                                 \
     hipLaunchKernelGGL((kd_chain_vjp_step_kernel<T, NORM, PATH, S>), dim3(grid), dim3(kChainVjpBlock), lds, st,  \
@@ -2120,8 +2139,9 @@ hipError_t launch_kd_chain_vjp_step(const LayerConst* hlcs, int nl, const LayerC
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     ChainKmOut<T> km{};
-    for (int s = 0; s < 6; ++s) km.k[s] = km_out[s];
-    hipLaunchKernelGGL((chain_vjp_step_finish_kernel<T>), dim3((unsigned)P + 1, 6), dim3(kBlock), 0, st, tslab, region,
+    for (int s = 0; s < (a.fsal ? 7 : 6); ++s) km.k[s] = km_out[s];
+    hipLaunchKernelGGL((chain_vjp_step_finish_kernel<T>), dim3((unsigned)P + 1, a.fsal ? 7 : 6), dim3(kBlock), 0, st,
+                       tslab, region,
                        (int64_t)grid, (int64_t)P, km, eslab, a.want_error ? err_out : nullptr);
     return hipGetLastError();
 }

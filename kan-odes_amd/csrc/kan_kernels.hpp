@@ -435,7 +435,7 @@ hipError_t launch_kd_chain_adjoint(const LayerConst* hlcs, int nl, const LayerCo
 // order chain_vjp_finish_kernel uses: the step is bitwise the six kd_chain_vjp_stage_kernel launches.
 template <typename T>
 struct ChainKmOut {
-    T* k[6];
+    T* k[7];
 };
 template <typename T>
 struct ChainAdjStep {
@@ -449,14 +449,25 @@ struct ChainAdjStep {
     T* lam_out;       // λ_new (stage 6's input)
     const T* kl1;     // kλ_1 (FSAL)
     T* kl7;           // kλ_7
-    int32_t want_error, pad;
+    int32_t want_error;
+    // fsal = 1: the step follows a saveat stop whose jump and FSAL re-evaluation the host folded into it: first
+    // λ' = λ + Σ_r jump[r] (the jump rows, in order) and kλ_1 = λ'ᵀ∂f/∂u at the forward dense output at the stop
+    // (j_u + Σ_q j_c[q] j_k[q]), its kμ_1 into slab region 6 (km_out[6]); the step then starts from λ'
+    int32_t fsal;
+    int32_t njump, pad;
+    const T* jump[8];
+    const T* j_u;
+    const T* j_k[7];
+    double j_c[7];
 };
 template <typename T>
 hipError_t launch_kd_chain_vjp_step(const LayerConst* hlcs, int nl, const LayerConst* lcs, const T* p, int64_t P,
                                     int64_t K, const ChainAdjStep<T>& a, int grid_cap, void* slab, size_t slab_bytes,
-                                    T* const* km_out, double* err_out, hipStream_t st);
+                                    T* const* km_out /* [6], [7] with fsal */, double* err_out, hipStream_t st);
 // slab bytes launch_kd_chain_vjp_step needs for K columns over at most grid_cap blocks
 size_t chain_vjp_step_slab_bytes(int64_t P, int64_t K, size_t esize, int grid_cap);
+// whether launch_kd_chain_vjp_step covers this chain (no launch)
+bool chain_vjp_step_supported(const LayerConst* hlcs, int nl, int64_t P, size_t esize);
 // One Tsit5 step of a small chain per trajectory column (kd_chain_step_kernel, kan_col.hip)
 struct ChainStepArgs {
     double a[6][6];   // dt·a_sj

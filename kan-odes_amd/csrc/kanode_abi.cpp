@@ -1482,8 +1482,8 @@ static kanode_status chain_adjoint_step_t(kanode_handle* h, const T* p, const ka
         HIP_TRY(h, hipMalloc(&h->cstep_slab, need));
         h->cstep_bytes = need;
     }
-    T* km[6];
-    for (int s = 0; s < 6; ++s) km[s] = (T*)km_out[s];
+    T* km[7];
+    for (int s = 0; s < (a.fsal ? 7 : 6); ++s) km[s] = (T*)km_out[s];
     const hipError_t e = kan::launch_kd_chain_vjp_step<T>(h->hlc, h->n_layers, h->dlc, p, h->P, batch, a, (int)cap,
                                                           h->cstep_slab, h->cstep_bytes, km, err_out, st);
     if (e == hipErrorNotSupported) return KANODE_OK;
@@ -1491,12 +1491,18 @@ static kanode_status chain_adjoint_step_t(kanode_handle* h, const T* p, const ka
     launched = true;
     return KANODE_OK;
 }
+bool kanode_internal_chain_adjoint_step_ok(const kanode_handle* h) {
+    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || !h->fused_step) return false;
+    for (int l = 0; l < h->n_layers; ++l)
+        if (h->kind[l] != KIND_COL) return false;
+    const size_t esize = h->spec.dtype == KANODE_F64 ? sizeof(double) : sizeof(float);
+    if ((int64_t)(h->slab_bytes / ((size_t)h->P * esize + sizeof(double))) - 1 < 1) return false;
+    return kan::chain_vjp_step_supported(h->hlc, h->n_layers, h->P, esize);
+}
 kanode_status kanode_internal_chain_adjoint_step(kanode_handle* h, const void* p, const void* args, void* const* km_out,
                                                  double* err_out, int64_t batch, void* stream, bool& launched) {
     launched = false;
-    if (h->spec.rhs_kind != KANODE_RHS_CHAIN || !h->fused_step) return KANODE_OK;
-    for (int l = 0; l < h->n_layers; ++l)
-        if (h->kind[l] != KIND_COL) return KANODE_OK;
+    if (!kanode_internal_chain_adjoint_step_ok(h)) return KANODE_OK;
     const hipStream_t st = (hipStream_t)stream;
     return h->spec.dtype == KANODE_F64
                ? chain_adjoint_step_t<double>(h, (const double*)p, *(const kan::ChainAdjStep<double>*)args, km_out,

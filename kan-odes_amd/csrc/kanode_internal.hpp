@@ -121,8 +121,11 @@ void kanode_internal_set_last_adjoint(kanode_handle* h, int path);
 // KANODE_OPT_RECORD_ADJOINT_STEPS: the handle's record of the accepted adjoint step sizes, or null when off
 // a whole InterpolatingAdjoint step of a small chain in one launch (+ its reduction): args = kan::ChainAdjStep<T>
 // of the handle's dtype; km_out[0..5] <- kμ_2..kμ_7; launched = false where not covered
+// (km_out[6] <- kμ_1 at the folded stop when args.fsal)
 kanode_status kanode_internal_chain_adjoint_step(kanode_handle* h, const void* p, const void* args, void* const* km_out,
                                                  double* err_out, int64_t batch, void* stream, bool& launched);
+// whether kanode_internal_chain_adjoint_step launches for this handle (the host may then fold stops into it)
+bool kanode_internal_chain_adjoint_step_ok(const kanode_handle* h);
 // forward sensitivities of a small Fisher-KPP field in one workgroup (kanode_forward_sensitivity_tsit5)
 bool kanode_internal_fsens_ok(const kanode_handle* h, int64_t batch);
 kanode_status kanode_internal_fk_fsens(kanode_handle* h, const void* p, const void* u0, int64_t batch,

@@ -1484,6 +1484,15 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
     int64_t naccept = 0, nreject = 0, it = 0;
     std::vector<double>* hrec = kanode_internal_adjoint_steps(h);
     if (hrec) hrec->clear();
+    // a small chain whose steps run as one launch each: a stop's jump and FSAL re-evaluation ride in the next
+    // step's launch (ChainAdjStep::fsal) instead of a launch of their own; `pend` holds them until that step
+    // is accepted (a rejected attempt forms them again)
+    const bool fold_stops = !s->qform && kanode_internal_chain_adjoint_step_ok(h);
+    struct {
+        bool on = false;
+        int ng = 0;
+        const void* g[8];
+    } pend;
     // A step that landed on stops[si] (tau == stops[si]): the saveat jump there, if any, and the next stop.
     // k0l / k0m: the current kλ_1 / kμ_1 buffers (the FSAL re-evaluation's outputs).
     auto take_stop = [&](void* k0l, void* k0m) -> kanode_status {
@@ -1492,7 +1501,12 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         for (auto& jm : jumps)
             if (jm.live && (!key || std::fabs(jm.ts - tsv) < std::fabs(key->ts - tsv))) key = &jm;
         if (key && std::fabs(key->ts - tsv) <= eps && si + 1 < stops.size()) {
-            if (key->rows.size() <= (size_t)KANODE_MAX_STAGES) {
+            if (fold_stops && key->rows.size() <= 8) {
+                pend.on = true;
+                pend.ng = 0;
+                for (int64_t r : key->rows) pend.g[pend.ng++] = (const char*)dl_du + r * sb;
+                key->live = false;
+            } else if (key->rows.size() <= (size_t)KANODE_MAX_STAGES) {
                 // callback λ += ∂L/∂u(t_j) and the FSAL re-evaluation (u_modified!) as ONE adjoint
                 // stage: λs = λ + Σ_r 1·g_r (the lincombs' fma order) -> λ_new, kλ_1 = λsᵀJ at λs
                 void* g[KANODE_MAX_STAGES];
@@ -1605,9 +1619,37 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
             ca.kl1 = (const T*)kl[0];
             ca.kl7 = (T*)kl[6];
             ca.want_error = o.adaptive ? 1 : 0;
-            void* kms[6] = {km[1], km[2], km[3], km[4], km[5], km[6]};
+            if (pend.on) {   // the stop's jump and kλ_1 / kμ_1 at τ (adj_rhs's dense output there)
+                const double t = tf - tau;
+                int64_t fi = (int64_t)(std::upper_bound(s->ts.begin(), s->ts.end(), t) - s->ts.begin()) - 1;
+                fi = std::max<int64_t>(0, std::min<int64_t>(nsteps - 1, fi));
+                const double dti = s->dts[fi];
+                const double th = std::min(1.0, std::max(0.0, (t - s->ts[fi]) / dti));
+                double c[7];
+                interp_weights(th, c);
+                ca.fsal = 1;
+                ca.njump = pend.ng;
+                for (int r = 0; r < pend.ng; ++r) ca.jump[r] = (const T*)pend.g[r];
+                ca.j_u = (const T*)s->u(fi);
+                for (int q = 0; q < 7; ++q) {
+                    ca.j_k[q] = (const T*)s->k(fi, q + 1);
+                    ca.j_c[q] = c[q] * dti;
+                }
+            }
+            void* kms[7] = {km[1], km[2], km[3], km[4], km[5], km[6], km[0]};
             SOLVE_TRY(kanode_internal_chain_adjoint_step(h, p, &ca, kms, o.adaptive ? ctl(s) + 0 : nullptr, s->batch, st,
                                                          fused_step));
+            if (pend.on && !fused_step) {   // (not launched after all: the stop's own stage, as take_stop would)
+                double ones[8];
+                void* g[8];
+                for (int r = 0; r < pend.ng; ++r) {
+                    ones[r] = 1.0;
+                    g[r] = const_cast<void*>(pend.g[r]);
+                }
+                SOLVE_TRY(adj_rhs(tau, lam[lcur], pend.ng, g, ones, kl[0], km[0], lam[lcur ^ 1], nullptr, nullptr));
+                lcur ^= 1;
+                pend.on = false;
+            }
         }
         for (int i = 0; i < 6 && !fused_step; ++i) {
             double lc[6];
@@ -1683,6 +1725,7 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         tau = tau + hstep;
         lcur ^= 1;
         mcur ^= 1;
+        pend.on = false;           // (the folded stop, if any, is part of this accepted step)
         std::swap(kl[0], kl[6]);   // FSAL
         std::swap(km[0], km[6]);
         if (hrec) hrec->push_back(hstep);
@@ -1694,6 +1737,12 @@ kanode_status adjoint_t(kanode_handle* h, const void* p, kanode_solution* s, con
         hstep = hnew;
     }
     SOLVE_TRY(kanode_internal_vjp_flush(h, st));   // (a deferred stage's last launch)
+    if (pend.on) {   // (a stop no step followed: maxiters) its jump still belongs to λ
+        for (int r = 0; r < pend.ng; ++r) {
+            const double one = 1.0;
+            SOLVE_TRY(lincomb<T>(h, lam[lcur], 1, &pend.g[r], &one, lam[lcur], n, st));
+        }
+    }
     if (it == o.maxiters && !(tau >= TT - 1e-14 * std::max(1.0, TT)))
         return kanode_internal_fail(h, KANODE_ERR_INVALID_ARG, "adjoint Tsit5: maxiters reached");
     for (auto& jm : jumps)   // a saveat at t0 adds to dL/du0 only
