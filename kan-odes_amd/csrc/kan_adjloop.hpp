@@ -125,11 +125,12 @@ __host__ __device__ inline void adj_loop_plan(const AdjLoopArgs& la, AdjLoopCtl&
 }
 
 // adjoint_t's loop top: done / maxiters, else the step clipped to the next stop (status stays 0)
-__host__ __device__ inline void adj_loop_top(const AdjLoopArgs& la, AdjLoopCtl& c) {
+// stop = stops[c.si] (the host passes its own copy: la.stops is device memory)
+__host__ __device__ inline void adj_loop_top(const AdjLoopArgs& la, AdjLoopCtl& c, double stop) {
     if (c.tau >= la.TT - 1e-14 * (la.TT > 1.0 ? la.TT : 1.0)) c.status = 1;
     else if (c.it >= la.maxiters) c.status = 2;
     else {
-        const double room = la.stops[c.si] - c.tau;
+        const double room = stop - c.tau;
         c.h = c.h < room ? c.h : room;
     }
 }

@@ -34,8 +34,13 @@ namespace kan {
 // the adjoint rows step (slot 0) and the standalone VJP (slot 1) adds its lifetime in shader clocks (s_memtime) and
 // in the 100 MHz reference clock (s_memrealtime); their ratio is the in-kernel clock (MI355X_MICROARCH.md, DVFS
 // give-back item 6).  Vector atomics only.  Absent from the product build.
+// Slots 2.. (same build): s_memrealtime phase sums of the device-controlled loops' kernels (tools/clock_probe.py
+// --phases): the finish launch's last workgroup (reduce, arrive, decide, plan) and the forward DEV step's
+// workgroups (decision, rows).
 #ifdef KAN_CLOCK_PROBE
-__device__ unsigned long long kan_clock_probe[4];
+__device__ unsigned long long kan_clock_probe[16];
+#define KAN_PROBE_T(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime();
+#define KAN_PROBE_ADD(slot, val) atomicAdd(&kan_clock_probe[(slot)], (unsigned long long)(val));
 #define KAN_PROBE_BEGIN                                                                                   \
     const unsigned long long kan_ck0_ = __builtin_amdgcn_s_memtime(), kan_rt0_ = __builtin_amdgcn_s_memrealtime();
 #define KAN_PROBE_END(slot)                                                                               \
@@ -47,6 +52,8 @@ __device__ unsigned long long kan_clock_probe[4];
 #else
 #define KAN_PROBE_BEGIN
 #define KAN_PROBE_END(slot)
+#define KAN_PROBE_T(v)
+#define KAN_PROBE_ADD(slot, val)
 #endif
 
 constexpr int kPPPerBlock = 4;                       // intervals built per block (13·4·4 = 208 lanes)
@@ -1233,9 +1240,17 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
     __shared__ unsigned arr;
     __shared__ AdjLoopCtl cs;   // the state after the decision
     __shared__ int64_t fis[6];
+    KAN_PROBE_T(pf0)
     const AdjLoopCtl* cp = la.ctl;
     if (cp->status != 0) return;
     AdjLoopCtl c = *cp;
+    // the controller's inputs that do not depend on the error terms, on thread 0 while the reduction runs
+    // (only the last workgroup to arrive uses them)
+    double qb2 = 0.0, stop_si = 0.0;
+    if (threadIdx.x == 0) {
+        qb2 = ::pow(c.qold, la.beta2);
+        stop_si = la.stops[c.si];
+    }
     int64_t w0 = c.fi - (kAdjWin - 8);
     if (w0 < 0) w0 = 0;
     const int64_t wn = la.nsteps - w0 < kAdjWin ? la.nsteps - w0 : kAdjWin;
@@ -1248,11 +1263,13 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
     adj_finish_block<false, true>(*(CFin*)&la.plan[c.it & 1].f, la.P, blockIdx.x, red, sums);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's error term has landed
     __syncthreads();
+    KAN_PROBE_T(pf1)
     if (threadIdx.x == 0) arr = __hip_atomic_fetch_add(la.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (arr != gridDim.x - 1u) return;
     if (threadIdx.x <= la.P) terms[threadIdx.x] = ld_agent(la.out + threadIdx.x);
     __syncthreads();
+    KAN_PROBE_T(pf2)
     if (threadIdx.x == 0) {
         double mus = 0.0;   // the μ terms in order, then the λ total (adjoint_t)
         for (int64_t q = 0; q < la.P; ++q) mus += terms[1 + q];
@@ -1265,7 +1282,7 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
             ++c.nreject;
             c.h = c.h / ::fmin(1.0 / la.qmin, q11 / la.gamma);
         } else {
-            double q = q11 / ::pow(c.qold, la.beta2);
+            double q = q11 / qb2;
             q = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, q / la.gamma));
             const double hnew = q > 0 ? c.h / q : c.h * la.qmax;
             c.qold = ::fmax(eest, la.qoldinit);
@@ -1276,15 +1293,16 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
             c.fs ^= 1;   // FSAL: kλ_7, kμ_7 become the next step's first stage values
             ++c.naccept;
             c.h = hnew;
-            if (::fabs(c.tau - la.stops[c.si]) <= 1e-12 * ::fmax(1.0, la.TT)) {
-                c.tau = la.stops[c.si];
+            if (::fabs(c.tau - stop_si) <= 1e-12 * ::fmax(1.0, la.TT)) {
+                c.tau = stop_si;
                 if (c.si + 1 < la.nstops) c.status = 3;   // the host takes the saveat jump and the next stop
             }
         }
-        if (c.status == 0) adj_loop_top(la, c);
+        if (c.status == 0) adj_loop_top(la, c, stop_si);
         cs = c;
     }
     __syncthreads();
+    KAN_PROBE_T(pf3)
     c = cs;
     const int t = threadIdx.x;
     if (c.status == 0) {   // the next attempt's step-dependent fields
@@ -1334,6 +1352,12 @@ __global__ void __launch_bounds__(kAdjFinBlock) adj_finish_loop_kernel(AdjLoopAr
         *la.ctl = c;
         if (c.status != 0 || (c.it & 7) == 0) *la.mirror = c;
         __hip_atomic_store(la.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        KAN_PROBE_T(pf4)
+        KAN_PROBE_ADD(2, pf1 - pf0)   // the last workgroup: start -> its error term landed
+        KAN_PROBE_ADD(3, pf2 - pf1)   // arrival, the terms' loads
+        KAN_PROBE_ADD(4, pf3 - pf2)   // the decision (thread 0)
+        KAN_PROBE_ADD(5, pf4 - pf3)   // the plan fields, the state's store
+        KAN_PROBE_ADD(6, 1)
     }
 }
 
@@ -1404,6 +1428,8 @@ __device__ __forceinline__ bool fk_loop_decide(const FkLoopArgs& la, int64_t q, 
         return false;
     }
     if (c.pending) {
+        // qold^β2 does not depend on the error: formed while the partials are in flight
+        const double qb2 = ::pow(c.qold, la.beta2);
         const double v[1] = {s};
         block_sum_to<double, 1>(v, 1, red, lsum);   // (the same order in every workgroup)
         const double eest = ::sqrt(*lsum / (double)la.n);
@@ -1413,7 +1439,7 @@ __device__ __forceinline__ bool fk_loop_decide(const FkLoopArgs& la, int64_t q, 
             ++c.nreject;
             c.dt = c.dt / ::fmin(1.0 / la.qmin, q11 / la.gamma);
         } else {
-            double qq = q11 / ::pow(c.qold, la.beta2);
+            double qq = q11 / qb2;
             qq = ::fmax(1.0 / la.qmax, ::fmin(1.0 / la.qmin, qq / la.gamma));
             if (1.0 <= qq && qq <= 1.0) qq = 1.0;   // qsteady_min = qsteady_max = 1
             const double dtnew = qq > 0 ? c.dt / qq : c.dt * la.qmax;
@@ -1451,6 +1477,7 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
                        const double* __restrict__ u, const double* __restrict__ k1, StepOut so, StepCoef sc,
                        double* __restrict__ err_slab, int64_t B, FkLoopArgs la, int64_t lq) {
     constexpr int Nx = 128 * NP;
+    KAN_PROBE_T(pw0)
     extern __shared__ double2 tl[];
     __shared__ double red[kBlock / kWave];
     // DEV: the attempt's coefficients in LDS (published by the table staging's barrier below)
@@ -1502,6 +1529,7 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     auto cq = [&](int m, int i) { return DEV ? lsc[0].q[m][i] : sc.q[m][i]; };        // dt·RI[i][m]
     const double abstol = DEV ? la.abstol : sc.abstol, reltol = DEV ? la.reltol : sc.reltol;
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
+    KAN_PROBE_T(pw1)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
     const int lane = threadIdx.x & (kWave - 1);
@@ -1578,8 +1606,16 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
         }
     }
     if constexpr (DEV) {
+        KAN_PROBE_T(pw2)
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
+        if (threadIdx.x == 0) {
+            KAN_PROBE_T(pw3)
+            KAN_PROBE_ADD(8, pw1 - pw0)    // decision + table staging
+            KAN_PROBE_ADD(9, pw2 - pw1)    // rows
+            KAN_PROBE_ADD(10, pw3 - pw2)   // error partial
+            KAN_PROBE_ADD(11, 1)
+        }
     } else if (want_err) {
         const double v[1] = {eacc};
         block_sum_to<double, 1>(v, 1, red, err_slab + blockIdx.x);
@@ -2114,11 +2150,11 @@ hipError_t launch_fk_adjoint_loop(const PPConst& hpc, const LayerConst& hlc, con
 }
 
 #ifdef KAN_CLOCK_PROBE
-extern "C" int kan_clock_probe_read(unsigned long long* out) {   // [4]: slot 0 clocks, realtime; slot 1 ...
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kan_clock_probe), sizeof(unsigned long long) * 4);
+extern "C" int kan_clock_probe_read(unsigned long long* out) {   // [16]: slot 0 clocks, realtime; slot 1 ...; phases
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kan_clock_probe), sizeof(unsigned long long) * 16);
 }
 extern "C" int kan_clock_probe_reset() {
-    const unsigned long long z[4] = {0, 0, 0, 0};
+    const unsigned long long z[16] = {};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(kan_clock_probe), z, sizeof(z));
 }
 #endif

@@ -1274,7 +1274,7 @@ kanode_status adjoint_fk_loop(kanode_handle* h, const void* p, kanode_solution* 
     const volatile kan::AdjLoopCtl* mir = A.hmir;
     for (;;) {
         // (re)start at c: the loop top, the attempt's plan, the state (the stream is drained: the staging is free)
-        kan::adj_loop_top(la, c);
+        kan::adj_loop_top(la, c, stops[(size_t)c.si]);   // (la.stops is the device copy)
         if (c.status != 0) break;
         kan::AdjLoopPlan* hp = (kan::AdjLoopPlan*)A.hplan;
         kan::adj_loop_plan(la, c, *hp, hfw);

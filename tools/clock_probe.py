@@ -25,7 +25,7 @@ from kanode import _lib as L  # noqa: E402
 lib = L.lib()
 if not hasattr(lib, "kan_clock_probe_read"):
     raise SystemExit("not a KAN_CLOCK_PROBE build: set KANODE_LIB to tools/bin/var/clock.so")
-buf = (C.c_ulonglong * 4)()
+buf = (C.c_ulonglong * 16)()
 
 
 def read():
@@ -47,6 +47,12 @@ t0 = time.perf_counter()
 ep = bench.epoch_adaptive_bench(dev, bench.fk_trained_like_params(), 256, 1 / 255, 0.01, 4096, 0, reps=2)
 v = read()
 out["rows_step_epoch_adaptive"] = {"GHz": ghz(v, 0), "clocks": v[0], "realtime_10ns": v[1], "epoch_s": ep["gpu"]}
+# phases of the device-controlled loops' other kernels over the same epochs (us; s_memrealtime is 100 MHz)
+nfin, nfw = max(v[6], 1), max(v[11], 1)
+out["finish_loop_last_workgroup_us"] = {"launches": v[6], "reduce": v[2] / nfin / 100, "arrive_and_terms": v[3] / nfin / 100,
+                                        "decide": v[4] / nfin / 100, "plan_and_state": v[5] / nfin / 100}
+out["forward_dev_step_per_workgroup_us"] = {"workgroups": v[11], "decision_and_tables": v[8] / nfw / 100,
+                                            "rows": v[9] / nfw / 100, "error_partial": v[10] / nfw / 100}
 # the standalone VJP at 1M trajectories (fk_vjp_pp_wave_kernel: slot 1)
 nx = 256
 kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign"))
