@@ -333,6 +333,32 @@ __device__ __forceinline__ T chain_forward(const Math<T>& M, const LayerConst* l
     return a;
 }
 
+// The layer constants (nw words) and the parameters (P) into LDS with every thread's loads in flight before its
+// first store (the plain strided loops wait for each load: at 64 threads and P = 240 that was eight dependent round
+// trips at every block's start)
+template <typename T>
+__device__ __forceinline__ void stage_chain_consts(int32_t* __restrict__ dst, const int32_t* __restrict__ src, int nw,
+                                                   T* __restrict__ ps, const T* __restrict__ p, int P) {
+    constexpr int R = 4;
+    const int nt = blockDim.x, n = nw > P ? nw : P;
+    for (int b = threadIdx.x; b < n; b += R * nt) {
+        int32_t w[R];
+        T v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = b + r * nt;
+            if (i < nw) w[r] = src[i];
+            if (i < P) v[r] = p[i];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = b + r * nt;
+            if (i < nw) dst[i] = w[r];
+            if (i < P) ps[i] = v[r];
+        }
+    }
+}
+
 template <typename T, int NORM, int PATH, class S>
 __global__ void __launch_bounds__(kChainBlock)
 kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restrict__ p, int P,
@@ -345,8 +371,7 @@ kd_chain_col_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __restr
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(chain_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
     }
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps)
     const Math<T> M{tab};
@@ -458,8 +483,7 @@ kd_chain_tsit5_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __res
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cs_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
     }
     KAN_EXP_TABLE_LDS(tab);
     __shared__ double red[kChainBlock / kWave];
@@ -623,8 +647,7 @@ kd_chain_vjp_stage_kernel(const LayerConst* __restrict__ lcs, int nl, const T* _
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int i = threadIdx.x; i < NG * P; i += blockDim.x) rows[i] = T(0);
     }
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps, rows)
@@ -708,8 +731,7 @@ kd_chain_vjp_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cs_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int i = threadIdx.x; i < nreg * NG * P; i += blockDim.x) rows[i] = T(0);
     }
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes lcl, ps, rows)
@@ -1131,8 +1153,7 @@ kd_chain_step_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __rest
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cst_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
     }
     KAN_EXP_TABLE_LDS(tab);
     const Math<T> M{tab};
@@ -1202,8 +1223,7 @@ kd_chain_adjoint_kernel(const LayerConst* __restrict__ lcs, int nl, const T* __r
         const int nw = nl * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(ca_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int i = threadIdx.x; i < NG * P + 9 * P; i += blockDim.x) rows[i] = T(0);
         for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
             tsl[i] = a.ts[i];
@@ -1402,8 +1422,7 @@ kd_chain_adjoint_wide_kernel(const LayerConst* __restrict__ lcs, const T* __rest
         const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cw_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int i = threadIdx.x; i < WideModel<T, NORM>::kEnd + 9 * P; i += blockDim.x) sx[i] = T(0);
         for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
             tsl[i] = a.ts[i];
@@ -1636,8 +1655,7 @@ kd_chain_adjoint_lvwave_kernel(const LayerConst* __restrict__ lcs, const T* __re
         const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int i = threadIdx.x; i < 9 * P; i += blockDim.x) mu[i] = T(0);
         for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
             tsl[i] = a.ts[i];
@@ -1696,8 +1714,7 @@ kd_chain_adjoint_lvsp_kernel(const LayerConst* __restrict__ lcs, const double* _
         const int nw = 2 * (int)(sizeof(LayerConst) / sizeof(int32_t));
         const int32_t* src = reinterpret_cast<const int32_t*>(lcs);
         int32_t* dst = reinterpret_cast<int32_t*>(cv_raw);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < P; i += blockDim.x) ps[i] = p[i];
+        stage_chain_consts(dst, src, nw, ps, p, P);
         for (int64_t i = threadIdx.x; i < a.nsteps; i += blockDim.x) {
             tsl[i] = a.ts[i];
             dtsl[i] = a.dts[i];
