@@ -68,16 +68,19 @@ constexpr int kPPChecks = 3;
 constexpr int kPPMaxIntervals = 512;
 constexpr int kPPMaxFns = 3;
 enum PPFn : int { PP_PHI = 0, PP_DPHI = 1, PP_SWISH = 2 };   // tabulated functions (slot = id)
-// After the kPPMaxFns table slots (kPPCoef·ni doubles each), one stamp per slot: the parameters
-// C_0..C_{G-1}, W the slot was built from, a valid flag and the build kernel's completion counter
-// (fk_pp_build_kernel skips the build when p matches).  pp_tables_doubles() sizes the whole buffer.
+constexpr int kPPPerBlock = 4;   // intervals built per block of fk_pp_build_kernel (13·4·4 = 208 lanes)
+// After the kPPMaxFns table slots (kPPCoef·ni doubles each), one stamp per slot and build block: the parameters
+// C_0..C_{G-1}, W that block's intervals were last built from and a valid flag (fk_pp_build_kernel: a block
+// skips its build when p matches its own stamp; each block reads and writes only its own, so no block waits for
+// another).  pp_tables_doubles() sizes the whole buffer.
 constexpr int kPPStampValid = kMaxGrid + 1;
-constexpr int kPPStampCount = kMaxGrid + 2;
-constexpr int kPPStampStride = kMaxGrid + 3;
-__host__ __device__ inline double* pp_stamp(double* tables, int ni, int fn) {
-    return tables + (int64_t)kPPMaxFns * kPPCoef * ni + (int64_t)fn * kPPStampStride;
+constexpr int kPPStampStride = kMaxGrid + 2;
+__host__ __device__ inline double* pp_stamp(double* tables, int ni, int fn, int blk) {
+    return tables + (int64_t)kPPMaxFns * kPPCoef * ni + ((int64_t)fn * (ni / kPPPerBlock) + blk) * kPPStampStride;
 }
-inline int64_t pp_tables_doubles(int ni) { return (int64_t)kPPMaxFns * (kPPCoef * ni + kPPStampStride); }
+inline int64_t pp_tables_doubles(int ni) {
+    return (int64_t)kPPMaxFns * kPPCoef * ni + (int64_t)kPPMaxFns * (ni / kPPPerBlock) * kPPStampStride;
+}
 struct PPConst {
     int32_t ni;                       // intervals (power of two, multiple of 16)
     int32_t enabled;                  // host admissibility (f64, rbf/rswaf, even Nx)

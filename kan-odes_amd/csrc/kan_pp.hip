@@ -56,7 +56,6 @@ __device__ unsigned long long kan_clock_probe[16];
 #define KAN_PROBE_ADD(slot, val)
 #endif
 
-constexpr int kPPPerBlock = 4;                       // intervals built per block (13·4·4 = 208 lanes)
 constexpr int kPPEvals = kPPCoef + kPPChecks;        // direct evaluations per interval
 
 // One block builds kPPPerBlock intervals of one tabulated function (blockIdx.y
@@ -75,50 +74,15 @@ struct PPFns {
     int fn[kPPMaxFns];
 };
 
-__device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
-                               const double* __restrict__ p, double* __restrict__ tables, PPFns fns);
-
+// Parameter stamp (pp_stamp): block b of function fn built its intervals from the parameters in its own stamp.
+// When p matches it bit for bit the block skips its build.  Every block compares and rewrites only its own stamp,
+// so there is no cross-block ordering to establish (round 5 and before: one stamp per function written by the
+// last block to arrive on a counter, i.e. 64 serialised atomics per build).  The constants a build needs are
+// loaded together with the stamp, so a build costs one memory round trip before its evaluations.
 __global__ void __launch_bounds__(kBlock)
 fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
                    const double* __restrict__ p, double* __restrict__ tables, PPFns fns) {
-    // Parameter stamp (pp_stamp_region): the table of slot fn was last built from the parameters in
-    // its stamp.  When p matches it bit for bit, the blocks skip the build; the last block to finish
-    // (all blocks have compared by then) writes the stamp of this launch.
-    {
-        const PPConst& pc0 = *pcp;
-        const int G0 = lcp->G, fn0 = fns.fn[blockIdx.y];
-        double* __restrict__ stamp = pp_stamp(tables, pc0.ni, fn0);
-        __shared__ int same;
-        if (threadIdx.x < kWave) {
-            const int j = threadIdx.x;
-            const double pj = j <= G0 && (j < G0 || lcp->use_base) ? p[j] : 0.0;
-            const bool ne = j <= G0 && __double_as_longlong(stamp[j]) != __double_as_longlong(pj);
-            const bool valid = stamp[kPPStampValid] == 1.0;
-            if (j == 0) same = 0;
-            const bool any_ne = __any(ne);
-            if (j == 0) same = valid && !any_ne;
-        }
-        __syncthreads();
-        if (!same) pp_build_block(lcp, pcp, p, tables, fns);
-        __syncthreads();   // every thread of this block has written its coefficients
-        if (threadIdx.x == 0) {
-            // no fence: the counter only has to order every block's stamp comparison (completed
-            // before the barrier above: its value decided `same`) before the last block's stamp
-            // write; the table and stamp stores reach the consumers through the kernel boundary.
-            // (An agent-scope __threadfence here wrote back the whole L2 once per block:
-            // buffer_wbl2, 64 of them per build.)
-            unsigned* cnt = reinterpret_cast<unsigned*>(stamp + kPPStampCount);
-            if (atomicAdd(cnt, 1u) == gridDim.x - 1) {
-                for (int j = 0; j <= G0; ++j) stamp[j] = j < G0 || lcp->use_base ? p[j] : 0.0;
-                stamp[kPPStampValid] = 1.0;
-                *cnt = 0u;
-            }
-        }
-    }
-}
-
-__device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst* __restrict__ pcp,
-                               const double* __restrict__ p, double* __restrict__ tables, PPFns fns) {
+    KAN_PROBE_T(pb0)
     __shared__ double sQ[kPPCoef * kPPCoef];
     __shared__ double sT[kPPEvals];              // nodes, then check points
     __shared__ double sC[kMaxGrid + 1];          // C_0..C_{G-1}, W
@@ -127,20 +91,32 @@ __device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst
     __shared__ double sv[kPPPerBlock][kPPChecks];
     __shared__ double cf[kPPPerBlock][kPPCoef];
     __shared__ int bad[kPPPerBlock];
+    __shared__ int same;
     const LayerConst& lc = *lcp;
     const PPConst& pc = *pcp;
     const int tid = threadIdx.x;
     const int G = lc.G;
     const int fn = fns.fn[blockIdx.y];
-    double* __restrict__ table = tables + (int64_t)fn * kPPCoef * pc.ni;
-    // every constant the block needs, loaded in one round (no dependent global loads later)
+    double* __restrict__ stamp = pp_stamp(tables, pc.ni, fn, blockIdx.x);
+    // every constant the build needs and the stamp comparison, in one round of loads
     if (tid < kPPCoef * kPPCoef) sQ[tid] = (&pc.Q[0][0])[tid];
     if (tid < kPPEvals) sT[tid] = tid < kPPCoef ? pc.xi[tid] : pc.tchk[tid - kPPCoef];
     if (tid <= G) sC[tid] = (tid < G || lc.use_base) ? p[tid] : 0.0;
     if (tid < G) sG[tid] = (double)lc.grid[tid];
     if (tid < kPPPerBlock) bad[tid] = 0;
-    KAN_EXP_TABLE_LDS(tab);   // its __syncthreads publishes the constants too
+    if (tid < kWave) {
+        const int j = tid;
+        const double pj = j <= G && (j < G || lc.use_base) ? p[j] : 0.0;
+        const bool ne = j <= G && __double_as_longlong(stamp[j]) != __double_as_longlong(pj);
+        const bool valid = stamp[kPPStampValid] == 1.0;
+        const bool any_ne = __any(ne);
+        if (j == 0) same = valid && !any_ne;
+    }
+    KAN_EXP_TABLE_LDS(tab);   // its __syncthreads publishes the constants and `same` too
+    KAN_PROBE_T(pb1)
+    if (same) return;          // (block-uniform)
     const Math<double> M{tab};
+    double* __restrict__ table = tables + (int64_t)fn * kPPCoef * pc.ni;
     const int k0 = blockIdx.x * kPPPerBlock;
     {
         // evaluation e = tid / 4 (all lanes of a quad take part in the shuffles)
@@ -226,6 +202,15 @@ __device__ void pp_build_block(const LayerConst* __restrict__ lcp, const PPConst
         const int kl = tid / kPPCoef, i = tid - kl * kPPCoef;
         const int64_t k = k0 + kl;
         table[((int64_t)(i >> 1) * pc.ni + k) * 2 + (i & 1)] = bad[kl] ? __builtin_nan("") : cf[kl][i];
+    }
+    // this block's stamp (read only by this block of later launches; published to them by the kernel boundary)
+    if (tid <= G) stamp[tid] = sC[tid];
+    if (tid == 0) stamp[kPPStampValid] = 1.0;
+    KAN_PROBE_T(pb2)
+    if (tid == 0) {
+        KAN_PROBE_ADD(12, pb1 - pb0)   // (diagnostic build) constants + stamp comparison
+        KAN_PROBE_ADD(13, pb2 - pb1)   // the build
+        KAN_PROBE_ADD(15, 1)
     }
 }
 

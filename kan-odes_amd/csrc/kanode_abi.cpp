@@ -1046,10 +1046,8 @@ kanode_status kanode_reserve(kanode_handle* h, int64_t max_batch) {
             h->ws_bytes = need;
         }
     }
-    // Reset the table stamps: the build's skip protocol assumes each slot's arrival counter
-    // is 0 when a launch starts, which holds for stream-ordered launches of one handle; re-zeroing the
-    // stamp region here (the call before graph capture / a new batch) also clears what an aborted
-    // launch could have left, and invalidates the stamps, so the next launch rebuilds every table.
+    // Reset the table stamps: re-zeroing the stamp region here (the call before graph capture / a
+    // new batch) invalidates every build block's stamp, so the next launch rebuilds every table.
     if (h->dtable) {
         const int64_t off = (int64_t)kan::kPPMaxFns * kan::kPPCoef * h->hpc.ni;
         HIP_TRY(h, hipDeviceSynchronize());

@@ -70,4 +70,14 @@ for _ in range(20):
 torch.cuda.synchronize()
 v = read()
 out["vjp_1M"] = {"GHz": ghz(v, 1), "ms_per_call": (time.perf_counter() - t0) / 20 * 1e3}
+# the table build with p changing every call (bench.py's headline loop): slots 12..15
+p2 = p.clone()
+p2[0] += 1e-3
+lib.kan_clock_probe_reset()
+for i in range(40):
+    rhs.hd.rhs(p if i % 2 else p2, u[:131072], torch.empty_like(u[:131072]))
+v = read()
+nb = max(v[15], 1)
+out["pp_build_per_block_us"] = {"blocks": v[15], "stamp_check": v[12] / nb / 100, "build": v[13] / nb / 100,
+                                "arrival": v[14] / nb / 100}
 print(json.dumps(out), flush=True)
