@@ -186,6 +186,22 @@ __device__ __forceinline__ A strided_rows_sum(const T* x, int64_t n, int64_t str
     return s;
 }
 
+// Global -> LDS copy of n 16-byte elements by direct-to-LDS loads (global_load_lds_dwordx4: the destination is the
+// wave-uniform base + lane·16, so each wave copies 64 consecutive elements per instruction).  No VGPR holds the data
+// and no load waits for the one before it: a strided register copy loop waits for each load before its ds_write,
+// one memory round trip per 16·blockDim bytes at every block's start.  The caller's next __syncthreads waits for
+// the copies (hipcc emits vmcnt(0) there while they are outstanding).
+template <typename V>
+__device__ __forceinline__ void lds_copy16(V* lds, const V* g, int n) {
+    static_assert(sizeof(V) == 16, "16-byte elements");
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int base = threadIdx.x & ~(kWave - 1); base < n; base += blockDim.x)
+        if (base + lane < n)
+            __builtin_amdgcn_global_load_lds((gvoid*)(g + base + lane), (lvoid*)(lds + base), 16, 0, 0);
+}
+
 // AGENT: the sums are stored with st_agent (another workgroup of the same launch reads them); sum q goes
 // to out[q·ostride]
 template <typename T, int N, bool AGENT = false>

@@ -260,7 +260,7 @@ fk_rhs_pp_kernel(const LayerConst* __restrict__ lcp, const double* __restrict__ 
                  const double2* __restrict__ table, int ni, double inv_w, double x0, double cd, double co, int Nx,
                  int tpt_log2, const double* __restrict__ u, double* __restrict__ du, int64_t B) {
     extern __shared__ double2 tl[];
-    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];   // (register copy: glds here cost occupancy)
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
     const LayerConst& lc = *lcp;
@@ -496,7 +496,7 @@ fk_rhs_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
             for (int k = 0; k < NP; ++k) v[r][k] = ld_stream(u + br * Nx + 128 * k + 2 * lane);
         }
     }
-    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kRhsBlock) tl[i] = table[i];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kRhsBlock) tl[i] = table[i];   // (direct-to-LDS: 0.8 % slower here)
 #if KAN_PP_COLD_GLOBAL_EXP
     // only the cold direct-formula branch takes exponentials: it reads the 2 KB 2^(j/256) table from
     // global memory instead of every block staging it in LDS
@@ -605,9 +605,14 @@ fk_vjp_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restri
     if (STG && stage_skip(sl.skip)) return;
     KAN_PROBE_BEGIN
     const int tsz = (kPPCoef / 2) * ni;   // double2 per table
-    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
-        tl[i] = tables[PP_DPHI * tsz + i];
-        tl[tsz + i] = tables[PP_SWISH * tsz + i];
+    if constexpr (STG) {   // (the stage form keeps the register copy: the direct-to-LDS loads cost it scratch)
+        for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
+            tl[i] = tables[PP_DPHI * tsz + i];
+            tl[tsz + i] = tables[PP_SWISH * tsz + i];
+        }
+    } else {
+        lds_copy16(tl, tables + PP_DPHI * tsz, tsz);
+        lds_copy16(tl + tsz, tables + PP_SWISH * tsz, tsz);
     }
     KAN_EXP_TABLE_LDS(tab);   // (its __syncthreads also publishes tl)
     const Math<double> M{tab};
@@ -767,7 +772,7 @@ fk_vjp_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __r
     extern __shared__ double2 tl[];
     __shared__ double red[(kVjpBlock / kWave) * (GT + 1)];
     const int tsz = (kPPCoef / 2) * ni;
-    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {
+    for (int i = threadIdx.x; i < tsz; i += kVjpBlock) {   // (register copy: direct-to-LDS loads cost scratch here)
         tl[i] = tables[PP_DPHI * tsz + i];
         tl[tsz + i] = tables[PP_SWISH * tsz + i];
     }
@@ -1469,7 +1474,7 @@ fk_step_pp_wave_kernel(const LayerConst* __restrict__ lcp, const double* __restr
     __shared__ StepCoef lsc[1];
     __shared__ double lsum;
     // the table's loads first: under DEV they overlap the state and partials loads of the decision
-    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];
+    for (int i = threadIdx.x; i < (kPPCoef / 2) * ni; i += kBlock) tl[i] = table[i];   // (register copy: glds here cost occupancy)
     // DEV: this wave's first row is loaded before the decision, for the attempt it will most likely take
     // (the previous one accepted: the next step's u and k_1); a rejection reloads it below
     const int64_t b0 = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
