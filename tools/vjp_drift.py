@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Why the adaptive reference epoch slows down once Adam moves p (tools/epoch_drift.py: the adjoint rows step
+54 -> ~115 us, the forward step unchanged): the standalone VJP timed on the trained-like p and on p after three
+Adam(1e-2) steps, at the initial states and at the states the solve reaches, with random and with tiny cotangents."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kan-odes_amd")]
+import bench  # noqa: E402
+import kanode  # noqa: E402
+
+dev = torch.device("cuda:0")
+nx, dx = 256, 1 / 255
+kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
+rhs = kanode.FisherKPPRHS(kan1, nx=nx, dx=dx, D=0.01, dtype=torch.float64, device=dev)
+u0 = bench.fk_ics(4096, nx, dx, seed=17, device=dev)
+saveat = [0.5 * i for i in range(11)]
+target = (0.9 * u0).unsqueeze(0).expand(len(saveat), -1, -1).contiguous()
+p0 = torch.as_tensor(bench.fk_trained_like_params(), device=dev)
+tr = kanode.Trainer(rhs, u0, (0.0, 5.0), saveat, target, p0.clone(), eta=1e-2, solver=kanode.Tsit5Options())
+for _ in range(3):
+    tr.step()
+p3 = tr.p.clone()
+sol0 = kanode.solve(rhs, u0, (0.0, 5.0), p0, saveat)
+sol3 = kanode.solve(rhs, u0, (0.0, 5.0), p3, saveat)
+u_late0 = sol0.u[-1].contiguous()
+u_late3 = sol3.u[-1].contiguous()
+
+
+def t_vjp(p, u, lam, reps=20):
+    for _ in range(3):
+        rhs.hd.vjp(p, u, lam)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rhs.hd.vjp(p, u, lam)
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) / reps * 1e6, 1)
+
+
+g = torch.Generator(device=dev).manual_seed(0)
+lam = torch.randn(u0.shape, generator=g, dtype=torch.float64, device=dev)
+out = {"p_drift": float((p3 - p0).abs().max()), "p0": p0.tolist(), "p3": p3.tolist()}
+for pn, p in (("p0", p0), ("p3", p3)):
+    for un, u in (("ic", u0), ("late0", u_late0), ("late3", u_late3)):
+        out[f"{pn}_{un}_us"] = t_vjp(p, u, lam)
+        out[f"{pn}_{un}_tinylam_us"] = t_vjp(p, u, lam * 1e-300)
+for un, u in (("ic", u0), ("late0", u_late0), ("late3", u_late3)):
+    out[f"u_{un}_range"] = [float(u.min()), float(u.max())]
+    out[f"u_{un}_frac_neg"] = float((u < 0).double().mean())
+print(json.dumps(out), flush=True)
