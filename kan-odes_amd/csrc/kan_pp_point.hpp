@@ -11,6 +11,9 @@
 #endif
 
 namespace kan {
+#ifdef KAN_CLOCK_PROBE
+extern __device__ unsigned long long kan_clock_probe[16];   // (kan_pp.hip, diagnostic build only)
+#endif
 
 // φ(u) by the reference's formula: normalizer, Σ_j C_j basis((n - g_j)/h) in
 // ascending j, + W swish(u).  `sc` returns Σ|terms|.  NORM / BASIS >= 0 fix the
@@ -168,8 +171,12 @@ __device__ __forceinline__ double pp_vjp_point(const Math<double>& M, const Laye
     // init: the moments and dW start at this point (the same bits as adding it to zeros; saves the
     // zeroing of 30 accumulator registers per stage in the adjoint step kernels)
     double dphi, sw;
-    if (__builtin_expect(!pp_eval2<SPLITH>(td, ts, ni, inv_w, x0, x, dphi, sw), 0))
+    if (__builtin_expect(!pp_eval2<SPLITH>(td, ts, ni, inv_w, x0, x, dphi, sw), 0)) {
+#ifdef KAN_CLOCK_PROBE   // (diagnostic build: points that take the direct formula, tools/vjp_drift.py --count)
+        atomicAdd(&kan_clock_probe[7], 1ull);
+#endif
         pp_direct_dphi_sw<NORM, BASIS_RBF>(M, lc, p, x, dphi, sw);
+    }
     dW = init ? l * sw : ::fma(l, sw, dW);
     const double n = normalize<NORM, double>(M, lc.norm, x);
     double z0, E0, R, taup;

@@ -33,6 +33,21 @@ u_late0 = sol0.u[-1].contiguous()
 u_late3 = sol3.u[-1].contiguous()
 
 
+COUNT = "--count" in sys.argv   # (with the diagnostic build: how many points take the direct formula per call)
+if COUNT:
+    import ctypes as C
+    from kanode import _lib as L
+    _buf = (C.c_ulonglong * 16)()
+
+
+def direct_points(p, u, lam):
+    L.lib().kan_clock_probe_reset()
+    rhs.hd.vjp(p, u, lam)
+    torch.cuda.synchronize()
+    L.lib().kan_clock_probe_read(_buf)
+    return int(_buf[7])
+
+
 def t_vjp(p, u, lam, reps=20):
     for _ in range(3):
         rhs.hd.vjp(p, u, lam)
@@ -51,6 +66,8 @@ for pn, p in (("p0", p0), ("p3", p3)):
     for un, u in (("ic", u0), ("late0", u_late0), ("late3", u_late3)):
         out[f"{pn}_{un}_us"] = t_vjp(p, u, lam)
         out[f"{pn}_{un}_tinylam_us"] = t_vjp(p, u, lam * 1e-300)
+        if COUNT:
+            out[f"{pn}_{un}_direct_points"] = direct_points(p, u, lam)
 for un, u in (("ic", u0), ("late0", u_late0), ("late3", u_late3)):
     out[f"u_{un}_range"] = [float(u.min()), float(u.max())]
     out[f"u_{un}_frac_neg"] = float((u < 0).double().mean())
