@@ -386,6 +386,10 @@ int32_t kanode_forward_sensitivity_supported(const kanode_handle* h, int64_t bat
  * (in backward order), out[i] for i < min(count, cap) (out may be NULL).  Returns the count (0 when not
  * recorded), -1 for NULL. */
 int64_t kanode_adjoint_step_sizes(const kanode_handle* h, double* out, int64_t cap);
+/* Fisher-KPP table path diagnostics (no reference counterpart): out[f] = the intervals of table f (0 φ, 1 φ', 2 swish)
+   its last build rejected (their points take the direct formula), -1 for a table not built yet.  Synchronous
+   (reads the device stamps after the handle's work); KANODE_ERR_UNSUPPORTED without a table path. */
+kanode_status kanode_table_rejections(kanode_handle* h, int32_t out[3]);
 
 /* --- the optimiser step after the gradient all-reduce -----------
  * Flux 0.14 Optimise.Adam + update!(opt, x, Δ) (LV_driver_KANODE.jl:219,287; Fisher-KPP_Source.jl:

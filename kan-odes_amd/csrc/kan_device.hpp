@@ -74,7 +74,8 @@ constexpr int kPPPerBlock = 4;   // intervals built per block of fk_pp_build_ker
 // skips its build when p matches its own stamp; each block reads and writes only its own, so no block waits for
 // another).  pp_tables_doubles() sizes the whole buffer.
 constexpr int kPPStampValid = kMaxGrid + 1;
-constexpr int kPPStampStride = kMaxGrid + 2;
+constexpr int kPPStampRejected = kMaxGrid + 2;   // intervals of the block the last build rejected (direct formula)
+constexpr int kPPStampStride = kMaxGrid + 3;
 __host__ __device__ inline double* pp_stamp(double* tables, int ni, int fn, int blk) {
     return tables + (int64_t)kPPMaxFns * kPPCoef * ni + ((int64_t)fn * (ni / kPPPerBlock) + blk) * kPPStampStride;
 }

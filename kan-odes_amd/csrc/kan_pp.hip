@@ -38,7 +38,7 @@ namespace kan {
 // --phases): the finish launch's last workgroup (reduce, arrive, decide, plan) and the forward DEV step's
 // workgroups (decision, rows).
 #ifdef KAN_CLOCK_PROBE
-__device__ unsigned long long kan_clock_probe[16];
+__device__ unsigned long long kan_clock_probe[32];
 #define KAN_PROBE_T(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime();
 #define KAN_PROBE_ADD(slot, val) atomicAdd(&kan_clock_probe[(slot)], (unsigned long long)(val));
 #define KAN_PROBE_BEGIN                                                                                   \
@@ -155,23 +155,27 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
             // conversion rounds at ~|Q|·eps·(variation over the interval, ~w·|f'|), so
             // where every term vanishes (swish(0) = 0) the floor keeps a correct fit from
             // being rejected; it admits absolute errors <= 2.5e-15 of that magnitude.
+            // (magnitudes by compare-and-negate: with the |x| source modifier the swish branch's scale came out
+            // as base + 4w(1 + u), negative below u ≈ -0.2, which rejected every swish interval there and sent
+            // those points of the VJP to the direct formula; tools/pp_direct_scan.py)
+            auto mag = [](double x) { return x < 0.0 ? -x : x; };
             double csum = 0.0;
-            for (int j = 0; j < G; ++j) csum += kabs(sC[j]);
-            const double wabs = lc.use_base ? kabs(sC[G]) : 0.0;
+            for (int j = 0; j < G; ++j) csum += mag(sC[j]);
+            const double wabs = lc.use_base ? mag(sC[G]) : 0.0;
             double v, sc, ref;
             if (fn == PP_PHI) {
                 v = s + base;
-                sc = a + kabs(base);
+                sc = a + mag(base);
                 ref = csum + wabs;
             } else if (fn == PP_DPHI) {
                 const double dn = dnormalize<NORM_RUNTIME, double>(lc.norm, n);
                 v = dn * s + base;
-                sc = dn * a + kabs(base);
+                sc = dn * a + mag(base);
                 ref = csum * invh + wabs;
             } else {
                 v = base;
-                sc = kabs(base);
-                ref = 1.0 + kabs(u);
+                sc = mag(base);
+                ref = 1.0 + mag(u);
             }
             sc += 4.0 * pc.w * ref;
             fv[kl][m] = v;
@@ -195,7 +199,15 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
         double y = cf[kl][kPPCoef - 1];
 #pragma unroll
         for (int i = kPPCoef - 2; i >= 0; --i) y = ::fma(y, t, cf[kl][i]);
-        if (!(kabs(y - fv[kl][kPPCoef + c]) <= pc.tol * sv[kl][c])) bad[kl] = 1;
+        if (!(kabs(y - fv[kl][kPPCoef + c]) <= pc.tol * sv[kl][c])) {
+            bad[kl] = 1;
+#ifdef KAN_CLOCK_PROBE   // (diagnostic build: rejected intervals per function and the worst residual / tolerance)
+            atomicAdd(&kan_clock_probe[16 + fn], 1ull);
+            const double r = kabs(y - fv[kl][kPPCoef + c]) / (pc.tol * sv[kl][c]);
+            atomicMax(&kan_clock_probe[19], (unsigned long long)__double_as_longlong(r == r ? r : 1e300));
+            atomicMax(&kan_clock_probe[20 + fn], (unsigned long long)(k0 + kl));
+#endif
+        }
     }
     __syncthreads();
     if (tid < kPPPerBlock * kPPCoef) {
@@ -205,7 +217,12 @@ fk_pp_build_kernel(const LayerConst* __restrict__ lcp, const PPConst* __restrict
     }
     // this block's stamp (read only by this block of later launches; published to them by the kernel boundary)
     if (tid <= G) stamp[tid] = sC[tid];
-    if (tid == 0) stamp[kPPStampValid] = 1.0;
+    if (tid == 0) {
+        stamp[kPPStampValid] = 1.0;
+        int nbad = 0;
+        for (int q = 0; q < kPPPerBlock; ++q) nbad += bad[q];
+        stamp[kPPStampRejected] = (double)nbad;   // (kanode_table_rejections)
+    }
     KAN_PROBE_T(pb2)
     if (tid == 0) {
         KAN_PROBE_ADD(12, pb1 - pb0)   // (diagnostic build) constants + stamp comparison
@@ -2140,11 +2157,11 @@ hipError_t launch_fk_adjoint_loop(const PPConst& hpc, const LayerConst& hlc, con
 }
 
 #ifdef KAN_CLOCK_PROBE
-extern "C" int kan_clock_probe_read(unsigned long long* out) {   // [16]: slot 0 clocks, realtime; slot 1 ...; phases
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kan_clock_probe), sizeof(unsigned long long) * 16);
+extern "C" int kan_clock_probe_read(unsigned long long* out) {   // [32]: slot 0 clocks, realtime; slot 1 ...; phases
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kan_clock_probe), sizeof(unsigned long long) * 32);
 }
 extern "C" int kan_clock_probe_reset() {
-    const unsigned long long z[16] = {};
+    const unsigned long long z[32] = {};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(kan_clock_probe), z, sizeof(z));
 }
 #endif

@@ -12,7 +12,7 @@
 
 namespace kan {
 #ifdef KAN_CLOCK_PROBE
-extern __device__ unsigned long long kan_clock_probe[16];   // (kan_pp.hip, diagnostic build only)
+extern __device__ unsigned long long kan_clock_probe[32];   // (kan_pp.hip, diagnostic build only)
 #endif
 
 // φ(u) by the reference's formula: normalizer, Σ_j C_j basis((n - g_j)/h) in

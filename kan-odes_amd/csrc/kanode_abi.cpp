@@ -1707,6 +1707,26 @@ std::vector<double>* kanode_internal_adjoint_steps(kanode_handle* h) {
     return h->record_adj_steps ? &h->adj_steps : nullptr;
 }
 
+extern "C" kanode_status kanode_table_rejections(kanode_handle* h, int32_t out[3]) {
+    if (!h || !out) return KANODE_ERR_INVALID_ARG;
+    if (!h->dtable || !h->pp_on) return fail(h, KANODE_ERR_UNSUPPORTED, "no pointwise table on this handle");
+    const int ni = h->hpc.ni, nb = ni / kan::kPPPerBlock;
+    const int64_t off = (int64_t)kan::kPPMaxFns * kan::kPPCoef * ni;
+    std::vector<double> st((size_t)kan::kPPMaxFns * nb * kan::kPPStampStride);
+    HIP_TRY(h, hipDeviceSynchronize());
+    HIP_TRY(h, hipMemcpy(st.data(), h->dtable + off, st.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int f = 0; f < kan::kPPMaxFns; ++f) {
+        int32_t n = 0;
+        bool built = true;
+        for (int b = 0; b < nb; ++b) {
+            const double* sp = st.data() + ((size_t)f * nb + b) * kan::kPPStampStride;
+            if (sp[kan::kPPStampValid] != 1.0) built = false;
+            else n += (int32_t)sp[kan::kPPStampRejected];
+        }
+        out[f] = built ? n : -1;
+    }
+    return KANODE_OK;
+}
 extern "C" int64_t kanode_adjoint_step_sizes(const kanode_handle* h, double* out, int64_t cap) {
     if (!h) return -1;
     const int64_t n = (int64_t)h->adj_steps.size();

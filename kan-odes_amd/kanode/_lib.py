@@ -134,6 +134,7 @@ SIGNATURES = [
                                      _P, C.POINTER(SolverOptsC), C.POINTER(C.c_void_p), C.POINTER(SolveStatsC), _P]),
     ("kanode_adjoint_tsit5", C.c_int, [_H, _P, _P, _P, _P, _P, C.POINTER(SolverOptsC), C.POINTER(SolveStatsC), _P]),
     ("kanode_adjoint_step_sizes", C.c_int64, [_H, _P, C.c_int64]),
+    ("kanode_table_rejections", C.c_int, [_H, _P]),
     ("kanode_forward_sensitivity_tsit5", C.c_int, [_H, _P, _P, C.c_int64, C.c_double, C.c_double,
                                                    C.POINTER(C.c_double), C.c_int64, _P, _P, C.POINTER(SolverOptsC),
                                                    C.POINTER(SolveStatsC), _P]),

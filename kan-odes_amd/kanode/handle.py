@@ -379,6 +379,13 @@ class KanodeHandle:
                 self._h, "kanode_adjoint_tsit5")
         return du0, dp, dict(naccept=st.naccept, nreject=st.nreject, nf=st.nf)
 
+    def table_rejections(self):
+        """Intervals the last table builds rejected: (φ, φ', swish), -1 for a table not built yet
+        (kanode_table_rejections; their points take the direct formula)."""
+        out = (C.c_int32 * 3)()
+        L.check(L.lib().kanode_table_rejections(self._h, out), self._h, "kanode_table_rejections")
+        return tuple(int(x) for x in out)
+
     def adjoint_step_sizes(self):
         """The accepted step sizes of the last adjoint_tsit5 (option record_adjoint_steps; else empty)."""
         n = int(L.lib().kanode_adjoint_step_sizes(self._h, None, 0))

@@ -340,3 +340,23 @@ def test_table_stamp_sees_a_change_of_w_alone(use_base):
         assert np.max(np.abs(du.cpu().numpy() - ref)) <= 1e-13 * scale
         assert np.max(np.abs(lamJ.cpu().numpy() - rJ)) <= 1e-12 * (np.max(np.abs(rJ)) + 4 * 0.01 * 255 ** 2)
         assert np.max(np.abs(dp.cpu().numpy() - rdp)) <= 1e-11 * np.max(np.abs(rdp))
+
+
+@pytest.mark.parametrize("which", ["trained", "random"])
+def test_tables_accept_every_interval(which):
+    """Round 6: the table build rejected every swish interval below u ≈ -0.16 (its acceptance scale, formed with the
+    |x| source modifier, came out negative there), so the VJP and the adjoint rows step sent those points to the
+    direct formula: 2-4x slower once training drove the states negative (DESIGN round 6).  The reference KAN is
+    smooth on the whole table range [-4, 4) but for softsign's kink at 0, an interval edge, so no interval of
+    φ, φ' or swish may be rejected, at the trained-like parameters and at random ones."""
+    import bench
+    dev = device()
+    kan1 = kanode.Chain(kanode.KDense(1, 1, 10, normalizer="softsign", basis_func="rbf"))
+    rhs = kanode.FisherKPPRHS(kan1, nx=256, dx=1 / 255, D=0.01, dtype=torch.float64, device=dev)
+    p = (bench.fk_trained_like_params() if which == "trained"
+         else np.random.default_rng(3).normal(0.0, 1.0, 11))
+    p = torch.as_tensor(p, device=dev)
+    u = torch.linspace(-3.9, 3.9, 8 * 256, dtype=torch.float64, device=dev).reshape(8, 256)
+    rhs.hd.rhs(p, u, torch.empty_like(u))
+    rhs.hd.vjp(p, u, torch.ones_like(u))
+    assert rhs.hd.table_rejections() == (0, 0, 0)

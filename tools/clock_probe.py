@@ -25,7 +25,7 @@ from kanode import _lib as L  # noqa: E402
 lib = L.lib()
 if not hasattr(lib, "kan_clock_probe_read"):
     raise SystemExit("not a KAN_CLOCK_PROBE build: set KANODE_LIB to tools/bin/var/clock.so")
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 
 
 def read():

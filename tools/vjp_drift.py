@@ -37,7 +37,7 @@ COUNT = "--count" in sys.argv   # (with the diagnostic build: how many points ta
 if COUNT:
     import ctypes as C
     from kanode import _lib as L
-    _buf = (C.c_ulonglong * 16)()
+    _buf = (C.c_ulonglong * 32)()
 
 
 def direct_points(p, u, lam):
