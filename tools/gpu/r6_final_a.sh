@@ -2,7 +2,7 @@
 # round-6 closing run, part A: the whole GPU suite and smoke() on the final tree
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp
-O=gpurun_out/r6_final; mkdir -p $O
+O=gpurun_out/${R6_FINAL:-r6_final}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest -v --timeout 300 --timeout-method thread tests -m gpu > $O/pytest_gpu.txt 2>&1
 rc=$?
 tail -3 $O/pytest_gpu.txt
