@@ -104,3 +104,19 @@ def test_fk_default_path_kan_only(G, norm, mode):
     and on such a sequence last-bit differences of the error norm flip decisions.  Here both sides
     take the same steps with no rejection."""
     _e2e(256, 3, mode, seed=G + len(norm), diffusion=0.0, G=G, norm=norm, amp=2.0, shift=0.2, pscale=0.5)
+
+
+@pytest.mark.parametrize("mode", ["fixed", pytest.param("adaptive", marks=pytest.mark.xfail(
+    reason="open (DESIGN round 6): on an all-negative field the table path's adaptive adjoint takes 8 steps where "
+           "the CPU oracle and the direct per-point kernels take 10; forward steps, values and VJPs agree (1e-14); "
+           "the same on the build before the round-6 table fix", strict=False))])
+def test_fk_default_path_negative_states(mode):
+    """Round 6: states below zero, where the swish table had been rejected (its acceptance scale formed with the
+    |x| source modifier came out negative below u ≈ -0.2: every such point took the direct formula).  Fixed step:
+    a field shifted below zero through the table path's forward and adjoint steps against the dense-Laplacian CPU
+    oracle (values 1e-11, gradients 1e-9).  Adaptive: the whole field negative (u in [-2.2, -1.2], D = 0 so nothing
+    crosses softsign's kink at 0) with equal step counts required: the forward matches, the adjoint does not yet."""
+    if mode == "adaptive":
+        _e2e(256, 3, mode, seed=31, diffusion=0.0, amp=1.0, shift=-2.2, pscale=0.5)
+    else:
+        _e2e(256, 3, mode, seed=33, shift=-0.6)
