@@ -50,7 +50,8 @@ def _run(f, dev, u0, p0, tspan, ts, w, opt):
     return sol.u.detach().cpu(), gp.cpu(), gu.cpu(), sol.stats
 
 
-def _e2e(nx, B, mode, seed, diffusion=D, G=10, norm="softsign", amp=1.0, shift=0.0, pscale=1.0, **opts):
+def _e2e(nx, B, mode, seed, diffusion=D, G=10, norm="softsign", amp=1.0, shift=0.0, pscale=1.0, adjoint_counts=True,
+         **opts):
     dx = 1.0 / (nx - 1)
     gpu = kanode.FisherKPPRHS(kanode.Chain(kanode.KDense(1, 1, G, normalizer=norm)), nx=nx, dx=dx, D=diffusion,
                               device=device())
@@ -71,8 +72,9 @@ def _e2e(nx, B, mode, seed, diffusion=D, G=10, norm="softsign", amp=1.0, shift=0
         ug, gg, gug, sg = _run(gpu, device(), t(u0), p0, tspan, ts, w, opt)
     uc, gc, guc, sc = _run(cpu, "cpu", torch.as_tensor(u0), p0, tspan, ts, w, opt)
     assert (sg["naccept"], sg["nreject"]) == (sc["naccept"], sc["nreject"])
-    assert (sg["adjoint"]["naccept"], sg["adjoint"]["nreject"]) == (sc["adjoint"]["naccept"],
-                                                                    sc["adjoint"]["nreject"])
+    if adjoint_counts:
+        assert (sg["adjoint"]["naccept"], sg["adjoint"]["nreject"]) == (sc["adjoint"]["naccept"],
+                                                                        sc["adjoint"]["nreject"])
     assert sg["naccept"] >= (40 if mode == "fixed" else 5)
     assert (ug - uc).abs().max().item() <= 1e-11
     assert (gg - gc).abs().max().item() <= 1e-9 * gc.abs().max().item()
@@ -106,17 +108,18 @@ def test_fk_default_path_kan_only(G, norm, mode):
     _e2e(256, 3, mode, seed=G + len(norm), diffusion=0.0, G=G, norm=norm, amp=2.0, shift=0.2, pscale=0.5)
 
 
-@pytest.mark.parametrize("mode", ["fixed", pytest.param("adaptive", marks=pytest.mark.xfail(
-    reason="open (DESIGN round 6): on an all-negative field the table path's adaptive adjoint takes 8 steps where "
-           "the CPU oracle and the direct per-point kernels take 10; forward steps, values and VJPs agree (1e-14); "
-           "the same on the build before the round-6 table fix", strict=False))])
+@pytest.mark.parametrize("mode", ["fixed", "adaptive"])
 def test_fk_default_path_negative_states(mode):
     """Round 6: states below zero, where the swish table had been rejected (its acceptance scale formed with the
     |x| source modifier came out negative below u ≈ -0.2: every such point took the direct formula).  Fixed step:
     a field shifted below zero through the table path's forward and adjoint steps against the dense-Laplacian CPU
     oracle (values 1e-11, gradients 1e-9).  Adaptive: the whole field negative (u in [-2.2, -1.2], D = 0 so nothing
-    crosses softsign's kink at 0) with equal step counts required: the forward matches, the adjoint does not yet."""
+    crosses softsign's kink at 0): equal forward step counts, values and gradients at the file's bars, adjoint step
+    counts NOT compared.  On this field the source is nearly linear and the adjoint's embedded error sits at the
+    rounding level, so its step sizes follow last-bit noise: the oracle's own VJP perturbed by 1e-15 relative moves
+    its second step 2%, by 1e-14 it takes 8 steps instead of 10 (tests/test_oracle_step_noise.py, on the CPU); the
+    table path takes 8, the direct kernels 10, all with dL/dp equal to 3e-13 (profiles/r06/negative)."""
     if mode == "adaptive":
-        _e2e(256, 3, mode, seed=31, diffusion=0.0, amp=1.0, shift=-2.2, pscale=0.5)
+        _e2e(256, 3, mode, seed=31, diffusion=0.0, amp=1.0, shift=-2.2, pscale=0.5, adjoint_counts=False)
     else:
         _e2e(256, 3, mode, seed=33, shift=-0.6)
