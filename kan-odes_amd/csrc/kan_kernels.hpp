@@ -355,6 +355,7 @@ struct ChainSolveArgs {
     double* ts;       // [cap] step start times (with rec)
     double* dts;      // [cap] step sizes (with rec)
     int64_t* out;     // naccept, nreject, nf, status
+    double* hts;      // or null: mapped host copy of ts | dts ([2][cap], with rec), fenced before out is written
 };
 // InterpolatingAdjoint of a small chain in one workgroup (kd_chain_adjoint_kernel): the backward
 // Tsit5 over [λ; μ] of kanode_solve.cpp adjoint_t, reading the dense output that

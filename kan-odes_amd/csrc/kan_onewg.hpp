@@ -143,6 +143,10 @@ __device__ __forceinline__ void onewg_tsit5(Mdl& m, const T* __restrict__ u0, co
             if (threadIdx.x == 0) {
                 a.ts[naccept] = t;
                 a.dts[naccept] = dt;
+                if (a.hts) {
+                    a.hts[naccept] = t;
+                    a.hts[a.cap + naccept] = dt;
+                }
             }
         }
         u = y;   // commit u <- u_new, k_1 <- k_7 (FSAL)
@@ -153,6 +157,7 @@ __device__ __forceinline__ void onewg_tsit5(Mdl& m, const T* __restrict__ u0, co
     }
     if (status == 0 && it == a.maxiters && !(t >= tf - 1e-14 * ::fmax(1.0, ::fabs(tf)))) status = 1;
     if (threadIdx.x == 0) {
+        if (a.hts) __threadfence_system();   // the host reads the step records once it sees the counters
         a.out[0] = naccept;
         a.out[1] = nreject;
         a.out[2] = nf + 1;

@@ -117,7 +117,8 @@ struct kanode_solution {
         int64_t saveat_cap = 0;
         double* ts = nullptr;              // [cap] then dts [cap]
         int64_t ts_cap = 0;
-        double* hts = nullptr;             // pinned host staging of ts | dts
+        double* hts = nullptr;             // pinned host staging of ts | dts (mapped, coherent)
+        double* mts = nullptr;             // its device address (null: copied)
         int64_t hts_cap = 0;
         int64_t* out = nullptr;            // naccept, nreject, nf, status
         void* adj_meta = nullptr;          // adjoint: stops, jump rows and offsets
@@ -728,23 +729,29 @@ kanode_status solve_fused_t(kanode_handle* h, const void* p, const void* u0, dou
     // the counters straight into the mapped host mirror when there is one (no copy launch to read them); without
     // step records to fetch, the host then spins on them instead of synchronising the stream (wait_ctl: the
     // wake-up of hipStreamSynchronize is ~20 us; what follows on the stream is ordered after the kernel anyway)
+    // the step records: pinned, mapped host staging the kernel writes alongside the device copy (else copied)
+    if (s->record && f.hts_cap < f.cap) {
+        if (f.hts) (void)hipHostFree(f.hts);
+        f.hts = nullptr;
+        f.mts = nullptr;
+        f.hts_cap = 0;
+        SOLVE_HIP(h, hipHostMalloc((void**)&f.hts, 2 * (size_t)f.cap * sizeof(double),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+        f.hts_cap = f.cap;
+        if (hipHostGetDevicePointer((void**)&f.mts, f.hts, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            f.mts = nullptr;
+        }
+    }
     a.out = s->mscal ? (int64_t*)s->mscal : f.out;
-    const bool spin = s->mscal && !s->record;
+    a.hts = s->record && s->mscal ? f.mts : nullptr;
+    const bool spin = s->mscal && (!s->record || a.hts);
     if (spin) arm_ctl(s->hscal, 4);
     bool launched = false;
     SOLVE_TRY(kanode_internal_chain_tsit5(h, p, u0, s->batch, &a, st, launched));
     if (!launched) return KANODE_OK;
-    // the counters and the step records in one stream synchronisation (the records through pinned staging,
-    // whole: their length is what the counters say)
-    if (s->record && f.hts_cap < f.cap) {
-        if (f.hts) (void)hipHostFree(f.hts);
-        f.hts = nullptr;
-        f.hts_cap = 0;
-        SOLVE_HIP(h, hipHostMalloc((void**)&f.hts, 2 * (size_t)f.cap * sizeof(double)));
-        f.hts_cap = f.cap;
-    }
     if (!s->mscal) SOLVE_HIP(h, hipMemcpyAsync(s->hscal, f.out, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    if (s->record)
+    if (s->record && !a.hts)
         SOLVE_HIP(h, hipMemcpyAsync(f.hts, f.ts, 2 * (size_t)f.cap * sizeof(double), hipMemcpyDeviceToHost, st));
     if (spin) SOLVE_TRY(wait_ctl(h, st, {{s->hscal, 4}}));
     else SOLVE_HIP(h, hipStreamSynchronize(st));
@@ -2187,6 +2194,7 @@ extern "C" kanode_status kanode_forward_sensitivity_tsit5(kanode_handle* h, cons
     if (f.hts_cap < f.ts_cap) {
         if (f.hts) (void)hipHostFree(f.hts);
         f.hts = nullptr;
+        f.mts = nullptr;
         f.hts_cap = 0;
         SOLVE_HIP(h, hipHostMalloc((void**)&f.hts, 2 * (size_t)f.ts_cap * sizeof(double)));
         f.hts_cap = f.ts_cap;

@@ -9,3 +9,4 @@ for r in 1 2 3; do
   timeout -k 10 120 python3 -u tools/lv1_probe.py --reps 100 --rounds 3 > $O/new_$r.json 2>&1
 done
 timeout -k 10 240 python3 -u tools/lv1_iter_cprofile.py --reps 300 > $O/cprofile_new.txt 2>&1
+[ -z "$WITH_BENCH" ] || timeout -k 10 600 python3 -u bench.py > $O/bench.json 2> $O/bench.err
