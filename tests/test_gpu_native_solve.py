@@ -441,6 +441,35 @@ def test_fused_chain_adjoint_saveat_edges(ts):
     assert (ua - uh).abs().max().item() <= 1e-9 * max(1e-300, uh.abs().max().item())
 
 
+def test_fused_chain_repeated_calls_with_changing_saveat_are_bitwise_fresh():
+    """Round 6: the one-workgroup solve and adjoint skip a saveat / stop upload whose bytes equal the last one, and
+    read their counters and step records from mapped host memory (kanode_solve.cpp solve_fused_t, adjoint_fused_t).
+    Alternating saveat lists (same length, other values; another length; back) on ONE handle, with and without
+    a gradient, give bitwise what a fresh handle gives, step records included."""
+    u0 = t(_lv_u0(2, 9))
+    p0 = t(np.random.default_rng(12).uniform(-0.3, 0.3, 240))
+    opt = kanode.Tsit5Options(abstol=1e-8, reltol=1e-7)
+    lists = [[0.1 * i for i in range(35)], [0.1 * i + 0.05 for i in range(35)], [0.0, 1.0, 3.5],
+             [0.1 * i for i in range(35)], [0.0, 1.0, 3.5]]
+
+    def run(rhs, ts, grad):
+        w = t(np.random.default_rng(len(ts)).normal(size=(len(ts), 2, 2)))
+        p = p0.clone().requires_grad_(grad)
+        sol = kanode.solve(rhs, u0, (0.0, 3.5), p, ts, opt, sensealg="interpolating_adjoint")
+        if not grad:
+            return sol.u.detach().cpu(), None, sol.stats["naccept"], None
+        (g,) = torch.autograd.grad((sol.u * w).sum(), [p])
+        return sol.u.detach().cpu(), g.cpu(), sol.stats["naccept"], sol.stats.get("dts")
+
+    shared = lv()
+    for grad in (False, True):
+        for ts in lists:
+            got, want = run(shared, ts, grad), run(lv(), ts, grad)
+            assert torch.equal(got[0], want[0]) and got[2] == want[2]
+            if grad:
+                assert torch.equal(got[1], want[1]) and got[3] == want[3]
+
+
 def test_fused_chain_solve_falls_back_when_dense_output_fills():
     """A dense output larger than the fused block (KANODE_OPT_FUSED_SOLVE_CAP) falls back to the
     host loop: same steps, same values, a usable dense output."""
